@@ -1,0 +1,308 @@
+// torch op registrations for the gfx950 kernels (namespace torch.ops.rfq_amd).
+//
+// Every op launches on the caller's current HIP stream, allocates nothing and
+// never synchronises, so whole decode steps can be captured into a hipGraph
+// (torch.cuda.CUDAGraph on ROCm) — cdna_hip_programming.md Guideline 9.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rfq {
+typedef uint16_t bf16_t;
+void launch_rms_norm(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
+void launch_fused_add_rms_norm(const bf16_t*, int64_t, bf16_t*, int64_t, const bf16_t*, bf16_t*,
+                               int64_t, int, int, float, hipStream_t);
+void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
+void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
+void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
+                    bf16_t*, int, int, int, int, hipStream_t);
+void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
+                        const int32_t*, bf16_t*, int64_t, float*, float*, int, int, int, float, int,
+                        hipStream_t);
+void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
+                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
+                         const int32_t*, int, bf16_t*, int64_t, int, int, float, hipStream_t);
+void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t*, int,
+                           const int32_t*, const float*, const uint64_t*, float*, int32_t*, int,
+                           hipStream_t);
+void launch_sample_final(const float*, const int32_t*, int, int, int, int32_t*, hipStream_t);
+void launch_moe_topk(const bf16_t*, int64_t, int, int, int, float*, int32_t*, bool, hipStream_t);
+void launch_moe_align(const int32_t*, int, int, int, int32_t*, int32_t*, int32_t*, int32_t*,
+                      int32_t*, int, int, hipStream_t);
+void launch_moe_gather(const bf16_t*, int64_t, const int32_t*, int, int, int, bf16_t*, hipStream_t);
+void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, const int32_t*,
+                             int, int, int, int, hipStream_t);
+void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
+                        int64_t, hipStream_t);
+}  // namespace rfq
+
+namespace {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_ROWMAJOR(t) TORCH_CHECK((t).dim() == 2 && (t).stride(1) == 1, #t " must be 2-D row-major")
+
+inline const rfq::bf16_t* bp(const Tensor& t) {
+  return reinterpret_cast<const rfq::bf16_t*>(t.data_ptr());
+}
+inline rfq::bf16_t* bpm(const Tensor& t) { return reinterpret_cast<rfq::bf16_t*>(t.data_ptr()); }
+
+void rms_norm(const Tensor& x, const Tensor& w, double eps, const Tensor& out) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d, "rms_norm: bad hidden size");
+  rfq::launch_rms_norm(bp(x), x.stride(0), bp(w), bpm(out), out.stride(0), x.size(0), d,
+                       (float)eps, cur_stream());
+}
+
+void fused_add_rms_norm(const Tensor& x, const Tensor& residual, const Tensor& w, double eps,
+                        const Tensor& out) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
+  const int d = x.size(1);
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && w.numel() == d && residual.size(1) == d,
+              "fused_add_rms_norm: bad hidden size");
+  TORCH_CHECK(residual.size(0) == x.size(0) && out.size(0) == x.size(0), "row mismatch");
+  rfq::launch_fused_add_rms_norm(bp(x), x.stride(0), bpm(residual), residual.stride(0), bp(w),
+                                 bpm(out), out.stride(0), x.size(0), d, (float)eps, cur_stream());
+}
+
+void silu_mul(const Tensor& gate_up, const Tensor& out) {
+  CHECK_DEV(gate_up); CHECK_BF16(gate_up); CHECK_BF16(out);
+  CHECK_ROWMAJOR(gate_up); CHECK_ROWMAJOR(out);
+  const int F = out.size(1);
+  TORCH_CHECK(gate_up.size(1) == 2 * F && F % 8 == 0 && out.size(0) == gate_up.size(0),
+              "silu_mul: shape mismatch");
+  rfq::launch_silu_mul(bp(gate_up), gate_up.stride(0), bpm(out), out.stride(0), out.size(0), F,
+                       cur_stream());
+}
+
+void embed(const Tensor& ids, const Tensor& table, const Tensor& out, int64_t vocab_start) {
+  CHECK_DEV(ids); CHECK_I32(ids); CHECK_BF16(table); CHECK_BF16(out);
+  TORCH_CHECK(table.is_contiguous() && out.is_contiguous(), "embed: contiguous tensors required");
+  const int d = table.size(1);
+  TORCH_CHECK(out.size(1) == d && out.size(0) == ids.numel() && d % 8 == 0, "embed: shape");
+  rfq::launch_embed(ids.data_ptr<int32_t>(), bp(table), bpm(out), ids.numel(), d,
+                    (int)vocab_start, (int)(vocab_start + table.size(0)), cur_stream());
+}
+
+void rope_kv(const Tensor& qkv, const Tensor& positions, const Tensor& cos_sin,
+             const Tensor& slot_mapping, const Tensor& k_cache, const Tensor& v_cache,
+             int64_t Hq, int64_t Hkv) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv); CHECK_ROWMAJOR(qkv);
+  CHECK_I32(positions); CHECK_I32(slot_mapping); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == 128,
+              "rope_kv: cos_sin must be fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == 128 &&
+                  k_cache.is_contiguous() && v_cache.is_contiguous(),
+              "rope_kv: cache must be [blocks, Hkv, BS, 128]");
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.size(1) >= (Hq + 2 * Hkv) * 128 && positions.numel() >= T &&
+                  slot_mapping.numel() >= T,
+              "rope_kv: shape mismatch");
+  rfq::launch_rope_kv(bpm(qkv), qkv.stride(0), positions.data_ptr<int32_t>(),
+                      cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int32_t>(), bpm(k_cache),
+                      bpm(v_cache), T, Hq, Hkv, k_cache.size(2), cur_stream());
+}
+
+void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                 const Tensor& block_tables, const Tensor& context_lens, const Tensor& out,
+                 const Tensor& part_o, const Tensor& part_ml, int64_t Hq, int64_t Hkv,
+                 double scale, int64_t num_splits) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_ROWMAJOR(block_tables);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 32 && k_cache.size(3) == 128 &&
+                  k_cache.size(1) == Hkv,
+              "attn_decode: cache must be [blocks, Hkv, 32, 128]");
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "attn_decode: GQA group must be <= 16");
+  const int B = out.size(0);
+  TORCH_CHECK(q.size(0) >= B && block_tables.size(0) >= B && context_lens.numel() >= B,
+              "attn_decode: batch mismatch");
+  TORCH_CHECK(num_splits >= 1 && num_splits <= 64, "attn_decode: num_splits in [1, 64]");
+  if (num_splits > 1) {
+    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
+                "partials must be fp32");
+    TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * num_splits * 128 &&
+                    part_ml.numel() >= (int64_t)B * Hq * num_splits * 2,
+                "attn_decode: partial buffers too small");
+  }
+  rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
+                          block_tables.data_ptr<int32_t>(), block_tables.stride(0),
+                          context_lens.data_ptr<int32_t>(), bpm(out), out.stride(0),
+                          part_o.data_ptr<float>(), part_ml.data_ptr<float>(), B, Hq, Hkv,
+                          (float)scale, num_splits, cur_stream());
+}
+
+void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                  const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
+                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_qblk,
+                  const Tensor& out, int64_t Hq, int64_t Hkv, double scale) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
+  CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
+  CHECK_I32(work_seq); CHECK_I32(work_qblk);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 32 && k_cache.size(3) == 128 &&
+                  k_cache.size(1) == Hkv,
+              "attn_prefill: cache must be [blocks, Hkv, 32, 128]");
+  TORCH_CHECK(Hq % Hkv == 0 && (Hq / Hkv) % 4 == 0, "attn_prefill: GQA group must be a multiple of 4");
+  TORCH_CHECK(work_seq.numel() == work_qblk.numel(), "work list mismatch");
+  rfq::launch_attn_prefill(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
+                           block_tables.data_ptr<int32_t>(), block_tables.stride(0),
+                           seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
+                           seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(),
+                           work_qblk.data_ptr<int32_t>(), work_seq.numel(), bpm(out),
+                           out.stride(0), Hq, Hkv, (float)scale, cur_stream());
+}
+
+void sample_partial(const Tensor& logits, int64_t v0, const Tensor& mask_table,
+                    const Tensor& mask_idx, const Tensor& temps, const Tensor& seeds,
+                    const Tensor& part_val, const Tensor& part_idx) {
+  CHECK_DEV(logits); CHECK_BF16(logits); CHECK_ROWMAJOR(logits);
+  TORCH_CHECK(mask_table.scalar_type() == at::kInt && mask_table.dim() == 2 &&
+                  mask_table.is_contiguous(),
+              "mask_table must be int32 [n_masks, words]");
+  CHECK_I32(mask_idx);
+  TORCH_CHECK(temps.scalar_type() == at::kFloat, "temps must be fp32");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong, "seeds must be int64");
+  TORCH_CHECK(part_val.dim() == 2 && part_idx.dim() == 2, "partials must be [B, splits]");
+  const int B = part_val.size(0), nsplit = part_val.size(1);
+  const int Vl = logits.size(1);
+  TORCH_CHECK(Vl % 8 == 0 && v0 % 8 == 0, "vocab shard must be 8-aligned");
+  TORCH_CHECK(logits.size(0) >= B && mask_idx.numel() >= B && temps.numel() >= B &&
+                  seeds.numel() >= B,
+              "sample_partial: batch mismatch");
+  TORCH_CHECK((v0 + Vl + 31) / 32 <= mask_table.size(1), "mask table too narrow");
+  rfq::launch_sample_partial(bp(logits), logits.stride(0), B, Vl, v0,
+                             reinterpret_cast<const uint32_t*>(mask_table.data_ptr<int32_t>()),
+                             mask_table.size(1), mask_idx.data_ptr<int32_t>(),
+                             temps.data_ptr<float>(),
+                             reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()),
+                             part_val.data_ptr<float>(), part_idx.data_ptr<int32_t>(), nsplit,
+                             cur_stream());
+}
+
+// part_val/part_idx: [groups, B, n] (groups = TP ranks after all-gather, or 1)
+void sample_final(const Tensor& part_val, const Tensor& part_idx, const Tensor& out) {
+  CHECK_DEV(part_val); CHECK_I32(part_idx); CHECK_I32(out);
+  TORCH_CHECK(part_val.dim() == 3 && part_val.is_contiguous() && part_idx.is_contiguous(),
+              "partials must be contiguous [groups, B, n]");
+  const int groups = part_val.size(0), B = part_val.size(1), n = part_val.size(2);
+  TORCH_CHECK(out.numel() >= B, "out too small");
+  rfq::launch_sample_final(part_val.data_ptr<float>(), part_idx.data_ptr<int32_t>(), B, n, groups,
+                           out.data_ptr<int32_t>(), cur_stream());
+}
+
+void moe_topk(const Tensor& router_logits, int64_t topk, bool renorm, const Tensor& weights,
+              const Tensor& ids) {
+  CHECK_DEV(router_logits); CHECK_BF16(router_logits); CHECK_ROWMAJOR(router_logits);
+  TORCH_CHECK(weights.scalar_type() == at::kFloat && ids.scalar_type() == at::kInt, "topk outputs");
+  const int T = router_logits.size(0), E = router_logits.size(1);
+  TORCH_CHECK(E <= 64 && topk <= 8, "moe_topk: E <= 64, k <= 8");
+  rfq::launch_moe_topk(bp(router_logits), router_logits.stride(0), T, E, topk,
+                       weights.data_ptr<float>(), ids.data_ptr<int32_t>(), renorm, cur_stream());
+}
+
+// Sort (token, k) pairs by expert, pad each expert's segment to a multiple of
+// `block_m`.  Outputs: sorted_ids [max_padded] (token*k+slot, or -1 padding),
+// expert_of_block [max_blocks], expert_offsets [E+1], num_blocks [1].
+void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
+               const Tensor& inv_pos, const Tensor& expert_of_block,
+               const Tensor& expert_offsets, const Tensor& num_blocks) {
+  CHECK_DEV(topk_ids); CHECK_I32(topk_ids); CHECK_I32(sorted_ids); CHECK_I32(expert_of_block);
+  CHECK_I32(expert_offsets); CHECK_I32(num_blocks); CHECK_I32(inv_pos);
+  TORCH_CHECK(E <= 64 && expert_offsets.numel() >= E + 1, "moe_align: E <= 64");
+  TORCH_CHECK(inv_pos.numel() >= topk_ids.numel(), "moe_align: inv_pos too small");
+  const int64_t need = topk_ids.numel() + E * (block_m - 1);
+  TORCH_CHECK(sorted_ids.numel() >= need && expert_of_block.numel() * block_m >= need,
+              "moe_align: output buffers too small");
+  rfq::launch_moe_align(topk_ids.data_ptr<int32_t>(), topk_ids.numel(), E, block_m,
+                        sorted_ids.data_ptr<int32_t>(), inv_pos.data_ptr<int32_t>(),
+                        expert_of_block.data_ptr<int32_t>(), expert_offsets.data_ptr<int32_t>(),
+                        num_blocks.data_ptr<int32_t>(), sorted_ids.numel(),
+                        expert_of_block.numel(), cur_stream());
+}
+
+void moe_gather(const Tensor& x, const Tensor& sorted_ids, int64_t topk, const Tensor& out) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_I32(sorted_ids); CHECK_BF16(out);
+  TORCH_CHECK(out.is_contiguous() && out.size(0) >= sorted_ids.numel() && out.size(1) == x.size(1),
+              "moe_gather: out shape");
+  rfq::launch_moe_gather(bp(x), x.stride(0), sorted_ids.data_ptr<int32_t>(), sorted_ids.numel(),
+                         x.size(1), topk, bpm(out), cur_stream());
+}
+
+// out[rows, N] = x[rows, K] @ w[e]^T for row blocks of 128 owned by expert e.
+void moe_grouped_gemm(const Tensor& x, const Tensor& w, const Tensor& out,
+                      const Tensor& expert_of_block, const Tensor& num_blocks) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
+  const int E = w.size(0), N = w.size(1), K = w.size(2);
+  TORCH_CHECK(x.size(1) == K && out.size(1) == N && out.size(0) == x.size(0), "moe gemm shape");
+  TORCH_CHECK(K % 64 == 0 && N % 128 == 0, "moe gemm: K % 64, N % 128");
+  TORCH_CHECK(x.size(0) % 128 == 0, "moe gemm: rows must be padded to 128");
+  rfq::launch_moe_grouped_gemm(bp(x), bp(w), bpm(out), expert_of_block.data_ptr<int32_t>(),
+                               num_blocks.data_ptr<int32_t>(), x.size(0) / 128, N, K, E,
+                               cur_stream());
+}
+
+// out[t] = sum_k weights[t,k] * y[pos of (t,k)]
+void moe_combine(const Tensor& y, const Tensor& inv_pos, const Tensor& weights, int64_t topk,
+                 const Tensor& out) {
+  CHECK_DEV(y); CHECK_BF16(y); CHECK_I32(inv_pos); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(weights.scalar_type() == at::kFloat, "weights fp32");
+  const int T = out.size(0), d = out.size(1);
+  rfq::launch_moe_combine(bp(y), inv_pos.data_ptr<int32_t>(), weights.data_ptr<float>(), T,
+                          topk, d, bpm(out), out.stride(0), cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(rfq_amd, m) {
+  m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()");
+  m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
+  m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
+  m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start) -> ()");
+  m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()");
+  m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor context_lens, Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, "
+        "int Hkv, float scale, int num_splits) -> ()");
+  m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
+        "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale) -> ()");
+  m.def("sample_partial(Tensor logits, int v0, Tensor mask_table, Tensor mask_idx, Tensor temps, "
+        "Tensor seeds, Tensor(a!) part_val, Tensor(b!) part_idx) -> ()");
+  m.def("sample_final(Tensor part_val, Tensor part_idx, Tensor(a!) out) -> ()");
+  m.def("moe_topk(Tensor router_logits, int topk, bool renorm, Tensor(a!) weights, Tensor(b!) ids) -> ()");
+  m.def("moe_align(Tensor topk_ids, int E, int block_m, Tensor(a!) sorted_ids, Tensor(b!) inv_pos, "
+        "Tensor(c!) expert_of_block, Tensor(d!) expert_offsets, Tensor(e!) num_blocks) -> ()");
+  m.def("moe_gather(Tensor x, Tensor sorted_ids, int topk, Tensor(a!) out) -> ()");
+  m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
+        "Tensor num_blocks) -> ()");
+  m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
+  m.impl("rms_norm", &rms_norm);
+  m.impl("fused_add_rms_norm", &fused_add_rms_norm);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("embed", &embed);
+  m.impl("rope_kv", &rope_kv);
+  m.impl("attn_decode", &attn_decode);
+  m.impl("attn_prefill", &attn_prefill);
+  m.impl("sample_partial", &sample_partial);
+  m.impl("sample_final", &sample_final);
+  m.impl("moe_topk", &moe_topk);
+  m.impl("moe_align", &moe_align);
+  m.impl("moe_gather", &moe_gather);
+  m.impl("moe_grouped_gemm", &moe_grouped_gemm);
+  m.impl("moe_combine", &moe_combine);
+}

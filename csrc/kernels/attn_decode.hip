@@ -1,0 +1,215 @@
+// Paged decode attention (q_len = 1 per sequence), GQA, split-K over the context.
+// SURVEY.md §2.4 K7 — the bandwidth-critical kernel of a large-batch decode step.
+//
+// Design (gfx950, wave64):
+//   * one wave per (split, kv_head, sequence); the G query heads that share a kv
+//     head are the N=16 dimension of mfma_f32_16x16x32_bf16 (G <= 16), so each K/V
+//     byte is read exactly once per kv head.
+//   * QK^T is computed swapped, S^T = K * Q^T: K fragments are 16-byte rows loaded
+//     straight from the page into VGPRs (no LDS round trip; Guideline "GEMV / M<=16").
+//     The result has one head per lane column, so the online-softmax state (running
+//     max, partial sum) is lane-local for its head.
+//   * P*V is computed as O^T = V^T * P^T: the S^T accumulators are converted in
+//     place into the bf16 B operand (accumulator-as-operand, §3), V goes through LDS
+//     once and is read back with ds_read_b64_tr_b16 (T10) in the permuted key order
+//     the accumulator layout implies.  O^T keeps the head on the lane, so the
+//     softmax rescale needs no cross-lane traffic.
+//   * V's LDS image is XOR-swizzled (chunk ^ ((row&7)<<1)) so every transposed read
+//     of a 32-lane half touches 16 distinct 16-byte slots (conflict-free).
+//   * split-K partials (unnormalised O, running max, sum) are merged by
+//     attn_decode_reduce; with one split the kernel writes bf16 output directly.
+//   The split size is derived per sequence from its context length on device, so a
+//   hipGraph captured with a fixed split count stays balanced as contexts grow.
+#include "common.h"
+
+namespace rfq {
+
+constexpr int kD = 128;
+constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
+
+__global__ __launch_bounds__(64) void attn_decode_kernel(
+    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
+    int bt_stride, const int32_t* __restrict__ context_lens, bf16_t* __restrict__ out,
+    int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int Hq,
+    int Hkv, float scale_log2, int num_splits) {
+  __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int g = lane >> 4;   // 16-lane group
+  const int c = lane & 15;   // head column within the GQA group
+  const int G = Hq / Hkv;
+  const int h = kvh * G + c;
+  const bool hvalid = c < G;
+
+  const int ctx = context_lens[b];
+  int tps = (ctx + num_splits - 1) / num_splits;
+  tps = (tps + kPage - 1) / kPage * kPage;
+  const int start = split * tps;
+  const int end = min(ctx, start + tps);
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) o[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (start < end) {
+    // Q^T fragments: B[k = dh][col = head]; lane holds Q[h][32ks + 8g .. +7]
+    s16x8 qf[4];
+    const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(hvalid ? h : kvh * G) * kD;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qf[ks] = reinterpret_cast<const s16x8*>(qrow + 32 * ks + 8 * g)[0];
+      if (!hvalid) qf[ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    const int32_t* bt = block_tables + (int64_t)b * bt_stride;
+
+    for (int kt = start; kt < end; kt += kPage) {
+      const int64_t page = bt[kt / kPage];
+      const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
+      const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
+      const int nvalid = end - kt;  // keys of this tile that exist (>= 1)
+
+      // ---- issue K fragment loads (A operand: row = key, k = dh) ----
+      s16x8 kf[2][4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          kf[mt][ks] = reinterpret_cast<const s16x8*>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g)[0];
+
+      // ---- V tile -> LDS (swizzled), rows past the context zeroed ----
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = g + 4 * i, ch = c;
+        s16x8 v = reinterpret_cast<const s16x8*>(vb + row * kD)[ch];
+        if (row >= nvalid) v = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        const int pch = ch ^ ((row & 7) << 1);
+        reinterpret_cast<s16x8*>(v_lds + row * kD)[pch] = v;
+      }
+
+      // ---- S^T = K Q^T ----
+      f32x4 s[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        s[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[mt][ks]), as_bf16x8(qf[ks]),
+                                                          s[mt], 0, 0, 0);
+      }
+      // lane holds S^T[key = 16mt + 4g + i][head c]
+      float mx = -INFINITY;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = 16 * mt + 4 * g + i;
+          float v = s[mt][i] * scale_log2;
+          if (key >= nvalid) v = -INFINITY;
+          s[mt][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - m_new);
+      float psum = 0.f;
+      float p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        p[j] = fast_exp2(s[j >> 2][j & 3] - m_new);
+        psum += p[j];
+      }
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) o[m] *= alpha;
+      // P^T as B operand: element j <-> key pi(g,j) = (j<4 ? 4g+j : 16+4g+j-4)
+      s16x8 pb = pack8(p);
+
+      __syncthreads();  // V tile visible (single wave: orders the LDS writes)
+
+      // ---- O^T += V^T P^T ----
+      const int q4 = c >> 2, p4 = c & 3;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int r0 = 4 * g + q4, r1 = 16 + 4 * g + q4;
+        const int ch = 2 * m + (p4 >> 1), sub = (p4 & 1) * 4;
+        const s16x4 a0 = ds_read_tr16(v_lds + r0 * kD + ((ch ^ ((r0 & 7) << 1)) * 8) + sub);
+        const s16x4 a1 = ds_read_tr16(v_lds + r1 * kD + ((ch ^ ((r1 & 7) << 1)) * 8) + sub);
+        const s16x8 a = (s16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        o[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb), o[m], 0, 0, 0);
+      }
+      __syncthreads();  // before the next tile overwrites v_lds
+    }
+  }
+
+  // total softmax denominator for head c (lanes c, c+16, c+32, c+48)
+  float l_tot = l_run;
+  l_tot += __shfl_xor(l_tot, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (!hvalid) return;
+
+  if (num_splits == 1) {
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    bf16_t* orow = out + (int64_t)b * out_stride + (int64_t)h * kD;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      uint2 w;
+      w.x = pack_bf16x2(o[m][0] * inv, o[m][1] * inv);
+      w.y = pack_bf16x2(o[m][2] * inv, o[m][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = w;
+    }
+  } else {
+    const int64_t pidx = ((int64_t)b * Hq + h) * num_splits + split;
+    float* po = part_o + pidx * kD;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[m];
+    if (g == 0) {
+      part_ml[pidx * 2 + 0] = m_run;
+      part_ml[pidx * 2 + 1] = l_tot;
+    }
+  }
+}
+
+// Merge split-K partials: one workgroup of 128 lanes (one per dh) per (seq, head).
+__global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
+    const float* __restrict__ part_o, const float* __restrict__ part_ml,
+    bf16_t* __restrict__ out, int64_t out_stride, int Hq, int num_splits) {
+  const int bh = blockIdx.x;
+  const int b = bh / Hq, h = bh % Hq;
+  const int d = threadIdx.x;
+  const float* ml = part_ml + (int64_t)bh * num_splits * 2;
+  float gm = -INFINITY;
+  for (int s = 0; s < num_splits; ++s) gm = fmaxf(gm, ml[2 * s]);
+  float num = 0.f, den = 0.f;
+  if (gm != -INFINITY) {
+    for (int s = 0; s < num_splits; ++s) {
+      const float ms = ml[2 * s];
+      if (ms == -INFINITY) continue;
+      const float w = fast_exp2(ms - gm);
+      num += w * part_o[((int64_t)bh * num_splits + s) * kD + d];
+      den += w * ml[2 * s + 1];
+    }
+  }
+  out[(int64_t)b * out_stride + (int64_t)h * kD + d] = f2bf(den > 0.f ? num / den : 0.f);
+}
+
+void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
+                        const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
+                        const int32_t* context_lens, bf16_t* out, int64_t out_stride,
+                        float* part_o, float* part_ml, int B, int Hq, int Hkv, float scale,
+                        int num_splits, hipStream_t s) {
+  if (B == 0) return;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(num_splits, Hkv, B);
+  attn_decode_kernel<<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables, bt_stride,
+                                         context_lens, out, out_stride, part_o, part_ml, Hq, Hkv,
+                                         scale_log2, num_splits);
+  if (num_splits > 1)
+    attn_decode_reduce_kernel<<<B * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
+                                                     num_splits);
+}
+
+}  // namespace rfq

@@ -1,0 +1,100 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+//
+// Everything here is written for wave64 and the gfx950 MFMA/LDS instruction set;
+// there is no portability layer.  bf16 tensors are carried as raw uint16 bits and
+// moved in 16-byte vectors (8 x bf16) — scalar bf16 traffic is ~2x slower on CDNA
+// (cdna_hip_programming.md, Guideline 13).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace rfq {
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;                                            // raw bf16 bits
+typedef short s16x8 __attribute__((ext_vector_type(8)));            // 8 x bf16 bits (16 B)
+typedef short s16x4 __attribute__((ext_vector_type(4)));            // 4 x bf16 bits (8 B)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));          // MFMA operand
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t x) {
+  return __uint_as_float(((uint32_t)x) << 16);
+}
+__device__ __forceinline__ float bf2f_s(short x) { return bf2f((bf16_t)x); }
+
+// Round-to-nearest-even f32 -> bf16 (lowers to v_cvt_pk_bf16_f32 on gfx950).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const s16x8& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = bf2f_s(v[i]);
+}
+
+__device__ __forceinline__ s16x8 pack8(const float* f) {
+  s16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(f[i]);
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(const s16x8& v) {
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Wave64 reductions via cross-lane shuffles.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64).  `scratch` >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = (lane < nw) ? scratch[lane] : 0.f;
+  t = wave_sum(t);
+  __syncthreads();
+  return t;
+}
+
+// Fast exp2 (v_exp_f32).
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Transposed LDS read: per 16-lane group, 4 rows x 16 cols of 16-bit data, lane i
+// receives column i (row q in element q).  Lane 4q+p supplies &tile[row q][col 4p].
+__device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(lds_ptr));
+}
+
+// Counter-based RNG (splitmix/murmur style finaliser) — deterministic per
+// (seed, row, column), identical on every TP rank for the same global column.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint32_t a, uint32_t b) {
+  uint64_t x = seed ^ (((uint64_t)a << 32) | b);
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+}  // namespace rfq

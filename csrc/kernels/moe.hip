@@ -1,0 +1,279 @@
+// Mixture-of-experts kernels for Mixtral-8x7B (BASELINE config 5; SURVEY.md
+// §2.4 K15-K18): router top-k, expert alignment (sort + pad), row gather,
+// MFMA grouped GEMM, weighted combine.
+//
+// Flow per MoE layer (T tokens, top-k, E experts):
+//   router_logits[T,E] --moe_topk--> (w[T,k], id[T,k])
+//   --moe_align--> sorted_ids[P] (pair index t*k+j or -1), inv_pos[T*k],
+//                  expert_of_block[P/128], num_blocks
+//   --moe_gather--> xs[P, d]            (rows grouped by expert, padded to 128)
+//   --grouped_gemm(w13)--> [P, 2F] --silu_mul--> [P, F] --grouped_gemm(w2)--> y[P, d]
+//   --moe_combine--> out[T, d] = sum_j w[t,j] * y[inv_pos[t*k+j]]
+// Every buffer is sized by the host from upper bounds and the GEMM reads the
+// live block count from device memory, so the whole chain is graph-capturable.
+#include "common.h"
+
+namespace rfq {
+
+// ---------------------------------------------------------------- router top-k
+__global__ void moe_topk_kernel(const bf16_t* __restrict__ logits, int64_t stride, int T, int E,
+                                int k, float* __restrict__ w_out, int32_t* __restrict__ id_out,
+                                bool renorm) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  float l[64];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    l[e] = bf2f(logits[(int64_t)t * stride + e]);
+    mx = fmaxf(mx, l[e]);
+  }
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) den += __expf(l[e] - mx);
+  uint64_t taken = 0;
+  float sel_sum = 0.f;
+  float wv[8];
+  int iv[8];
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((taken >> e) & 1ull) && (best < 0 || l[e] > bv)) { bv = l[e]; best = e; }
+    taken |= 1ull << best;
+    wv[j] = __expf(bv - mx) / den;
+    iv[j] = best;
+    sel_sum += wv[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    w_out[(int64_t)t * k + j] = renorm ? wv[j] / sel_sum : wv[j];
+    id_out[(int64_t)t * k + j] = iv[j];
+  }
+}
+
+// ------------------------------------------------------------ align (one block)
+// Counting sort of the T*k (token, slot) pairs by expert; each expert segment is
+// padded to a multiple of block_m with -1 entries.
+__global__ __launch_bounds__(1024) void moe_align_kernel(
+    const int32_t* __restrict__ ids, int n, int E, int block_m, int32_t* __restrict__ sorted_ids,
+    int32_t* __restrict__ inv_pos, int32_t* __restrict__ expert_of_block,
+    int32_t* __restrict__ expert_offsets, int32_t* __restrict__ num_blocks, int cap,
+    int block_cap) {
+  __shared__ int cnt[64];
+  __shared__ int off[65];
+  __shared__ int cursor[64];
+  for (int e = threadIdx.x; e < 64; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[ids[i]], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      off[e] = acc;
+      cursor[e] = acc;
+      acc += (cnt[e] + block_m - 1) / block_m * block_m;
+    }
+    off[E] = acc;
+    *num_blocks = acc / block_m;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e <= E; e += blockDim.x) expert_offsets[e] = off[e];
+  const int total = off[E];
+  for (int i = threadIdx.x; i < cap; i += blockDim.x) sorted_ids[i] = -1;
+  for (int bi = threadIdx.x; bi < block_cap; bi += blockDim.x) {
+    int e_of = -1;
+    const int r = bi * block_m;
+    if (r < total)
+      for (int e = 0; e < E; ++e)
+        if (r >= off[e] && r < off[e + 1]) e_of = e;
+    expert_of_block[bi] = e_of;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int p = atomicAdd(&cursor[ids[i]], 1);
+    sorted_ids[p] = i;
+    inv_pos[i] = p;
+  }
+}
+
+// ------------------------------------------------------------------- gather
+__global__ __launch_bounds__(256) void moe_gather_kernel(const bf16_t* __restrict__ x,
+                                                         int64_t x_stride,
+                                                         const int32_t* __restrict__ sorted_ids,
+                                                         int P, int d, int topk,
+                                                         bf16_t* __restrict__ out) {
+  const int cpr = d >> 3;
+  const int64_t total = (int64_t)P * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cpr;
+    const int c = (int)(i - r * cpr);
+    const int sid = sorted_ids[r];
+    s16x8 v = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    if (sid >= 0) v = reinterpret_cast<const s16x8*>(x + (int64_t)(sid / topk) * x_stride)[c];
+    reinterpret_cast<s16x8*>(out + r * d)[c] = v;
+  }
+}
+
+// --------------------------------------------------------------- grouped GEMM
+// out[r, n] = sum_k x[r, k] * w[e(r), n, k]   (x: [P, K], w: [E, N, K] row-major)
+// Tile 128x128, K-step 64, 4 waves each owning a 64x64 quadrant as 2x2
+// mfma_f32_32x32x16_bf16 accumulators.  Both operands are K-contiguous, so the
+// LDS images are [128 rows][64 k] with 128-B rows; chunk ch of row r lives at
+// ch ^ ((r >> 1) & 7), which makes the 16-lane ds_read_b128 groups hit 16
+// distinct 16-B slots (T2).  Register-staged double buffering: the next K-tile's
+// global loads are issued before the current tile's MFMAs (T14).
+constexpr int kBM = 128, kBN = 128, kBK = 64;
+
+__device__ __forceinline__ int swz64(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(256) void moe_grouped_gemm_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+    const int32_t* __restrict__ expert_of_block, const int32_t* __restrict__ num_blocks, int N,
+    int K) {
+  __shared__ __attribute__((aligned(16))) bf16_t a_lds[kBM * kBK];
+  __shared__ __attribute__((aligned(16))) bf16_t b_lds[kBN * kBK];
+  const int ntn = N / kBN;
+  const int rb = blockIdx.x / ntn, cn = blockIdx.x % ntn;
+  if (rb >= *num_blocks) return;
+  const int e = expert_of_block[rb];
+  if (e < 0) return;
+  const bf16_t* xa = x + (int64_t)rb * kBM * K;
+  const bf16_t* wb = w + ((int64_t)e * N + (int64_t)cn * kBN) * K;
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h2 = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;  // quadrant
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  // staging: 128 rows x 8 chunks = 1024 chunks per operand, 4 per thread
+  s16x8 ra[4], rbv[4];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7;
+      ra[i] = reinterpret_cast<const s16x8*>(xa + (int64_t)row * K + k0)[ch];
+      rbv[i] = reinterpret_cast<const s16x8*>(wb + (int64_t)row * K + k0)[ch];
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7;
+      reinterpret_cast<s16x8*>(a_lds + row * kBK)[swz64(row, ch)] = ra[i];
+      reinterpret_cast<s16x8*>(b_lds + row * kBK)[swz64(row, ch)] = rbv[i];
+    }
+  };
+
+  load_tile(0);
+  for (int k0 = 0; k0 < K; k0 += kBK) {
+    store_tile();
+    __syncthreads();
+    if (k0 + kBK < K) load_tile(k0 + kBK);  // in flight under the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      s16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + r;
+        af[i] = reinterpret_cast<const s16x8*>(a_lds + row * kBK)[swz64(row, 2 * ks + h2)];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 64 + j * 32 + r;
+        bfr[j] = reinterpret_cast<const s16x8*>(b_lds + row * kBK)[swz64(row, 2 * ks + h2)];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(af[i]), as_bf16x8(bfr[j]),
+                                                              acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // C layout: col = lane & 31, row = (q&3) + 8(q>>2) + 4*h2
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = rb * kBM + wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h2;
+        const int col = cn * kBN + wn * 64 + j * 32 + r;
+        out[(int64_t)row * N + col] = f2bf(acc[i][j][q]);
+      }
+}
+
+// ------------------------------------------------------------------ combine
+__global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ y,
+                                                          const int32_t* __restrict__ inv_pos,
+                                                          const float* __restrict__ wts, int T,
+                                                          int k, int d, bf16_t* __restrict__ out,
+                                                          int64_t out_stride) {
+  const int cpr = d >> 3;
+  const int64_t total = (int64_t)T * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / cpr;
+    const int c = (int)(i - t * cpr);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = wts[t * k + j];
+      const int p = inv_pos[t * k + j];
+      float v[8];
+      unpack8(reinterpret_cast<const s16x8*>(y + (int64_t)p * d)[c], v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+    }
+    reinterpret_cast<s16x8*>(out + t * out_stride)[c] = pack8(acc);
+  }
+}
+
+static inline int moe_stream_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+void launch_moe_topk(const bf16_t* logits, int64_t stride, int T, int E, int k, float* w,
+                     int32_t* ids, bool renorm, hipStream_t s) {
+  if (T == 0) return;
+  moe_topk_kernel<<<(T + 127) / 128, 128, 0, s>>>(logits, stride, T, E, k, w, ids, renorm);
+}
+
+void launch_moe_align(const int32_t* ids, int n, int E, int block_m, int32_t* sorted_ids,
+                      int32_t* inv_pos, int32_t* expert_of_block, int32_t* expert_offsets,
+                      int32_t* num_blocks, int cap, int block_cap, hipStream_t s) {
+  moe_align_kernel<<<1, 1024, 0, s>>>(ids, n, E, block_m, sorted_ids, inv_pos, expert_of_block,
+                                      expert_offsets, num_blocks, cap, block_cap);
+}
+
+void launch_moe_gather(const bf16_t* x, int64_t x_stride, const int32_t* sorted_ids, int P,
+                         int d, int topk, bf16_t* out, hipStream_t s) {
+  if (P == 0) return;
+  moe_gather_kernel<<<moe_stream_grid((int64_t)P * (d >> 3)), 256, 0, s>>>(x, x_stride, sorted_ids,
+                                                                          P, d, topk, out);
+}
+
+void launch_moe_grouped_gemm(const bf16_t* x, const bf16_t* w, bf16_t* out,
+                             const int32_t* expert_of_block, const int32_t* num_blocks,
+                             int max_blocks, int N, int K, int E, hipStream_t s) {
+  if (max_blocks == 0) return;
+  (void)E;
+  moe_grouped_gemm_kernel<<<max_blocks * (N / kBN), 256, 0, s>>>(x, w, out, expert_of_block,
+                                                                  num_blocks, N, K);
+}
+
+void launch_moe_combine(const bf16_t* y, const int32_t* inv_pos, const float* w, int T, int k,
+                        int d, bf16_t* out, int64_t out_stride, hipStream_t s) {
+  if (T == 0) return;
+  moe_combine_kernel<<<moe_stream_grid((int64_t)T * (d >> 3)), 256, 0, s>>>(y, inv_pos, w, T, k, d,
+                                                                          out, out_stride);
+}
+
+}  // namespace rfq

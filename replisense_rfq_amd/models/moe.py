@@ -1,0 +1,90 @@
+"""Mixtral sparse-MoE MLP on the gfx950 kernels (BASELINE.json config 5).
+
+The routed computation runs entirely in hand-written kernels
+(``csrc/kernels/moe.hip``): top-2 router softmax, counting-sort alignment of the
+(token, slot) pairs into 128-row expert blocks, row gather, MFMA grouped GEMM for
+the fused w1|w3 projection, SwiGLU, grouped GEMM for w2 and the weighted combine.
+Buffers are sized from upper bounds once per batch size so the chain can be
+captured into a hipGraph.  On CPU the torch oracle (:func:`ops.reference.moe_forward`)
+is used instead.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+
+BLOCK_M = 128
+
+
+@dataclass
+class MoEBuffers:
+    max_tokens: int
+    topk: int
+    E: int
+    weights: torch.Tensor
+    ids: torch.Tensor
+    sorted_ids: torch.Tensor
+    inv_pos: torch.Tensor
+    expert_of_block: torch.Tensor
+    expert_offsets: torch.Tensor
+    num_blocks: torch.Tensor
+    xs: torch.Tensor
+    h13: torch.Tensor
+    act: torch.Tensor
+    y: torch.Tensor
+
+    @classmethod
+    def allocate(cls, max_tokens: int, topk: int, E: int, d: int, F: int, device,
+                 dtype=torch.bfloat16) -> "MoEBuffers":
+        n = max_tokens * topk
+        cap = n + E * (BLOCK_M - 1)
+        cap = (cap + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+        nb = cap // BLOCK_M
+        i32 = dict(dtype=torch.int32, device=device)
+        return cls(
+            max_tokens=max_tokens, topk=topk, E=E,
+            weights=torch.empty(max_tokens, topk, dtype=torch.float32, device=device),
+            ids=torch.empty(max_tokens, topk, **i32),
+            sorted_ids=torch.empty(cap, **i32),
+            inv_pos=torch.empty(n, **i32),
+            expert_of_block=torch.empty(nb, **i32),
+            expert_offsets=torch.empty(E + 1, **i32),
+            num_blocks=torch.empty(1, **i32),
+            xs=torch.empty(cap, d, dtype=dtype, device=device),
+            h13=torch.empty(cap, 2 * F, dtype=dtype, device=device),
+            act=torch.empty(cap, F, dtype=dtype, device=device),
+            y=torch.empty(cap, d, dtype=dtype, device=device),
+        )
+
+
+def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
+            topk: int, bufs: MoEBuffers | None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """x [T, d] -> [T, d].  w13 [E, 2F, d] (gate|up), w2 [E, d, F], router_w [E, d]."""
+    T = x.shape[0]
+    logits = x @ router_w.t()
+    if not x.is_cuda:
+        return ref.moe_forward(x, w13, w2, logits, topk)
+    E = w13.shape[0]
+    assert bufs is not None and T <= bufs.max_tokens
+    out = torch.empty_like(x) if out is None else out
+    # buffers are sliced to this step's token count but keep their capacity-based
+    # padding so the grouped GEMM grid is fixed for a given bucket
+    n = T * topk
+    cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+    nb = cap // BLOCK_M
+    w, ids = bufs.weights[:T], bufs.ids[:T]
+    ops.moe_topk(logits, topk, True, w, ids)
+    sorted_ids, eob = bufs.sorted_ids[:cap], bufs.expert_of_block[:nb]
+    ops.moe_align(ids, E, BLOCK_M, sorted_ids, bufs.inv_pos[:n], eob, bufs.expert_offsets,
+                  bufs.num_blocks)
+    xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
+    ops.moe_gather(x, sorted_ids, topk, xs)
+    ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks)
+    ops.silu_mul(h13, act)
+    ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks)
+    ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
+    return out

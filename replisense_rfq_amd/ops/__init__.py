@@ -1,0 +1,147 @@
+"""Device ops: thin dispatch from tensor device to the gfx950 kernel or the torch oracle.
+
+GPU tensors always go to ``torch.ops.rfq_amd.*`` (hand-written HIP kernels in
+``csrc/kernels``); the library is loaded on first use and a GPU call fails loudly
+if it cannot be.  CPU tensors use :mod:`.reference` (tests / CPU engine).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+from . import reference as ref
+
+__all__ = [
+    "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
+    "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
+    "moe_combine", "native_available",
+]
+
+
+def native_available() -> bool:
+    return _native.available()
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def rms_norm(x, w, eps, out=None):
+    out = torch.empty_like(x) if out is None else out
+    if _gpu(x):
+        _native.ops().rms_norm(x, w, eps, out)
+    else:
+        ref.rms_norm(x, w, eps, out)
+    return out
+
+
+def fused_add_rms_norm(x, residual, w, eps, out=None):
+    """residual <- x + residual ; out <- rmsnorm(residual) * w  (out may alias x)."""
+    out = torch.empty_like(x) if out is None else out
+    if _gpu(x):
+        _native.ops().fused_add_rms_norm(x, residual, w, eps, out)
+    else:
+        ref.fused_add_rms_norm(x, residual, w, eps, out)
+    return out
+
+
+def silu_mul(gate_up, out=None):
+    F = gate_up.shape[1] // 2
+    out = torch.empty((gate_up.shape[0], F), dtype=gate_up.dtype, device=gate_up.device) \
+        if out is None else out
+    if _gpu(gate_up):
+        _native.ops().silu_mul(gate_up, out)
+    else:
+        ref.silu_mul(gate_up, out)
+    return out
+
+
+def embed(ids, table, out=None, vocab_start: int = 0):
+    out = torch.empty((ids.numel(), table.shape[1]), dtype=table.dtype, device=table.device) \
+        if out is None else out
+    if _gpu(table):
+        _native.ops().embed(ids, table, out, vocab_start)
+    else:
+        ref.embed(ids, table, out, vocab_start)
+    return out
+
+
+def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
+    if _gpu(qkv):
+        _native.ops().rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
+    else:
+        ref.rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
+                Hq, Hkv, scale, num_splits=1):
+    if _gpu(q):
+        _native.ops().attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o,
+                                  part_ml, Hq, Hkv, scale, num_splits)
+    else:
+        ref.attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
+                        Hq, Hkv, scale, num_splits)
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
+                 work_seq, work_qblk, out, Hq, Hkv, scale):
+    if _gpu(q):
+        _native.ops().attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len,
+                                   seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale)
+    else:
+        ref.attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
+                         work_seq, work_qblk, out, Hq, Hkv, scale)
+
+
+def sample_partial(logits, v0, mask_table, mask_idx, temps, seeds, part_val, part_idx):
+    """GPU-only first stage (per-shard (val, idx) partials)."""
+    _native.ops().sample_partial(logits, v0, mask_table, mask_idx, temps, seeds, part_val,
+                                 part_idx)
+
+
+def sample_final(part_val, part_idx, out):
+    _native.ops().sample_final(part_val, part_idx, out)
+
+
+def sample(logits, mask_table, mask_idx, temps, seeds, v0=0, nsplit=8, out=None):
+    """Single-device grammar-masked Gumbel-max sampling -> int32 token ids [B]."""
+    B = logits.shape[0]
+    if _gpu(logits):
+        pv = torch.empty((1, B, nsplit), dtype=torch.float32, device=logits.device)
+        pi = torch.empty((1, B, nsplit), dtype=torch.int32, device=logits.device)
+        out = torch.empty(B, dtype=torch.int32, device=logits.device) if out is None else out
+        sample_partial(logits, v0, mask_table, mask_idx, temps, seeds, pv[0], pi[0])
+        sample_final(pv, pi, out)
+        return out
+    _, idx = ref.sample(logits, mask_table, mask_idx, temps, seeds, v0)
+    if out is not None:
+        out.copy_(idx)
+        return out
+    return idx
+
+
+def moe_topk(router_logits, topk, renorm, weights, ids):
+    if _gpu(router_logits):
+        _native.ops().moe_topk(router_logits, topk, renorm, weights, ids)
+    else:
+        w, i = ref.moe_topk(router_logits, topk, renorm)
+        weights.copy_(w)
+        ids.copy_(i)
+
+
+def moe_align(topk_ids, E, block_m, sorted_ids, inv_pos, expert_of_block, expert_offsets,
+              num_blocks):
+    _native.ops().moe_align(topk_ids, E, block_m, sorted_ids, inv_pos, expert_of_block,
+                            expert_offsets, num_blocks)
+
+
+def moe_gather(x, sorted_ids, topk, out):
+    _native.ops().moe_gather(x, sorted_ids, topk, out)
+
+
+def moe_grouped_gemm(x, w, out, expert_of_block, num_blocks):
+    _native.ops().moe_grouped_gemm(x, w, out, expert_of_block, num_blocks)
+
+
+def moe_combine(y, inv_pos, weights, topk, out):
+    _native.ops().moe_combine(y, inv_pos, weights, topk, out)

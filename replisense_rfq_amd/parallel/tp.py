@@ -1,0 +1,110 @@
+"""Tensor parallelism over RCCL/xGMI (Megatron column/row split).
+
+SURVEY.md §2.3 / §2.5: per decoder layer the QKV and gate|up projections are
+column-parallel (each rank owns Hq/TP query heads, Hkv/TP kv heads and FFN/TP
+columns), the O and down projections are row-parallel and followed by ONE
+all-reduce each (C1, C2); the LM head is vocab-parallel and the sampler reduces
+(value, index) partials with an all-gather (C3).  Embeddings are replicated (no
+collective).  One process per GPU; ``torch.distributed`` backend ``"nccl"`` is
+RCCL on ROCm and its collectives are capturable inside hipGraphs.
+
+On a CPU host the same code runs over ``gloo`` (tests use world_size 2-4).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPContext:
+    rank: int = 0
+    world: int = 1
+    group: object = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    def shard(self, n: int) -> tuple[int, int]:
+        """[start, end) of this rank's slice of a dimension of size n (n % world == 0)."""
+        if n % self.world:
+            raise ValueError(f"dimension {n} not divisible by TP={self.world}")
+        s = n // self.world
+        return self.rank * s, (self.rank + 1) * s
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out: [world, *inp.shape]"""
+        if self.world > 1:
+            dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group)
+        else:
+            out[0].copy_(inp)
+        return out
+
+    def broadcast_obj(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+
+SINGLE = TPContext()
+
+
+def init_distributed(backend: str | None = None, timeout_s: float = 600.0) -> TPContext:
+    """Initialise the default process group from torchrun env vars (RANK/WORLD_SIZE/...).
+
+    Returns a TPContext spanning the whole world.  Idempotent.
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world == 1:
+        return TPContext()
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", rank))
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s),
+                                    device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+    return TPContext(rank=dist.get_rank(), world=dist.get_world_size(), group=dist.group.WORLD)
+
+
+def split_groups(tp: int) -> tuple[TPContext, int, int]:
+    """Partition the world into world/tp tensor-parallel groups (DP replicas x TP).
+
+    Returns (tp_context, dp_rank, dp_world).  Must be called by every rank.
+    """
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if tp == 1:
+        return TPContext(), rank, world
+    if world % tp:
+        raise ValueError(f"world {world} not divisible by tp {tp}")
+    mine = None
+    for g in range(world // tp):
+        ranks = list(range(g * tp, (g + 1) * tp))
+        grp = dist.new_group(ranks)
+        if rank in ranks:
+            mine = TPContext(rank=rank - g * tp, world=tp, group=grp)
+    return mine, rank // tp, world // tp
