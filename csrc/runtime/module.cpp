@@ -1,0 +1,139 @@
+// pybind11 bindings of the host runtime: replisense_rfq_amd._runtime
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "block_manager.h"
+#include "grammar.h"
+
+namespace py = pybind11;
+using namespace rfqrt;
+
+template <typename T>
+using arr = py::array_t<T, py::array::c_style | py::array::forcecast>;
+
+template <typename T>
+static std::vector<T> vec(const py::dict& d, const char* k) {
+  arr<T> a = d[k].cast<arr<T>>();
+  return std::vector<T>(a.data(), a.data() + a.size());
+}
+
+static Grammar* make_grammar(const py::dict& d) {
+  auto* g = new Grammar();
+  auto ops = vec<int32_t>(d, "ops");
+  for (size_t i = 0; i + 5 <= ops.size(); i += 5)
+    g->ops.push_back(Op{ops[i], ops[i + 1], ops[i + 2], ops[i + 3], ops[i + 4]});
+  g->lit_off = vec<int32_t>(d, "lit_off");
+  g->lit_tok = vec<int32_t>(d, "lit_tok");
+  g->lit1_off = vec<int32_t>(d, "lit1_off");
+  g->lit1_tok = vec<int32_t>(d, "lit1_tok");
+  g->choice_off = vec<int32_t>(d, "choice_off");
+  auto alts = vec<int32_t>(d, "alts");
+  for (size_t i = 0; i + 6 <= alts.size(); i += 6)
+    g->alts.push_back(Alt{alts[i], alts[i + 1], alts[i + 2], alts[i + 3], alts[i + 4], alts[i + 5]});
+  g->alt_rest = vec<int32_t>(d, "alt_rest");
+  g->choice_mask = vec<int32_t>(d, "choice_mask");
+  g->choice_mask_close = vec<int32_t>(d, "choice_mask_close");
+  g->max_items = vec<int32_t>(d, "max_items");
+  g->num_masks = vec<int32_t>(d, "num_masks");
+  g->null_rest = vec<int32_t>(d, "null_rest");
+  g->tok_class = vec<uint8_t>(d, "tok_class");
+  g->tok_chars = vec<uint8_t>(d, "tok_chars");
+  g->tok_digits = vec<uint8_t>(d, "tok_digits");
+  auto sc = vec<int32_t>(d, "scalars");  // str_mask quote zero dot null_first end0 end1 end2 start
+  g->str_mask = sc[0]; g->quote = sc[1]; g->zero = sc[2]; g->dot = sc[3]; g->null_first = sc[4];
+  g->end_tok[0] = sc[5]; g->end_tok[1] = sc[6]; g->end_tok[2] = sc[7]; g->start_pc = sc[8];
+  return g;
+}
+
+PYBIND11_MODULE(_runtime, m) {
+  m.doc() = "replisense_rfq_amd native host runtime (grammar automaton, KV block manager)";
+
+  py::class_<Grammar>(m, "Grammar")
+      .def(py::init(&make_grammar))
+      .def("initial", [](const Grammar& g) {
+        std::vector<int32_t> forced;
+        State s = g.initial(forced);
+        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem), forced);
+      })
+      .def("advance", [](const Grammar& g, py::tuple st, int32_t tok) {
+        State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
+                st[3].cast<int32_t>()};
+        std::vector<int32_t> forced;
+        if (!g.advance(s, tok, forced)) throw py::value_error("token not allowed by grammar");
+        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem), forced);
+      })
+      .def("mask", [](const Grammar& g, py::tuple st) {
+        State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
+                st[3].cast<int32_t>()};
+        return g.mask(s);
+      })
+      // states: int32 [n, 4] updated in place; tokens: int32 [n]
+      // returns (mask_idx[n] (-1 = finished), forced_offsets[n+1], forced_tokens, ok[n])
+      .def("batch_advance", [](const Grammar& g, py::array_t<int32_t, py::array::c_style> states,
+                               arr<int32_t> tokens) {
+        const py::ssize_t n = tokens.size();
+        if (states.ndim() != 2 || states.shape(0) != n || states.shape(1) != 4)
+          throw py::value_error("states must be int32 [n, 4]");
+        auto S = states.mutable_unchecked<2>();
+        const int32_t* tk = tokens.data();
+        py::array_t<int32_t> masks(n), offs(n + 1);
+        py::array_t<bool> ok(n);
+        auto M = masks.mutable_unchecked<1>();
+        auto O = offs.mutable_unchecked<1>();
+        auto K = ok.mutable_unchecked<1>();
+        std::vector<int32_t> forced;
+        forced.reserve(n * 8);
+        {
+          py::gil_scoped_release nogil;
+          for (py::ssize_t i = 0; i < n; ++i) {
+            O(i) = (int32_t)forced.size();
+            State s{S(i, 0), S(i, 1), S(i, 2), S(i, 3)};
+            const bool good = g.advance(s, tk[i], forced);
+            K(i) = good;
+            S(i, 0) = s.pc; S(i, 1) = s.sub; S(i, 2) = s.cnt; S(i, 3) = s.rem;
+            M(i) = g.mask(s);
+          }
+          O(n) = (int32_t)forced.size();
+        }
+        py::array_t<int32_t> ft(forced.size());
+        std::copy(forced.begin(), forced.end(), ft.mutable_data());
+        return py::make_tuple(masks, offs, ft, ok);
+      })
+      .def("num_ops", [](const Grammar& g) { return (int)g.ops.size(); });
+
+  py::class_<BlockManager>(m, "BlockManager")
+      .def(py::init<int32_t, int32_t>())
+      .def_property_readonly("num_blocks", &BlockManager::num_blocks)
+      .def_property_readonly("block_size", &BlockManager::block_size)
+      .def_property_readonly("num_free", &BlockManager::num_free)
+      .def_property_readonly("num_cached", &BlockManager::num_cached)
+      .def_readonly("hits", &BlockManager::hits)
+      .def_readonly("queries", &BlockManager::queries)
+      .def_readonly("evictions", &BlockManager::evictions)
+      .def("allocate", [](BlockManager& bm, int32_t n) -> py::object {
+        std::vector<int32_t> out;
+        if (!bm.allocate(n, out)) return py::none();
+        return py::cast(out);
+      })
+      .def("release", [](BlockManager& bm, const std::vector<int32_t>& blocks) {
+        bm.release(blocks.data(), (int32_t)blocks.size());
+      })
+      .def("match_prefix", [](BlockManager& bm, const std::vector<uint64_t>& hashes) {
+        std::vector<int32_t> out;
+        bm.match_prefix(hashes.data(), (int32_t)hashes.size(), out);
+        return out;
+      })
+      .def("register_block", &BlockManager::register_block)
+      .def("refcount", &BlockManager::refcount)
+      .def_static("hash_blocks", [](arr<int32_t> tokens, int32_t block_size, uint64_t parent) {
+        const int32_t n = (int32_t)tokens.size() / block_size;
+        std::vector<uint64_t> out(n);
+        const int32_t* t = tokens.data();
+        for (int32_t i = 0; i < n; ++i) {
+          parent = BlockManager::hash_block(parent, t + (int64_t)i * block_size, block_size);
+          out[i] = parent;
+        }
+        return out;
+      }, py::arg("tokens"), py::arg("block_size"), py::arg("parent") = 0);
+}

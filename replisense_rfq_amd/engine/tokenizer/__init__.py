@@ -1,0 +1,116 @@
+"""Tokenizers + chat templates for the served model families.
+
+The byte-level BPE vocabularies (128,256 ids for Llama-3, 32,000 for Mixtral) are
+trained offline by tools/train_tokenizer.py and shipped gzip'd next to this file;
+the `tokenizers` (Rust) library does encode/decode.  The chat templates reproduce
+the Llama-3 header format and the Mistral [INST] format, so a request is
+``[system, user]`` exactly as ag2 sent it to Groq.
+"""
+from __future__ import annotations
+
+import functools
+import gzip
+from pathlib import Path
+
+from tokenizers import Tokenizer as _HFTok
+
+_DIR = Path(__file__).resolve().parent
+
+
+def _bytes_to_unicode() -> dict[int, str]:
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + \
+        list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, map(chr, cs)))
+
+
+_U2B = {u: b for b, u in _bytes_to_unicode().items()}
+
+
+class Tokenizer:
+    def __init__(self, flavor: str = "llama3"):
+        path = _DIR / f"{flavor}_synth.json.gz"
+        with gzip.open(path, "rb") as f:
+            self._tok = _HFTok.from_str(f.read().decode())
+        self.flavor = flavor
+        self.vocab_size = self._tok.get_vocab_size()
+        if flavor == "llama3":
+            self.bos_id = self._tok.token_to_id("<|begin_of_text|>")
+            self.eot_id = self._tok.token_to_id("<|eot_id|>")
+            self.eos_ids = (self._tok.token_to_id("<|end_of_text|>"), self.eot_id)
+            self._hdr_start = self._tok.token_to_id("<|start_header_id|>")
+            self._hdr_end = self._tok.token_to_id("<|end_header_id|>")
+        else:
+            self.bos_id = self._tok.token_to_id("<s>")
+            self.eot_id = self._tok.token_to_id("</s>")
+            self.eos_ids = (self.eot_id,)
+
+    # -------------------------------------------------------------- encode/decode
+    def encode(self, text: str) -> list[int]:
+        return self._tok.encode(text, add_special_tokens=False).ids
+
+    def encode_batch(self, texts: list[str]) -> list[list[int]]:
+        return [e.ids for e in self._tok.encode_batch(texts, add_special_tokens=False)]
+
+    def decode(self, ids, skip_special: bool = True) -> str:
+        return self._tok.decode(list(ids), skip_special_tokens=skip_special)
+
+    @functools.lru_cache(maxsize=1)
+    def token_bytes_table(self) -> list[bytes | None]:
+        """Raw bytes of every id (None for special/added tokens)."""
+        out: list[bytes | None] = [None] * self.vocab_size
+        added = {t.content for t in self._tok.get_added_tokens_decoder().values()}
+        for s, i in self._tok.get_vocab(with_added_tokens=True).items():
+            if s in added or i >= self.vocab_size:
+                continue
+            try:
+                out[i] = bytes(_U2B[c] for c in s)
+            except KeyError:
+                out[i] = None
+        return out
+
+    # ------------------------------------------------------------- chat template
+    def chat_ids(self, messages: list[dict], add_generation_prompt: bool = True) -> list[int]:
+        if self.flavor == "llama3":
+            ids = [self.bos_id]
+            for m in messages:
+                ids += [self._hdr_start] + self.encode(m["role"]) + [self._hdr_end]
+                ids += self.encode("\n\n" + m["content"].strip()) + [self.eot_id]
+            if add_generation_prompt:
+                ids += [self._hdr_start] + self.encode("assistant") + [self._hdr_end]
+                ids += self.encode("\n\n")
+            return ids
+        # Mistral/Mixtral: system text is folded into the first user turn
+        sys_txt = "".join(m["content"] for m in messages if m["role"] == "system")
+        ids = [self.bos_id]
+        for m in messages:
+            if m["role"] == "user":
+                body = (sys_txt + "\n\n" + m["content"]) if sys_txt else m["content"]
+                sys_txt = ""
+                ids += self.encode(f"[INST] {body} [/INST]")
+            elif m["role"] == "assistant":
+                ids += self.encode(m["content"]) + [self.eot_id]
+        return ids
+
+    def shared_prefix_len(self, a: list[int], b: list[int]) -> int:
+        n = 0
+        for x, y in zip(a, b):
+            if x != y:
+                break
+            n += 1
+        return n
+
+
+@functools.lru_cache(maxsize=4)
+def get_tokenizer(flavor: str = "llama3") -> Tokenizer:
+    return Tokenizer(flavor)
+
+
+def flavor_for_vocab(vocab_size: int) -> str:
+    return "mixtral" if vocab_size == 32000 else "llama3"

@@ -1,0 +1,152 @@
+"""Llama-3 / Mixtral decoder on the gfx950 kernels.
+
+One class serves Llama-3-8B, Llama-3-70B (TP=1..8) and Mixtral-8x7B (sparse MoE
+MLP).  A forward pass consumes a *mixed* token batch laid out as
+``[decode tokens (one per running sequence) | prefill/extend tokens]``:
+
+  embed -> for each layer:
+     fused_add_rms_norm -> QKV GEMM (hipBLASLt) -> rope_kv (q in place, k/v into
+     the paged cache) -> attn_decode (split-K MFMA, decode rows) + attn_prefill
+     (varlen causal MFMA flash, extend rows) -> O GEMM -> [all-reduce]
+     -> fused_add_rms_norm -> gate|up GEMM -> silu_mul -> down GEMM -> [all-reduce]
+        (MoE: router -> top-2 -> align -> grouped MFMA GEMMs -> combine)
+  -> final norm on the rows that need logits -> vocab-parallel LM head.
+
+Residual adds are fused into the following RMSNorm, the q rotation happens in
+place inside the QKV GEMM output, and attention writes straight into the O-GEMM
+input, so a layer is 5 GEMMs + 5 custom kernels with no extra copies.  Every op
+is stream-ordered and allocation-stable, so the decode path is captured into a
+hipGraph by the engine (engine/graphs.py).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel.tp import SINGLE, TPContext
+from .config import ModelConfig
+from .moe import MoEBuffers, moe_mlp
+from .weights import init_weights
+
+
+@dataclass
+class ForwardMeta:
+    """Device-side description of one engine step (all int32 unless noted)."""
+    input_ids: torch.Tensor            # [T]
+    positions: torch.Tensor            # [T]
+    slot_mapping: torch.Tensor         # [T]
+    num_decode: int                    # first num_decode rows are q_len=1 sequences
+    dec_block_tables: torch.Tensor | None = None   # [D, maxb]
+    dec_context_lens: torch.Tensor | None = None   # [D]
+    num_prefill_tokens: int = 0
+    pf_block_tables: torch.Tensor | None = None    # [P, maxb]
+    pf_q_start: torch.Tensor | None = None         # [P] offset inside the prefill rows
+    pf_q_len: torch.Tensor | None = None           # [P]
+    pf_kv_len: torch.Tensor | None = None          # [P]
+    work_seq: torch.Tensor | None = None           # [W]
+    work_qblk: torch.Tensor | None = None          # [W]
+    logits_idx: torch.Tensor | None = None         # [S] int64 rows needing logits
+    decode_splits: int = 1
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def num_tokens(self) -> int:
+        return self.num_decode + self.num_prefill_tokens
+
+
+class DecoderLM:
+    def __init__(self, cfg: ModelConfig, device, tp: TPContext = SINGLE, seed: int = 0,
+                 weights: dict | None = None, dtype=torch.bfloat16):
+        self.cfg = cfg
+        self.tp = tp
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.hq = cfg.n_heads // tp.world
+        self.hkv = cfg.n_kv_heads // tp.world
+        self.ffn_local = cfg.ffn // tp.world
+        self.w = weights if weights is not None else init_weights(cfg, tp, self.device, dtype, seed)
+        self.vocab_start = self.w["vocab_start"]
+        self.vocab_local = self.w["lm_head"].shape[0]
+        self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                        device=self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.kv_k = None
+        self.kv_v = None
+        self._moe_bufs: dict[int, MoEBuffers] = {}
+
+    # ------------------------------------------------------------------ KV pool
+    def attach_kv_cache(self, k_pool: torch.Tensor, v_pool: torch.Tensor) -> None:
+        """Pools shaped [L, num_blocks, Hkv_local, 32, 128]."""
+        assert k_pool.shape[0] == self.cfg.n_layers and k_pool.shape[2] == self.hkv
+        self.kv_k, self.kv_v = k_pool, v_pool
+
+    def moe_buffers(self, max_tokens: int) -> MoEBuffers:
+        cap = 1
+        while cap < max_tokens:
+            cap *= 2
+        if cap not in self._moe_bufs:
+            self._moe_bufs[cap] = MoEBuffers.allocate(cap, self.cfg.moe_topk, self.cfg.n_experts,
+                                                      self.cfg.hidden, self.ffn_local,
+                                                      self.device, self.dtype)
+        return self._moe_bufs[cap]
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, m: ForwardMeta) -> torch.Tensor:
+        cfg, w = self.cfg, self.w
+        T, D = m.num_tokens, m.num_decode
+        eps = cfg.rms_eps
+        hq, hkv = self.hq, self.hkv
+        qd = hq * cfg.head_dim
+
+        h = ops.embed(m.input_ids[:T], w["embed"])
+        residual = h
+        x = ops.rms_norm(h, w["layers"][0]["attn_norm"], eps)
+        attn = torch.empty((T, qd), dtype=self.dtype, device=self.device)
+        dec_parts = None
+        if D > 0 and m.decode_splits > 1 and x.is_cuda:
+            dec_parts = (torch.empty(D * hq * m.decode_splits * 128, device=self.device),
+                         torch.empty(D * hq * m.decode_splits * 2, device=self.device))
+        moe_bufs = self.moe_buffers(T) if (cfg.is_moe and x.is_cuda) else None
+        L = cfg.n_layers
+        for li in range(L):
+            lw = w["layers"][li]
+            kc, vc = self.kv_k[li], self.kv_v[li]
+            qkv = x @ lw["qkv"].t()
+            ops.rope_kv(qkv, m.positions, self.cos_sin, m.slot_mapping, kc, vc, hq, hkv)
+            if D > 0:
+                po, pm = dec_parts if dec_parts is not None else (attn, attn)
+                ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_context_lens,
+                                attn[:D], po, pm, hq, hkv, self.scale,
+                                m.decode_splits if dec_parts is not None else 1)
+            if m.num_prefill_tokens > 0:
+                ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
+                                 m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
+                                 self.scale)
+            o = attn @ lw["o"].t()
+            self.tp.all_reduce_(o)
+            ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
+            if cfg.is_moe:
+                mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs)
+            else:
+                gu = x @ lw["gate_up"].t()
+                a = ops.silu_mul(gu)
+                mo = a @ lw["down"].t()
+            self.tp.all_reduce_(mo)
+            nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
+            ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
+        xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
+        return xs @ w["lm_head"].t()
+
+    # ------------------------------------------------------------- conveniences
+    def weight_bytes(self) -> int:
+        tot = 0
+        for k, v in self.w.items():
+            if isinstance(v, torch.Tensor):
+                tot += v.numel() * v.element_size()
+        for lw in self.w["layers"]:
+            tot += sum(t.numel() * t.element_size() for t in lw.values())
+        return tot

@@ -1,0 +1,139 @@
+"""Seeded random-init weights, generated directly as this rank's TP shard.
+
+BASELINE.json runs the benchmark on random-init weights of the real
+architectures (no checkpoints, no network).  Each tensor is drawn on the target
+device from a generator seeded by (seed, layer, name, tp_rank), so TP workers
+build their shards independently with no weight broadcast
+and a replica restart regenerates identical weights.
+
+Layout (torch Linear convention, out = x @ W^T):
+  qkv     [(Hq + 2 Hkv)/TP * 128, d]      column-parallel (q heads | k heads | v heads)
+  o       [d, Hq/TP * 128]                row-parallel
+  gate_up [2 F/TP, d]                     column-parallel (gate | up)
+  down    [d, F/TP]                       row-parallel
+  MoE:    router [E, d]; w13 [E, 2F/TP, d]; w2 [E, d, F/TP]
+  embed   [V, d] replicated; lm_head [V/TP, d] vocab-parallel
+
+A safetensors loader with the same names is provided for real checkpoints.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import torch
+
+from ..parallel.tp import TPContext
+from .config import ModelConfig
+
+
+def _seed(*parts) -> int:
+    h = hashlib.blake2b(repr(parts).encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & ((1 << 63) - 1)
+
+
+def _randn(shape, std, seed_parts, device, dtype):
+    g = torch.Generator(device=device)
+    g.manual_seed(_seed(*seed_parts))
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    t.normal_(0.0, std, generator=g)
+    return t.to(dtype)
+
+
+class LayerWeights(dict):
+    __getattr__ = dict.__getitem__
+
+
+def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, seed: int = 0):
+    d, D = cfg.hidden, cfg.head_dim
+    R = tp.world
+    if cfg.n_heads % R or cfg.n_kv_heads % R or cfg.ffn % R or cfg.vocab_size % R:
+        raise ValueError(f"{cfg.name} is not divisible by TP={R}")
+    hq, hkv, F = cfg.n_heads // R, cfg.n_kv_heads // R, cfg.ffn // R
+    std = cfg.init_std
+    r = tp.rank
+    ones = lambda n: torch.ones(n, dtype=dtype, device=device)  # noqa: E731
+    layers = []
+    for li in range(cfg.n_layers):
+        lw = LayerWeights(
+            attn_norm=ones(d),
+            mlp_norm=ones(d),
+            qkv=_randn(((hq + 2 * hkv) * D, d), std, (seed, li, "qkv", r), device, dtype),
+            o=_randn((d, hq * D), std, (seed, li, "o", r), device, dtype),
+        )
+        if cfg.is_moe:
+            E = cfg.n_experts
+            lw["router"] = _randn((E, d), std, (seed, li, "router"), device, dtype)
+            lw["w13"] = _randn((E, 2 * F, d), std, (seed, li, "w13", r), device, dtype)
+            lw["w2"] = _randn((E, d, F), std, (seed, li, "w2", r), device, dtype)
+        else:
+            lw["gate_up"] = _randn((2 * F, d), std, (seed, li, "gate_up", r), device, dtype)
+            lw["down"] = _randn((d, F), std, (seed, li, "down", r), device, dtype)
+        layers.append(lw)
+    v0, v1 = tp.shard(cfg.vocab_size)
+    return dict(
+        embed=_randn((cfg.vocab_size, d), std, (seed, "embed"), device, dtype),
+        final_norm=ones(d),
+        lm_head=_randn((v1 - v0, d), std, (seed, "lm_head", r), device, dtype),
+        layers=layers,
+        vocab_start=v0,
+    )
+
+
+def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16):
+    """Load HF-style Llama/Mixtral safetensors shards into this rank's layout."""
+    import glob
+    import os
+
+    from safetensors import safe_open
+
+    files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
+    tensors = {}
+    for f in files:
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in fh.keys():
+                tensors[k] = fh.get_tensor(k)
+
+    def cols(t, n):           # column-parallel rows of W
+        a, b = tp.shard(n)
+        return t[a:b]
+
+    def rows(t, n):           # row-parallel columns of W
+        a, b = tp.shard(n)
+        return t[:, a:b]
+
+    D, F = cfg.head_dim, cfg.ffn
+    layers = []
+    for li in range(cfg.n_layers):
+        p = f"model.layers.{li}."
+        q = cols(tensors[p + "self_attn.q_proj.weight"], cfg.n_heads * D)
+        k = cols(tensors[p + "self_attn.k_proj.weight"], cfg.n_kv_heads * D)
+        v = cols(tensors[p + "self_attn.v_proj.weight"], cfg.n_kv_heads * D)
+        lw = LayerWeights(
+            attn_norm=tensors[p + "input_layernorm.weight"],
+            mlp_norm=tensors[p + "post_attention_layernorm.weight"],
+            qkv=torch.cat([q, k, v]),
+            o=rows(tensors[p + "self_attn.o_proj.weight"], cfg.n_heads * D),
+        )
+        if cfg.is_moe:
+            ex = p + "block_sparse_moe."
+            lw["router"] = tensors[ex + "gate.weight"]
+            lw["w13"] = torch.stack([torch.cat([cols(tensors[f"{ex}experts.{e}.w1.weight"], F),
+                                                cols(tensors[f"{ex}experts.{e}.w3.weight"], F)])
+                                     for e in range(cfg.n_experts)])
+            lw["w2"] = torch.stack([rows(tensors[f"{ex}experts.{e}.w2.weight"], F)
+                                    for e in range(cfg.n_experts)])
+        else:
+            lw["gate_up"] = torch.cat([cols(tensors[p + "mlp.gate_proj.weight"], F),
+                                       cols(tensors[p + "mlp.up_proj.weight"], F)])
+            lw["down"] = rows(tensors[p + "mlp.down_proj.weight"], F)
+        layers.append(LayerWeights({k: t.to(device=device, dtype=dtype).contiguous()
+                                    for k, t in lw.items()}))
+    v0, v1 = tp.shard(cfg.vocab_size)
+    head = tensors.get("lm_head.weight", tensors["model.embed_tokens.weight"])
+    return dict(
+        embed=tensors["model.embed_tokens.weight"].to(device=device, dtype=dtype),
+        final_norm=tensors["model.norm.weight"].to(device=device, dtype=dtype),
+        lm_head=head[v0:v1].to(device=device, dtype=dtype).contiguous(),
+        layers=layers,
+        vocab_start=v0,
+    )

@@ -1,0 +1,36 @@
+"""Native host runtime (``_runtime`` pybind11 module built from csrc/runtime/*.cpp).
+
+Provides the grammar automaton executor and the paged-KV block manager used on
+the scheduler's per-step hot path.  Built in-tree by ``replisense_rfq_amd._build``.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_mod = None
+
+
+def load():
+    """Import (building first if needed) the native runtime module."""
+    global _mod
+    if _mod is not None:
+        return _mod
+    try:
+        _mod = importlib.import_module("replisense_rfq_amd._runtime")
+    except ImportError:
+        if os.environ.get("RFQ_AUTOBUILD", "1") != "1":
+            raise
+        from .. import _build
+
+        _build.build_runtime()
+        _mod = importlib.import_module("replisense_rfq_amd._runtime")
+    return _mod
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
