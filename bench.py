@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""RFQ extraction benchmark — BASELINE.json metric:
+"RFQ docs/sec whole-node + p50 /parse-text/ latency, Llama-3-8B TP=1 and 70B TP=8".
+
+One process per GPU (torchrun).  Each TP group is one engine replica (default
+Llama-3-8B, TP=1 => DP=N replicas, weak scaling: every replica processes the same
+number of documents per step).  A *step* = one wave of ``--docs-per-step``
+synthetic RFQ documents per replica pushed through the full extraction path:
+prompt build (8,000-char truncation + byte-identical template) -> Llama-3 chat
+tokenisation -> continuous-batching engine (chunked prefill, prefix cache,
+grammar-constrained Gumbel sampling at T=0.1, jump-forward, hipGraph decode) ->
+detokenise -> JSON recovery + pydantic validation (rfq_agent.py:185-206).
+Weights are random-init (no checkpoints offline); documents are synthetic with
+the reference's length distribution.
+
+Timed region: exactly --steps waves, bracketed by barrier + cuda synchronize on
+both sides; the max over ranks is reported.  After it, the single-request p50
+latency of the same path (the reference's 0.883 s p50 Groq server time,
+BASELINE.md) is measured on replica 0.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from replisense_rfq_amd.engine.engine import LLMEngine
+from replisense_rfq_amd.engine.sequence import SamplingParams
+from replisense_rfq_amd.parallel.tp import init_distributed, split_groups
+from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
+from replisense_rfq_amd.utils import synth
+from replisense_rfq_amd.utils.config import EngineConfig
+
+BASELINE_P50_S = 0.883          # Groq llama3-70b p50 server time per request
+BASELINE_DOCS_PER_S = 1.0 / BASELINE_P50_S
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--docs-per-step", type=int, default=256)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--latency-runs", type=int, default=5)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-jump-forward", action="store_true")
+    ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--prefill-chunk", type=int, default=16384)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+class Replica:
+    def __init__(self, engine: LLMEngine, dp_rank: int, seed: int):
+        self.engine = engine
+        self.tok = engine.tokenizer
+        self.dp_rank = dp_rank
+        self.seed = seed
+        self.wave = 0
+        self.last = {}
+
+    def docs(self, n: int):
+        base = (self.seed * 7919 + self.dp_rank) * 1_000_003 + self.wave * 10_007
+        self.wave += 1
+        return [synth.make_rfq(base + i) for i in range(n)]
+
+    def run_wave(self, n: int) -> int:
+        docs = self.docs(n)
+        msgs = [build_messages(d.text) for d in docs]
+        prompts = [self.tok.chat_ids(m) for m in msgs]
+        eng = self.engine
+        params = SamplingParams(temperature=eng.cfg.temperature, max_tokens=eng.cfg.max_tokens,
+                                grammar=eng.grammar is not None)
+        seqs = eng.generate(prompts, params, seeds=[hash((self.wave, i)) & 0xFFFF
+                                                    for i in range(n)])
+        ok = 0
+        for s in seqs:
+            out = parse_and_validate_response(eng.decode_text(s), "direct_text_input")
+            ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
+        eng.runner.tp.enabled and eng.shutdown()
+        self.last = dict(
+            prompt_tokens=sum(s.prompt_len for s in seqs) / n,
+            completion_tokens=sum(s.num_generated for s in seqs) / n,
+            sampled_tokens=sum(s.num_sampled for s in seqs) / n,
+            prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n,
+            valid=ok / n)
+        return ok
+
+    def latency(self, runs: int) -> list[float]:
+        out = []
+        eng = self.engine
+        for i in range(runs):
+            d = synth.make_rfq(10_000_000 + self.dp_rank * 1000 + i)
+            t0 = time.perf_counter()
+            ids = self.tok.chat_ids(build_messages(d.text))
+            s, = eng.generate([ids])
+            parse_and_validate_response(eng.decode_text(s), "direct_text_input")
+            out.append(time.perf_counter() - t0)
+            eng.runner.tp.enabled and eng.shutdown()
+        return out
+
+
+def sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    wctx = init_distributed()
+    tp, dp_rank, dp_world = split_groups(args.tp) if world > 1 else (wctx, 0, 1)
+    cfg = EngineConfig.from_env(
+        model=args.model, tp=args.tp, seed=args.seed, max_num_seqs=args.max_num_seqs,
+        use_graphs=not args.no_graphs, jump_forward=not args.no_jump_forward,
+        prefix_cache=not args.no_prefix_cache, max_batched_tokens=args.prefill_chunk)
+    t_init = time.perf_counter()
+    engine = LLMEngine(cfg, tp=tp)
+    t_init = time.perf_counter() - t_init
+    rep = Replica(engine, dp_rank, args.seed)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def phase(fn):
+        """TP rank 0 drives `fn`; the other ranks of its group mirror the steps."""
+        if tp.rank == 0:
+            r = fn()
+        else:
+            engine.worker_loop()
+            r = None
+        return r
+
+    for _ in range(args.warmup):
+        phase(lambda: rep.run_wave(args.docs_per_step))
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        phase(lambda: rep.run_wave(args.docs_per_step))
+    sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    steps_before = engine.num_steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device=engine.device if engine.device.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    lat = []
+    if args.latency_runs and dp_rank == 0:
+        lat = phase(lambda: rep.latency(args.latency_runs)) or []
+    barrier()
+
+    if rank == 0:
+        docs = args.docs_per_step * dp_world * args.steps
+        value = docs / dt
+        p50 = statistics.median(lat) if lat else None
+        st = engine.stats()
+        out = {
+            "metric": "rfq_docs_per_sec_whole_node",
+            "value": round(value, 3),
+            "unit": "docs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_DOCS_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic RFQ documents (reference length distribution), random-init weights",
+            "config": {"model": args.model, "global_batch": args.docs_per_step * dp_world,
+                       "seq_len": int(rep.last.get("prompt_tokens", 0) +
+                                      rep.last.get("completion_tokens", 0)),
+                       "parallelism": f"dp{dp_world}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
+                       "docs_per_step_per_replica": args.docs_per_step,
+                       "temperature": cfg.temperature, "grammar": cfg.grammar,
+                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs},
+            "p50_parse_text_latency_s": round(p50, 4) if p50 is not None else None,
+            "latency_vs_baseline_p50": round(BASELINE_P50_S / p50, 2) if p50 else None,
+            "baseline": "vs_baseline = docs/s / (1 / 0.883 s), the reference's single-stream "
+                        "Groq llama3-70b p50 server time (BASELINE.md)",
+            "per_doc": {k: round(v, 2) for k, v in rep.last.items()},
+            "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
+                       "engine_steps": steps_before, "graph_steps": st.get("graph_steps"),
+                       "kv_blocks": st.get("blocks"), "preempted": st.get("preempted")},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+"""Typed engine/service configuration from environment + CLI.
+
+Reference env vars are kept with their defaults (MAX_FILE_SIZE_MB=10,
+ALLOWED_ORIGINS=*, PORT=8000, ENVIRONMENT=development, LOG_LEVEL=info —
+app/main.py:37,85,414-416); GROQ_API_KEY is no longer required because inference
+is on-node.  Engine knobs are RFQ_* variables.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import asdict, dataclass, field, fields
+
+
+def _env(name, default, cast=str):
+    v = os.environ.get(name)
+    if v is None or v == "":
+        return default
+    if cast is bool:
+        return v.lower() in ("1", "true", "on", "yes")
+    return cast(v)
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    tp: int = 1
+    dp: int = 1
+    device: str = "auto"                 # auto -> cuda if available else cpu
+    seed: int = 0
+    kv_fraction: float = 0.45            # of free HBM for the paged KV pool
+    max_kv_blocks: int = 0               # 0 = from kv_fraction
+    block_size: int = 32                 # tokens per KV page (kernel tile)
+    max_num_seqs: int = 256
+    max_batched_tokens: int = 16384      # prefill chunk budget per step
+    max_model_len: int = 8192            # llama3-70b-8192 context
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    use_graphs: bool = True
+    grammar: bool = True
+    jump_forward: bool = True
+    prefix_cache: bool = True
+    temperature: float = 0.1             # rfq_agent.py:66
+    max_tokens: int = 1200               # rfq_agent.py:67
+    request_timeout_s: float = 30.0      # rfq_agent.py:69
+    step_timeout_s: float = 120.0        # watchdog
+    custom_allreduce: bool = False
+    trace: bool = False                  # per-request JSON spans
+
+    @classmethod
+    def from_env(cls, **overrides) -> "EngineConfig":
+        c = cls(
+            model=_env("RFQ_MODEL", cls.model),
+            tp=_env("RFQ_TP", cls.tp, int),
+            dp=_env("RFQ_DP", cls.dp, int),
+            device=_env("RFQ_DEVICE", cls.device),
+            seed=_env("RFQ_SEED", cls.seed, int),
+            kv_fraction=_env("RFQ_KV_FRACTION", cls.kv_fraction, float),
+            max_num_seqs=_env("RFQ_MAX_BATCH", cls.max_num_seqs, int),
+            max_batched_tokens=_env("RFQ_PREFILL_CHUNK", cls.max_batched_tokens, int),
+            use_graphs=_env("RFQ_GRAPHS", cls.use_graphs, bool),
+            grammar=_env("RFQ_GRAMMAR", cls.grammar, bool),
+            jump_forward=_env("RFQ_JUMP_FORWARD", cls.jump_forward, bool),
+            prefix_cache=_env("RFQ_PREFIX_CACHE", cls.prefix_cache, bool),
+            custom_allreduce=_env("RFQ_CUSTOM_AR", cls.custom_allreduce, bool),
+            trace=_env("RFQ_TRACE", cls.trace, bool),
+        )
+        gb = os.environ.get("RFQ_GRAPH_BUCKETS")
+        if gb:
+            c.graph_buckets = tuple(int(x) for x in gb.split(","))
+        for k, v in overrides.items():
+            if v is not None:
+                setattr(c, k, v)
+        return c
+
+    def to_dict(self):
+        return asdict(self)
+
+
+@dataclass
+class ServiceConfig:
+    max_file_size_mb: int = field(default_factory=lambda: _env("MAX_FILE_SIZE_MB", 10, int))
+    allowed_origins: str = field(default_factory=lambda: _env("ALLOWED_ORIGINS", "*"))
+    port: int = field(default_factory=lambda: _env("PORT", 8000, int))
+    environment: str = field(default_factory=lambda: _env("ENVIRONMENT", "development"))
+    log_level: str = field(default_factory=lambda: _env("LOG_LEVEL", "info"))
+    backend: str = field(default_factory=lambda: _env("RFQ_BACKEND", "engine"))  # engine|mock
+
+
+def field_names(cls) -> list[str]:
+    return [f.name for f in fields(cls)]
