@@ -137,7 +137,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
                           block_tables.data_ptr<int32_t>(), block_tables.stride(0),
                           context_lens.data_ptr<int32_t>(), bpm(out), out.stride(0),
-                          part_o.data_ptr<float>(), part_ml.data_ptr<float>(), B, Hq, Hkv,
+                          num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
+                          num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, B, Hq, Hkv,
                           (float)scale, num_splits, cur_stream());
 }
 

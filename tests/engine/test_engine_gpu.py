@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _meta(T, device, nblocks):
-    ids = torch.randint(0, 1000, (T,), dtype=torch.int32)
+    g = torch.Generator().manual_seed(1234)
+    ids = torch.randint(0, 1000, (T,), dtype=torch.int32, generator=g)
     pos = torch.arange(T, dtype=torch.int32)
     bt = torch.arange((T + 31) // 32, dtype=torch.int32)[None]
     m = dict(input_ids=ids, positions=pos, slot_mapping=pos.clone(), num_decode=0,
@@ -75,20 +76,63 @@ def test_engine_generates_valid_rfq_json(gpu):
     assert all(s.prefix_hit_tokens >= 400 for s in seqs2), [s.prefix_hit_tokens for s in seqs2]
 
 
-def test_graph_and_eager_agree(gpu):
-    prompts = None
-    outs = []
+def test_graph_replay_matches_eager_forward(gpu):
+    """A captured decode forward replays to bit-identical logits (same kernels, same
+    shapes) and picks up new metadata written into its static input buffers."""
+    cfg = get_config("tiny-llama")
+    m = DecoderLM(cfg, gpu, seed=5)
+    nb, B = 64, 8
+    shape = (cfg.n_layers, nb, m.hkv, 32, 128)
+    g0 = torch.Generator(device="cpu").manual_seed(0)
+    m.attach_kv_cache(torch.randn(shape, generator=g0).to(gpu, torch.bfloat16),
+                      torch.randn(shape, generator=g0).to(gpu, torch.bfloat16))
+    i32 = dict(dtype=torch.int32, device=gpu)
+    st = dict(ids=torch.zeros(B, **i32), pos=torch.zeros(B, **i32),
+              slots=torch.zeros(B, **i32), bt=torch.zeros(B, 8, **i32), ctx=torch.ones(B, **i32))
+
+    def meta():
+        return ForwardMeta(input_ids=st["ids"], positions=st["pos"], slot_mapping=st["slots"],
+                           num_decode=B, dec_block_tables=st["bt"], dec_context_lens=st["ctx"],
+                           decode_splits=4)
+
+    def fill(seed):
+        g = torch.Generator().manual_seed(seed)
+        st["ids"].copy_(torch.randint(0, 5000, (B,), generator=g))
+        ctx = torch.randint(1, 200, (B,), generator=g)
+        st["ctx"].copy_(ctx)
+        st["pos"].copy_(ctx - 1)
+        bt = torch.arange(B * 8).view(B, 8) % (nb - 1)
+        st["bt"].copy_(bt)
+        st["slots"].copy_(bt[torch.arange(B), (ctx - 1) // 32] * 32 + (ctx - 1) % 32)
+
+    fill(1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        m.forward(meta())
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = m.forward(meta())
+    for seed in (2, 3):
+        fill(seed)
+        graph.replay()
+        got = out.clone()
+        fill(seed)
+        exp = m.forward(meta())
+        assert torch.equal(got, exp)
+
+
+def test_engine_graphs_on_and_off_both_valid(gpu):
     for graphs in (False, True):
         eng = _engine(graphs)
         tok = eng.tokenizer
-        prompts = prompts or [tok.chat_ids(build_messages(synth.make_rfq(10 + i).text))
-                              for i in range(4)]
-        seqs = eng.generate(prompts)
-        outs.append([s.output_ids for s in seqs])
+        prompts = [tok.chat_ids(build_messages(synth.make_rfq(10 + i).text)) for i in range(4)]
+        for s in eng.generate(prompts):
+            RFQResponse(**json.loads(eng.decode_text(s)))
+        assert (eng.stats()["graph_steps"] > 0) == graphs
         del eng
         torch.cuda.empty_cache()
-    same = sum(a == b for a, b in zip(*outs))
-    assert same >= 3, "graph replay diverged from eager decode"
 
 
 def test_mixtral_engine(gpu):
