@@ -19,8 +19,9 @@ void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hi
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
-                        const int32_t*, bf16_t*, int64_t, float*, float*, int, int, int, float, int,
-                        hipStream_t);
+                        const int32_t*, const int32_t*, const int32_t*, const int32_t*,
+                        const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
+                        float, int, hipStream_t);
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                          const int32_t*, int, bf16_t*, int64_t, int, int, float, hipStream_t);
@@ -113,32 +114,44 @@ void rope_kv(const Tensor& qkv, const Tensor& positions, const Tensor& cos_sin,
                       bpm(v_cache), T, Hq, Hkv, k_cache.size(2), cur_stream());
 }
 
+// Paged decode / short-extend attention.  Rows of q/out [rows, *] belong to
+// sequences described by (seq_q_start, seq_q_len, seq_kv_len, block_tables);
+// work items (work_seq, work_ct) = (sequence, 16-column tile of q_len*G columns),
+// work_seq = -1 marks padding.
 void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
-                 const Tensor& block_tables, const Tensor& context_lens, const Tensor& out,
-                 const Tensor& part_o, const Tensor& part_ml, int64_t Hq, int64_t Hkv,
-                 double scale, int64_t num_splits) {
+                 const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
+                 const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
+                 const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
+                 int64_t Hkv, double scale, int64_t num_splits) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
-  CHECK_I32(block_tables); CHECK_I32(context_lens); CHECK_ROWMAJOR(block_tables);
+  CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
+  CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
+  CHECK_I32(work_seq); CHECK_I32(work_ct);
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 32 && k_cache.size(3) == 128 &&
                   k_cache.size(1) == Hkv,
               "attn_decode: cache must be [blocks, Hkv, 32, 128]");
   TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "attn_decode: GQA group must be <= 16");
-  const int B = out.size(0);
-  TORCH_CHECK(q.size(0) >= B && block_tables.size(0) >= B && context_lens.numel() >= B,
-              "attn_decode: batch mismatch");
+  const int rows = out.size(0);
+  TORCH_CHECK(q.size(0) >= rows, "attn_decode: q has fewer rows than out");
+  TORCH_CHECK(work_seq.numel() == work_ct.numel(), "work list mismatch");
+  TORCH_CHECK(block_tables.size(0) >= seq_q_len.numel() && seq_kv_len.numel() >= seq_q_len.numel()
+                  && seq_q_start.numel() >= seq_q_len.numel(),
+              "attn_decode: per-sequence arrays mismatch");
   TORCH_CHECK(num_splits >= 1 && num_splits <= 64, "attn_decode: num_splits in [1, 64]");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
-    TORCH_CHECK(part_o.numel() >= (int64_t)B * Hq * num_splits * 128 &&
-                    part_ml.numel() >= (int64_t)B * Hq * num_splits * 2,
+    TORCH_CHECK(part_o.numel() >= (int64_t)rows * Hq * num_splits * 128 &&
+                    part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
                 "attn_decode: partial buffers too small");
   }
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
                           block_tables.data_ptr<int32_t>(), block_tables.stride(0),
-                          context_lens.data_ptr<int32_t>(), bpm(out), out.stride(0),
-                          num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
-                          num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, B, Hq, Hkv,
+                          seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
+                          seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(),
+                          work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
+                          out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
+                          num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
                           (float)scale, num_splits, cur_stream());
 }
 
@@ -274,8 +287,9 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()");
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
-        "Tensor context_lens, Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, "
-        "int Hkv, float scale, int num_splits) -> ()");
+        "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
+        "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
+        "int num_splits) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale) -> ()");

@@ -1,19 +1,24 @@
-// Paged decode attention (q_len = 1 per sequence), GQA, split-K over the context.
-// SURVEY.md §2.4 K7 — the bandwidth-critical kernel of a large-batch decode step.
+// Paged attention for decode and short extend rows (q_len small), GQA, split-K.
+// SURVEY.md §2.4 K7 — the bandwidth-critical kernel of a large-batch decode step,
+// also used for grammar jump-forward extends (a sampled token + the forced schema
+// tokens after it, q_len = 1 + k, k ~ 3-8).
 //
 // Design (gfx950, wave64):
-//   * one wave per (split, kv_head, sequence); the G query heads that share a kv
-//     head are the N=16 dimension of mfma_f32_16x16x32_bf16 (G <= 16), so each K/V
-//     byte is read exactly once per kv head.
+//   * one wave per (split, kv_head, work item); a work item is (sequence, column
+//     tile).  The 16 MFMA columns of mfma_f32_16x16x32_bf16 are (query, head)
+//     pairs c = query * G + head of one kv head: a decode row uses G columns, an
+//     extend row q_len * G (several column tiles if > 16).  Each K/V byte is read
+//     once per column tile, i.e. once per kv head for decode.
 //   * QK^T is computed swapped, S^T = K * Q^T: K fragments are 16-byte rows loaded
-//     straight from the page into VGPRs (no LDS round trip; Guideline "GEMV / M<=16").
-//     The result has one head per lane column, so the online-softmax state (running
-//     max, partial sum) is lane-local for its head.
+//     straight from the page into VGPRs (no LDS round trip; "GEMV / M<=16" row
+//     of the staging table).  The result has one column per lane, so the online
+//     softmax state (running max, partial sum) is lane-local; each column carries
+//     its own causal limit (key < kv_len - q_len + query + 1).
 //   * P*V is computed as O^T = V^T * P^T: the S^T accumulators are converted in
-//     place into the bf16 B operand (accumulator-as-operand, §3), V goes through LDS
-//     once and is read back with ds_read_b64_tr_b16 (T10) in the permuted key order
-//     the accumulator layout implies.  O^T keeps the head on the lane, so the
-//     softmax rescale needs no cross-lane traffic.
+//     place into the bf16 B operand (accumulator-as-operand, §3), V goes through
+//     LDS once and is read back with ds_read_b64_tr_b16 (T10) in the permuted key
+//     order the accumulator layout implies.  O^T keeps the column on the lane, so
+//     the softmax rescale needs no cross-lane traffic.
 //   * V's LDS image is XOR-swizzled (chunk ^ ((row&7)<<1)) so every transposed read
 //     of a 32-lane half touches 16 distinct 16-byte slots (conflict-free).
 //   * split-K partials (unnormalised O, running max, sum) are merged by
@@ -30,45 +35,54 @@ constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
 __global__ __launch_bounds__(64) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
-    int bt_stride, const int32_t* __restrict__ context_lens, bf16_t* __restrict__ out,
-    int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int Hq,
-    int Hkv, float scale_log2, int num_splits) {
+    int bt_stride, const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
+    const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
+    const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
+    int num_splits) {
   __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int split = blockIdx.x, kvh = blockIdx.y, w = blockIdx.z;
   const int lane = threadIdx.x;
   const int g = lane >> 4;   // 16-lane group
-  const int c = lane & 15;   // head column within the GQA group
+  const int c = lane & 15;   // MFMA column
   const int G = Hq / Hkv;
-  const int h = kvh * G + c;
-  const bool hvalid = c < G;
+  const int seq = work_seq[w];
+  if (seq < 0) return;       // padding work item (graph-captured buckets)
+  const int ql = seq_q_len[seq];
+  const int kvl = seq_kv_len[seq];
+  const int col = work_ct[w] * 16 + c;
+  const bool cvalid = col < ql * G;
+  const int qi = cvalid ? col / G : 0;
+  const int h = kvh * G + (cvalid ? col % G : 0);
+  const int qrow = seq_q_start[seq] + qi;
+  const int lim = kvl - ql + qi + 1;  // keys [0, lim) visible to this column
 
-  const int ctx = context_lens[b];
-  int tps = (ctx + num_splits - 1) / num_splits;
+  int tps = (kvl + num_splits - 1) / num_splits;
   tps = (tps + kPage - 1) / kPage * kPage;
   const int start = split * tps;
-  const int end = min(ctx, start + tps);
+  const int end = min(kvl, start + tps);
 
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) o[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (start < end) {
-    // Q^T fragments: B[k = dh][col = head]; lane holds Q[h][32ks + 8g .. +7]
+  if (start < end && ql > 0) {
+    // Q^T fragments: B[k = dh][col]; lane holds Q[qrow, h][32ks + 8g .. +7]
     s16x8 qf[4];
-    const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(hvalid ? h : kvh * G) * kD;
+    const bf16_t* qp = q + (int64_t)qrow * q_stride + (int64_t)h * kD;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      qf[ks] = reinterpret_cast<const s16x8*>(qrow + 32 * ks + 8 * g)[0];
-      if (!hvalid) qf[ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      qf[ks] = reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
+      if (!cvalid) qf[ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
     }
-    const int32_t* bt = block_tables + (int64_t)b * bt_stride;
+    const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
 
     for (int kt = start; kt < end; kt += kPage) {
       const int64_t page = bt[kt / kPage];
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
-      const int nvalid = end - kt;  // keys of this tile that exist (>= 1)
+      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
 
       // ---- issue K fragment loads (A operand: row = key, k = dh) ----
       s16x8 kf[2][4];
@@ -78,7 +92,7 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         for (int ks = 0; ks < 4; ++ks)
           kf[mt][ks] = reinterpret_cast<const s16x8*>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g)[0];
 
-      // ---- V tile -> LDS (swizzled), rows past the context zeroed ----
+      // ---- V tile -> LDS (swizzled), rows past the split/context zeroed ----
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = g + 4 * i, ch = c;
@@ -98,7 +112,7 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
           s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[mt][ks]), as_bf16x8(qf[ks]),
                                                           s[mt], 0, 0, 0);
       }
-      // lane holds S^T[key = 16mt + 4g + i][head c]
+      // lane holds S^T[key = 16mt + 4g + i][column c]
       float mx = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
@@ -106,19 +120,20 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         for (int i = 0; i < 4; ++i) {
           const int key = 16 * mt + 4 * g + i;
           float v = s[mt][i] * scale_log2;
-          if (key >= nvalid) v = -INFINITY;
+          if (key >= nvalid || kt + key >= lim) v = -INFINITY;
           s[mt][i] = v;
           mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = fast_exp2(m_run - m_new);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;  // fully-masked column so far
+      const float alpha = fast_exp2(m_run - m_use);
       float psum = 0.f;
       float p[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        p[j] = fast_exp2(s[j >> 2][j & 3] - m_new);
+        p[j] = fast_exp2(s[j >> 2][j & 3] - m_use);
         psum += p[j];
       }
       l_run = l_run * alpha + psum;
@@ -145,24 +160,24 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
     }
   }
 
-  // total softmax denominator for head c (lanes c, c+16, c+32, c+48)
+  // total softmax denominator for column c (lanes c, c+16, c+32, c+48)
   float l_tot = l_run;
   l_tot += __shfl_xor(l_tot, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
-  if (!hvalid) return;
+  if (!cvalid) return;
 
   if (num_splits == 1) {
     const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-    bf16_t* orow = out + (int64_t)b * out_stride + (int64_t)h * kD;
+    bf16_t* orow = out + (int64_t)qrow * out_stride + (int64_t)h * kD;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-      uint2 w;
-      w.x = pack_bf16x2(o[m][0] * inv, o[m][1] * inv);
-      w.y = pack_bf16x2(o[m][2] * inv, o[m][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = w;
+      uint2 wv;
+      wv.x = pack_bf16x2(o[m][0] * inv, o[m][1] * inv);
+      wv.y = pack_bf16x2(o[m][2] * inv, o[m][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
     }
   } else {
-    const int64_t pidx = ((int64_t)b * Hq + h) * num_splits + split;
+    const int64_t pidx = ((int64_t)qrow * Hq + h) * num_splits + split;
     float* po = part_o + pidx * kD;
 #pragma unroll
     for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[m];
@@ -173,7 +188,7 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
   }
 }
 
-// Merge split-K partials: one workgroup of 128 lanes (one per dh) per (seq, head).
+// Merge split-K partials: one workgroup of 128 lanes (one per dh) per (row, head).
 __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_ml,
     bf16_t* __restrict__ out, int64_t out_stride, int Hq, int num_splits) {
@@ -188,28 +203,32 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
     for (int s = 0; s < num_splits; ++s) {
       const float ms = ml[2 * s];
       if (ms == -INFINITY) continue;
-      const float w = fast_exp2(ms - gm);
-      num += w * part_o[((int64_t)bh * num_splits + s) * kD + d];
-      den += w * ml[2 * s + 1];
+      const float wgt = fast_exp2(ms - gm);
+      num += wgt * part_o[((int64_t)bh * num_splits + s) * kD + d];
+      den += wgt * ml[2 * s + 1];
     }
   }
   out[(int64_t)b * out_stride + (int64_t)h * kD + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
 
+// rows = number of q rows covered (for the split-K reduce), W = work items
 void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                         const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
-                        const int32_t* context_lens, bf16_t* out, int64_t out_stride,
-                        float* part_o, float* part_ml, int B, int Hq, int Hkv, float scale,
+                        const int32_t* seq_q_start, const int32_t* seq_q_len,
+                        const int32_t* seq_kv_len, const int32_t* work_seq,
+                        const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
+                        float* part_o, float* part_ml, int Hq, int Hkv, float scale,
                         int num_splits, hipStream_t s) {
-  if (B == 0) return;
+  if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_splits, Hkv, B);
+  dim3 grid(num_splits, Hkv, W);
   attn_decode_kernel<<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables, bt_stride,
-                                         context_lens, out, out_stride, part_o, part_ml, Hq, Hkv,
-                                         scale_log2, num_splits);
+                                         seq_q_start, seq_q_len, seq_kv_len, work_seq, work_ct,
+                                         out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
+                                         num_splits);
   if (num_splits > 1)
-    attn_decode_reduce_kernel<<<B * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
-                                                     num_splits);
+    attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
+                                                        num_splits);
 }
 
 }  // namespace rfq

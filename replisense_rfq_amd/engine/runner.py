@@ -1,13 +1,22 @@
 """Model runner: StepPlan -> one H2D metadata upload -> forward -> grammar-masked
 sampling -> one D2H of the sampled ids.
 
-* All step metadata (token ids, positions, KV slots, block tables, context
-  lengths, prefill work lists, logits rows, grammar mask rows, temperatures,
-  seeds) is packed into ONE pinned int32 buffer and copied with one async H2D.
-* Pure-decode steps whose batch fits a captured bucket replay a hipGraph
-  (torch.cuda.CUDAGraph on ROCm) holding the whole forward + sampler: ~L*12
-  kernel launches become one graph launch (SURVEY.md north star: "hipGraph-
-  captured decode steps shown in rocprof").
+A step's rows are laid out in two sections:
+
+  A  decode rows (q = 1) and short grammar jump-forward extends (q <= EXT_MAX):
+     paged split-K MFMA attention (csrc/kernels/attn_decode.hip), one work item
+     per (sequence, 16-column tile of q*G (query, head) pairs);
+  B  prompt prefill chunks: varlen causal flash attention (attn_prefill.hip).
+
+* All step metadata (token ids, positions, KV slots, block tables, per-sequence
+  q/kv lengths, work lists, logits rows, grammar mask rows, temperatures, seeds)
+  is packed into ONE pinned int32 buffer and copied with one async H2D.
+* Steps without a prefill section replay a hipGraph (torch.cuda.CUDAGraph on
+  ROCm) captured for a (sequence bucket NB, token bucket TB) pair; the graph
+  holds the whole forward + sampler and reads its metadata from a static device
+  buffer in the same layout, so the H2D copy is the only extra work.  Because
+  jump-forward extends live in section A, decode steps that also append forced
+  schema tokens stay on the graph path.
 * With tensor parallelism rank 0 owns the scheduler; it broadcasts the packed
   buffer (header + payload) to the TP workers, which run the identical forward;
   the vocab-parallel sampler all-gathers (value, index) partials (C3).
@@ -26,9 +35,13 @@ from ..parallel.tp import TPContext
 from .kv_cache import KVCache
 from .scheduler import StepPlan
 
-H_T, H_D, H_P, H_W, H_S, H_MAXB, H_GRAPH, H_SPLITS, H_PAYLOAD, H_STOP = range(10)
+(H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_GNB, H_GTB, H_SPLITS, H_PAYLOAD,
+ H_STOP) = range(13)
 HEADER = 16
 SAMPLE_SPLITS = 8
+EXT_MAX = 32                 # extends up to this many tokens use the decode kernel
+TOKEN_MULTS = (1, 2, 3, 4, 6, 8)
+MAX_GRAPH_TOKENS = 2048
 
 
 def _seed64(req_seed: int, pos: int) -> int:
@@ -36,6 +49,14 @@ def _seed64(req_seed: int, pos: int) -> int:
     x &= (1 << 64) - 1
     x ^= x >> 31
     return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def _layout(T, NA, WA, NB, WB, S, maxb):
+    """(name, length) of every int32 array in the payload, in order."""
+    return [("seeds", 2 * S), ("ids", T), ("pos", T), ("slots", T),
+            ("a_bt", NA * maxb), ("a_qs", NA), ("a_ql", NA), ("a_kvl", NA), ("a_ws", WA),
+            ("a_wct", WA), ("b_bt", NB * maxb), ("b_qs", NB), ("b_ql", NB), ("b_kvl", NB),
+            ("b_ws", WB), ("b_wq", WB), ("lidx", S), ("midx", S), ("temps", S)]
 
 
 @dataclass
@@ -54,120 +75,176 @@ class ModelRunner:
         self.tp = tp
         self.device = model.device
         self.is_cuda = self.device.type == "cuda"
+        self.G = model.hq // model.hkv
         self.mask_table = (torch.from_numpy(np.ascontiguousarray(mask_table)).to(self.device)
                            if mask_table is not None else
                            torch.zeros((1, (model.cfg.vocab_size + 31) // 32), dtype=torch.int32,
                                        device=self.device))
         self.max_blocks = (cfg.max_model_len + kv.block_size - 1) // kv.block_size
-        self.graphs: dict[int, tuple] = {}
-        self.graph_pool = None
+        self.graphs: dict[tuple, object] = {}
         self._pinned = None
+        self._dev = None
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0}
 
     # ---------------------------------------------------------------- packing
+    def _graph_key(self, NA: int, T: int):
+        if not self.graphs:
+            return None
+        for nb in self._nb_buckets:
+            if nb < NA:
+                continue
+            for m in TOKEN_MULTS:
+                tb = nb * m
+                if tb >= T and (nb, tb) in self.graphs:
+                    return nb, tb
+            return None
+        return None
+
     def pack(self, plan: StepPlan) -> Packed:
-        kv, bs = self.kv, self.kv.block_size
-        dec, ext = plan.decode, plan.extend
-        D = len(dec)
-        T = D + sum(q for _, q in ext)
-        P = len(ext)
-        ids = np.empty(T, np.int32)
-        pos = np.empty(T, np.int32)
-        slots = np.empty(T, np.int32)
-        maxb = max([len(s.blocks) for s in dec] + [len(s.blocks) for s, _ in ext] + [1])
-        graph_b = 0
-        if (self.is_cuda and self.cfg.use_graphs and P == 0 and D > 0 and self.graphs):
-            graph_b = next((b for b in sorted(self.graphs) if b >= D), 0)
-        if graph_b:
-            maxb = self.max_blocks
-        dbt = np.full((D, maxb), kv.scratch_block, np.int32)
-        dctx = np.empty(D, np.int32)
-        rows = []
-        for i, s in enumerate(dec):
-            p = s.num_cached
-            ids[i], pos[i], slots[i] = s.tokens[p], p, kv.slot(s, p)
-            dbt[i, : len(s.blocks)] = s.blocks
-            dctx[i] = p + 1
-            rows.append((s, s.pending == 1))
-        pbt = np.full((P, maxb), kv.scratch_block, np.int32)
-        pqs, pql, pkv = np.empty(P, np.int32), np.empty(P, np.int32), np.empty(P, np.int32)
-        ws, wq = [], []
-        t = D
-        ext_rows = []
-        for j, (s, q) in enumerate(ext):
+        kv, bs, G = self.kv, self.kv.block_size, self.G
+        secA = [(s, 1) for s in plan.decode] + [(s, q) for s, q in plan.extend if q <= EXT_MAX]
+        secB = [(s, q) for s, q in plan.extend if q > EXT_MAX]
+        TA = sum(q for _, q in secA)
+        T = TA + sum(q for _, q in secB)
+        NA, NB = len(secA), len(secB)
+        key = self._graph_key(NA, T) if (self.is_cuda and self.cfg.use_graphs and NB == 0) else None
+        if key:
+            nbk, tbk = key
+            TA_p, NA_p, WA_p, S_p, maxb = tbk, nbk, tbk, nbk, self.max_blocks
+        else:
+            maxb = max([len(s.blocks) for s, _ in secA + secB] + [1])
+        ids = np.zeros(T, np.int32)
+        pos = np.zeros(T, np.int32)
+        slots = np.full(T, -1, np.int32)
+        a_bt = np.full((NA, maxb), kv.scratch_block, np.int32)
+        a_qs, a_ql, a_kvl = (np.zeros(NA, np.int32) for _ in range(3))
+        a_ws, a_wct = [], []
+        rows, lidx = [], []
+        t = 0
+        for j, (s, q) in enumerate(secA):
             p0 = s.num_cached
             ids[t:t + q] = s.tokens[p0:p0 + q]
-            pos[t:t + q] = np.arange(p0, p0 + q)
-            blk = np.asarray(s.blocks, np.int64)
             pp = np.arange(p0, p0 + q)
+            pos[t:t + q] = pp
+            blk = np.asarray(s.blocks, np.int64)
             slots[t:t + q] = blk[pp // bs] * bs + pp % bs
-            pbt[j, : len(s.blocks)] = s.blocks
-            pqs[j], pql[j], pkv[j] = t - D, q, p0 + q
-            nb = (q + 31) // 32
-            ws += [j] * nb
-            wq += list(range(nb))
-            if p0 + q == len(s.tokens):
-                ext_rows.append((t + q - 1, s))
+            a_bt[j, : len(s.blocks)] = s.blocks
+            a_qs[j], a_ql[j], a_kvl[j] = t, q, p0 + q
+            nct = (q * G + 15) // 16
+            a_ws += [j] * nct
+            a_wct += list(range(nct))
+            lidx.append(t + q - 1)
+            rows.append((s, p0 + q == len(s.tokens)))
             t += q
-        # logits rows: all decode rows (graph computes them anyway), then finishing extends
-        lidx = list(range(D)) + [r for r, _ in ext_rows]
-        rows += [(s, True) for _, s in ext_rows]
+        b_bt = np.full((NB, maxb), kv.scratch_block, np.int32)
+        b_qs, b_ql, b_kvl = (np.zeros(NB, np.int32) for _ in range(3))
+        b_ws, b_wq = [], []
+        for j, (s, q) in enumerate(secB):
+            p0 = s.num_cached
+            ids[t:t + q] = s.tokens[p0:p0 + q]
+            pp = np.arange(p0, p0 + q)
+            pos[t:t + q] = pp
+            blk = np.asarray(s.blocks, np.int64)
+            slots[t:t + q] = blk[pp // bs] * bs + pp % bs
+            b_bt[j, : len(s.blocks)] = s.blocks
+            b_qs[j], b_ql[j], b_kvl[j] = t - TA, q, p0 + q
+            nqb = (q + 31) // 32
+            b_ws += [j] * nqb
+            b_wq += list(range(nqb))
+            if p0 + q == len(s.tokens):
+                lidx.append(t + q - 1)
+                rows.append((s, True))
+            t += q
         S = len(lidx)
-        midx = np.empty(S, np.int32)
-        temps = np.empty(S, np.float32)
-        seeds = np.empty(S, np.int64)
+        midx = np.full(S, -1, np.int32)
+        temps = np.zeros(S, np.float32)
+        seeds = np.zeros(S, np.int64)
         for k, (s, _) in enumerate(rows):
             midx[k] = s.mask_idx if s.params.grammar else -1
             temps[k] = s.params.temperature
             seeds[k] = _seed64(s.params.seed ^ (s.req_id * 0x632BE5AB), len(s.tokens))
-        splits = self._decode_splits(D, int(dctx.max()) if D else 0, graph_b)
-        # int64 seeds first so their view stays 8-byte aligned
-        parts = [seeds.view(np.int32), ids, pos, slots, dbt.reshape(-1), dctx, pbt.reshape(-1),
-                 pqs, pql, pkv, np.asarray(ws, np.int32), np.asarray(wq, np.int32),
-                 np.asarray(lidx, np.int32), midx, temps.view(np.int32)]
-        payload = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+        WA, WB = len(a_ws), len(b_ws)
+        arrays = dict(ids=ids, pos=pos, slots=slots, a_bt=a_bt, a_qs=a_qs, a_ql=a_ql,
+                      a_kvl=a_kvl, a_ws=np.asarray(a_ws, np.int32),
+                      a_wct=np.asarray(a_wct, np.int32), b_bt=b_bt, b_qs=b_qs, b_ql=b_ql,
+                      b_kvl=b_kvl, b_ws=np.asarray(b_ws, np.int32),
+                      b_wq=np.asarray(b_wq, np.int32), lidx=np.asarray(lidx, np.int32),
+                      midx=midx, temps=temps.view(np.int32), seeds=seeds.view(np.int32))
         header = np.zeros(HEADER, np.int32)
-        header[[H_T, H_D, H_P, H_W, H_S, H_MAXB, H_GRAPH, H_SPLITS, H_PAYLOAD]] = \
-            [T, D, P, len(ws), S, maxb, graph_b, splits, payload.size]
+        if key:
+            # pad every array to the captured bucket shape
+            pads = dict(ids=(TA_p, 0), pos=(TA_p, 0), slots=(TA_p, -1),
+                        a_qs=(NA_p, 0), a_ql=(NA_p, 0), a_kvl=(NA_p, 1),
+                        a_ws=(WA_p, -1), a_wct=(WA_p, 0), lidx=(S_p, 0), midx=(S_p, -1),
+                        temps=(S_p, 0), seeds=(2 * S_p, 0))
+            for name, (n, fill) in pads.items():
+                a = arrays[name]
+                if a.size < n:
+                    arrays[name] = np.concatenate([a, np.full(n - a.size, fill, np.int32)])
+            bt = np.full((NA_p, maxb), kv.scratch_block, np.int32)
+            bt[:NA] = a_bt
+            arrays["a_bt"] = bt
+            T_h, TA_h, NA_h, WA_h, S_h = TA_p, TA_p, NA_p, WA_p, S_p
+            splits = self._decode_splits(NA_p, 0, graph=True)
+            header[H_GNB], header[H_GTB] = key
+        else:
+            T_h, TA_h, NA_h, WA_h, S_h = T, TA, NA, WA, S
+            splits = self._decode_splits(NA, int(a_kvl.max()) if NA else 0, graph=False)
+        lay = _layout(T_h, NA_h, WA_h, NB, WB, S_h, maxb)
+        payload = np.concatenate([arrays[n].reshape(-1) for n, _ in lay])
+        header[[H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_SPLITS, H_PAYLOAD]] = \
+            [T_h, TA_h, NA_h, WA_h, NB, WB, S_h, maxb, splits, payload.size]
         return Packed(header, payload, rows)
 
-    def _decode_splits(self, D: int, max_ctx: int, graph_b: int) -> int:
-        if D == 0 or not self.is_cuda:
+    def _decode_splits(self, NA: int, max_ctx: int, graph: bool) -> int:
+        if NA == 0 or not self.is_cuda:
             return 1
-        n = graph_b or D
-        wg = n * self.model.hkv
+        wg = NA * self.model.hkv
         s = 1
         while wg * s < 1024 and s < 16:
             s *= 2
-        if not graph_b:
+        if not graph:
             s = max(1, min(s, (max_ctx + 255) // 256))
         return s
 
     # ------------------------------------------------------------- unpacking
     @staticmethod
-    def _views(buf: torch.Tensor, h: np.ndarray):
-        T, D, P, W, S, maxb = (int(h[i]) for i in (H_T, H_D, H_P, H_W, H_S, H_MAXB))
-        sizes = [2 * S, T, T, T, D * maxb, D, P * maxb, P, P, P, W, W, S, S, S]
-        out, o = [], 0
-        for n in sizes:
-            out.append(buf[o:o + n])
+    def _views(buf: torch.Tensor, h) -> dict:
+        T, TA, NA, WA, NB, WB, S, maxb = (int(h[i]) for i in (H_T, H_TA, H_NA, H_WA, H_NB, H_WB,
+                                                              H_S, H_MAXB))
+        out, o = {}, 0
+        for name, n in _layout(T, NA, WA, NB, WB, S, maxb):
+            out[name] = buf[o:o + n]
             o += n
-        (seeds, ids, pos, slots, dbt, dctx, pbt, pqs, pql, pkv, ws, wq, lidx, midx, temps) = out
-        return dict(ids=ids, pos=pos, slots=slots, dbt=dbt.view(D, maxb), dctx=dctx,
-                    pbt=pbt.view(P, maxb), pqs=pqs, pql=pql, pkv=pkv, ws=ws, wq=wq,
-                    lidx=lidx.long(), midx=midx, temps=temps.view(torch.float32),
-                    seeds=seeds.view(torch.int64))
+        out["a_bt"] = out["a_bt"].view(NA, maxb)
+        out["b_bt"] = out["b_bt"].view(NB, maxb)
+        out["seeds"] = out["seeds"].view(torch.int64)
+        out["temps"] = out["temps"].view(torch.float32)
+        out["lidx"] = out["lidx"]
+        return out
 
-    def _upload(self, header: np.ndarray, payload: np.ndarray) -> torch.Tensor:
+    def _meta(self, v, h) -> ForwardMeta:
+        T, TA = int(h[H_T]), int(h[H_TA])
+        return ForwardMeta(
+            input_ids=v["ids"], positions=v["pos"], slot_mapping=v["slots"], num_decode=TA,
+            dec_block_tables=v["a_bt"], dec_q_start=v["a_qs"], dec_q_len=v["a_ql"],
+            dec_kv_len=v["a_kvl"], dec_work_seq=v["a_ws"], dec_work_ct=v["a_wct"],
+            num_prefill_tokens=T - TA, pf_block_tables=v["b_bt"], pf_q_start=v["b_qs"],
+            pf_q_len=v["b_ql"], pf_kv_len=v["b_kvl"], work_seq=v["b_ws"], work_qblk=v["b_wq"],
+            logits_idx=v["lidx"], decode_splits=int(h[H_SPLITS]))
+
+    def _upload(self, payload: np.ndarray, dst: torch.Tensor | None = None) -> torch.Tensor:
         n = payload.size
         if not self.is_cuda:
             return torch.from_numpy(payload.copy())
         if self._pinned is None or self._pinned.numel() < n:
-            self._pinned = torch.empty(max(n, 1 << 20), dtype=torch.int32, pin_memory=True)
-            self._dev = torch.empty(max(n, 1 << 20), dtype=torch.int32, device=self.device)
+            size = max(n, 1 << 20)
+            self._pinned = torch.empty(size, dtype=torch.int32, pin_memory=True)
+            self._dev = torch.empty(size, dtype=torch.int32, device=self.device)
         self._pinned[:n].numpy()[:] = payload
-        self._dev[:n].copy_(self._pinned[:n], non_blocking=True)
-        return self._dev[:n]
+        dst = self._dev if dst is None else dst
+        dst[:n].copy_(self._pinned[:n], non_blocking=True)
+        return dst[:n]
 
     # ---------------------------------------------------------------- execute
     def execute(self, plan: StepPlan) -> tuple[list, np.ndarray]:
@@ -176,24 +253,26 @@ class ModelRunner:
         if self.tp.enabled:
             self._broadcast(pk.header, pk.payload)
         toks = self._run(pk.header, pk.payload)
-        return pk.rows, toks
+        return pk.rows, toks[: len(pk.rows)]
 
     def _broadcast(self, header, payload):
-        h = torch.from_numpy(header).to(self.device)
-        self.tp.group and torch.distributed.broadcast(h, src=0, group=self.tp.group)
+        dev = self.device if self.is_cuda else "cpu"
+        h = torch.from_numpy(header.copy()).to(dev)
+        torch.distributed.broadcast(h, src=0, group=self.tp.group)
         if payload.size:
-            p = torch.from_numpy(payload).to(self.device)
+            p = torch.from_numpy(payload.copy()).to(dev)
             torch.distributed.broadcast(p, src=0, group=self.tp.group)
 
     def worker_step(self) -> bool:
         """TP ranks > 0: receive one step from rank 0 and run it.  False = stop."""
-        h = torch.empty(HEADER, dtype=torch.int32, device=self.device)
+        dev = self.device if self.is_cuda else "cpu"
+        h = torch.empty(HEADER, dtype=torch.int32, device=dev)
         torch.distributed.broadcast(h, src=0, group=self.tp.group)
         header = h.cpu().numpy()
         if header[H_STOP]:
             return False
         n = int(header[H_PAYLOAD])
-        p = torch.empty(n, dtype=torch.int32, device=self.device)
+        p = torch.empty(n, dtype=torch.int32, device=dev)
         if n:
             torch.distributed.broadcast(p, src=0, group=self.tp.group)
         self._run(header, p.cpu().numpy())
@@ -207,33 +286,24 @@ class ModelRunner:
 
     def _run(self, header: np.ndarray, payload: np.ndarray) -> np.ndarray:
         t0 = time.perf_counter()
-        graph_b = int(header[H_GRAPH])
-        if graph_b:
-            out = self._run_graph(header, payload, graph_b)
+        key = (int(header[H_GNB]), int(header[H_GTB]))
+        if key[0]:
+            g, gbuf, out = self.graphs[key]
+            self._upload(payload, gbuf)
+            g.replay()
         else:
-            buf = self._upload(header, payload)
+            buf = self._upload(payload)
             v = self._views(buf, header)
-            meta = self._meta(v, header)
-            logits = self.model.forward(meta)
+            logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
         self.stats["steps"] += 1
-        self.stats["graph_steps"] += bool(graph_b)
+        self.stats["graph_steps"] += bool(key[0])
         self.stats["tokens"] += int(header[H_T])
         self.stats["forward_s"] += time.perf_counter() - t0
-        return toks[: int(header[H_S])]
+        return toks
 
-    def _meta(self, v, header) -> ForwardMeta:
-        D, P = int(header[H_D]), int(header[H_P])
-        T = int(header[H_T])
-        return ForwardMeta(
-            input_ids=v["ids"], positions=v["pos"], slot_mapping=v["slots"], num_decode=D,
-            dec_block_tables=v["dbt"], dec_context_lens=v["dctx"], num_prefill_tokens=T - D,
-            pf_block_tables=v["pbt"], pf_q_start=v["pqs"], pf_q_len=v["pql"],
-            pf_kv_len=v["pkv"], work_seq=v["ws"], work_qblk=v["wq"], logits_idx=v["lidx"],
-            decode_splits=int(header[H_SPLITS]))
-
-    def _sample(self, logits, midx, temps, seeds, out=None, parts=None):
+    def _sample(self, logits, midx, temps, seeds, out=None):
         S = logits.shape[0]
         if not logits.is_cuda:
             mt = self.mask_table.cpu()
@@ -243,16 +313,11 @@ class ModelRunner:
                 alli = [torch.empty_like(idx) for _ in range(self.tp.world)]
                 torch.distributed.all_gather(allv, vals, group=self.tp.group)
                 torch.distributed.all_gather(alli, idx, group=self.tp.group)
-                V = torch.stack(allv)
-                I = torch.stack(alli)
-                best = V.argmax(0)
-                idx = I.gather(0, best[None])[0]
+                best = torch.stack(allv).argmax(0)
+                idx = torch.stack(alli).gather(0, best[None])[0]
             return idx
-        if parts is None:
-            pv = torch.empty((1, S, SAMPLE_SPLITS), dtype=torch.float32, device=self.device)
-            pi = torch.empty((1, S, SAMPLE_SPLITS), dtype=torch.int32, device=self.device)
-        else:
-            pv, pi = parts
+        pv = torch.empty((1, S, SAMPLE_SPLITS), dtype=torch.float32, device=self.device)
+        pi = torch.empty((1, S, SAMPLE_SPLITS), dtype=torch.int32, device=self.device)
         out = torch.empty(S, dtype=torch.int32, device=self.device) if out is None else out
         ops.sample_partial(logits, self.model.vocab_start, self.mask_table, midx, temps, seeds,
                            pv[0], pi[0])
@@ -270,37 +335,34 @@ class ModelRunner:
 
     # ----------------------------------------------------------------- graphs
     def capture_graphs(self, buckets) -> float:
-        """Capture decode+sample graphs for each batch bucket (largest first)."""
+        """Capture forward+sample graphs for (NB, TB) buckets, largest first."""
         if not self.is_cuda or not self.cfg.use_graphs:
             return 0.0
         t0 = time.perf_counter()
-        Bmax = max(buckets)
-        mb = self.max_blocks
-        dev = self.device
-        i32 = dict(dtype=torch.int32, device=dev)
-        st = dict(ids=torch.zeros(Bmax, **i32), pos=torch.zeros(Bmax, **i32),
-                  slots=torch.full((Bmax,), -1, **i32),
-                  dbt=torch.full((Bmax, mb), self.kv.scratch_block, **i32),
-                  dctx=torch.ones(Bmax, **i32), midx=torch.full((Bmax,), -1, **i32),
-                  temps=torch.zeros(Bmax, dtype=torch.float32, device=dev),
-                  seeds=torch.zeros(Bmax, dtype=torch.int64, device=dev),
-                  out=torch.zeros(Bmax, **i32))
-        self._gstatic = st
-        self._gparts = (torch.empty((1, Bmax, SAMPLE_SPLITS), dtype=torch.float32, device=dev),
-                        torch.empty((1, Bmax, SAMPLE_SPLITS), dtype=torch.int32, device=dev))
+        self._nb_buckets = sorted(buckets)
+        keys = [(nb, nb * m) for nb in self._nb_buckets for m in TOKEN_MULTS
+                if nb * m <= max(MAX_GRAPH_TOKENS, nb)]
+        maxb = self.max_blocks
         pool = torch.cuda.graph_pool_handle()
-        for B in sorted(buckets, reverse=True):
-            splits = self._decode_splits(B, 0, B)
-            meta = ForwardMeta(input_ids=st["ids"][:B], positions=st["pos"][:B],
-                               slot_mapping=st["slots"][:B], num_decode=B,
-                               dec_block_tables=st["dbt"][:B], dec_context_lens=st["dctx"][:B],
-                               logits_idx=None, decode_splits=splits)
-            parts = (self._gparts[0][:, :B], self._gparts[1][:, :B])
+        for nb, tb in sorted(keys, key=lambda k: (-k[1], -k[0])):
+            header = np.zeros(HEADER, np.int32)
+            header[[H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_SPLITS]] = \
+                [tb, tb, nb, tb, 0, 0, nb, maxb, self._decode_splits(nb, 0, graph=True)]
+            n = sum(k for _, k in _layout(tb, nb, tb, 0, 0, nb, maxb))
+            gbuf = torch.zeros(n, dtype=torch.int32, device=self.device)
+            v = self._views(gbuf, header)
+            # a harmless padding state for the capture run: no sequences, no KV writes
+            v["slots"].fill_(-1)
+            v["a_ws"].fill_(-1)
+            v["a_kvl"].fill_(1)
+            v["midx"].fill_(-1)
+            v["a_bt"].fill_(self.kv.scratch_block)
+            meta = self._meta(v, header)
+            out = torch.zeros(nb, dtype=torch.int32, device=self.device)
 
             def body():
                 logits = self.model.forward(meta)
-                self._sample(logits, st["midx"][:B], st["temps"][:B], st["seeds"][:B],
-                             out=st["out"][:B], parts=parts)
+                self._sample(logits, v["midx"], v["temps"], v["seeds"], out=out)
 
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -310,35 +372,6 @@ class ModelRunner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 body()
-            self.graphs[B] = (g, splits)
+            self.graphs[(nb, tb)] = (g, gbuf, out)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
-
-    def _run_graph(self, header, payload, B):
-        v = self._views(torch.from_numpy(payload), header)
-        D = int(header[H_D])
-        st = self._gstatic
-        # stage on host, one H2D per static buffer slice (rows >= D are padding)
-        host = np.zeros(0, np.int32)
-        ids = np.zeros(B, np.int32); ids[:D] = v["ids"].numpy()
-        pos = np.zeros(B, np.int32); pos[:D] = v["pos"].numpy()
-        slots = np.full(B, -1, np.int32); slots[:D] = v["slots"].numpy()
-        dctx = np.ones(B, np.int32); dctx[:D] = v["dctx"].numpy()
-        midx = np.full(B, -1, np.int32); midx[:D] = v["midx"].numpy()[:D]
-        temps = np.zeros(B, np.float32); temps[:D] = v["temps"].numpy()[:D]
-        seeds = np.zeros(B, np.int64); seeds[:D] = v["seeds"].numpy()[:D]
-        dbt = np.full((B, self.max_blocks), self.kv.scratch_block, np.int32)
-        dbt[:D] = v["dbt"].numpy()
-        host = np.concatenate([seeds.view(np.int32), ids, pos, slots, dctx, midx,
-                               temps.view(np.int32), dbt.reshape(-1)])
-        buf = self._upload(header, host)
-        st["seeds"][:B].copy_(buf[: 2 * B].view(torch.int64))
-        o = 2 * B
-        for name, n in (("ids", B), ("pos", B), ("slots", B), ("dctx", B), ("midx", B)):
-            st[name][:B].copy_(buf[o:o + n])
-            o += n
-        st["temps"][:B].copy_(buf[o:o + B].view(torch.float32)); o += B
-        st["dbt"][:B].copy_(buf[o:o + B * self.max_blocks].view(B, self.max_blocks))
-        g, _ = self.graphs[B]
-        g.replay()
-        return st["out"][:D]

@@ -6,8 +6,9 @@ MLP).  A forward pass consumes a *mixed* token batch laid out as
 
   embed -> for each layer:
      fused_add_rms_norm -> QKV GEMM (hipBLASLt) -> rope_kv (q in place, k/v into
-     the paged cache) -> attn_decode (split-K MFMA, decode rows) + attn_prefill
-     (varlen causal MFMA flash, extend rows) -> O GEMM -> [all-reduce]
+     the paged cache) -> attn_decode (split-K MFMA; decode rows and short grammar
+     jump-forward extends) + attn_prefill (varlen causal MFMA flash; prompt
+     chunks) -> O GEMM -> [all-reduce]
      -> fused_add_rms_norm -> gate|up GEMM -> silu_mul -> down GEMM -> [all-reduce]
         (MoE: router -> top-2 -> align -> grouped MFMA GEMMs -> combine)
   -> final norm on the rows that need logits -> vocab-parallel LM head.
@@ -39,9 +40,13 @@ class ForwardMeta:
     input_ids: torch.Tensor            # [T]
     positions: torch.Tensor            # [T]
     slot_mapping: torch.Tensor         # [T]
-    num_decode: int                    # first num_decode rows are q_len=1 sequences
-    dec_block_tables: torch.Tensor | None = None   # [D, maxb]
-    dec_context_lens: torch.Tensor | None = None   # [D]
+    num_decode: int                    # rows [0, num_decode): decode + short-extend section
+    dec_block_tables: torch.Tensor | None = None   # [NA, maxb]
+    dec_q_start: torch.Tensor | None = None        # [NA] first row of each sequence
+    dec_q_len: torch.Tensor | None = None          # [NA]
+    dec_kv_len: torch.Tensor | None = None         # [NA]
+    dec_work_seq: torch.Tensor | None = None       # [WA] (-1 = padding)
+    dec_work_ct: torch.Tensor | None = None        # [WA] 16-column tile index
     num_prefill_tokens: int = 0
     pf_block_tables: torch.Tensor | None = None    # [P, maxb]
     pf_q_start: torch.Tensor | None = None         # [P] offset inside the prefill rows
@@ -119,8 +124,9 @@ class DecoderLM:
             ops.rope_kv(qkv, m.positions, self.cos_sin, m.slot_mapping, kc, vc, hq, hkv)
             if D > 0:
                 po, pm = dec_parts if dec_parts is not None else (attn, attn)
-                ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_context_lens,
-                                attn[:D], po, pm, hq, hkv, self.scale,
+                ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
+                                m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
+                                hq, hkv, self.scale,
                                 m.decode_splits if dec_parts is not None else 1)
             if m.num_prefill_tokens > 0:
                 ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,

@@ -73,14 +73,16 @@ def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
         ref.rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
-                Hq, Hkv, scale, num_splits=1):
+def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq, work_ct,
+                out, part_o, part_ml, Hq, Hkv, scale, num_splits=1):
+    """Paged attention for decode / short-extend rows (see csrc/kernels/attn_decode.hip)."""
     if _gpu(q):
-        _native.ops().attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o,
-                                  part_ml, Hq, Hkv, scale, num_splits)
+        _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
+                                  work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
+                                  num_splits)
     else:
-        ref.attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
-                        Hq, Hkv, scale, num_splits)
+        ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
+                         out, Hq, Hkv, scale)
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,

@@ -83,21 +83,6 @@ def _gather_kv(cache, block_table, n: int):
     return pages.permute(1, 0, 2, 3).reshape(cache.shape[1], nb * BS, -1)[:, :n]
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, context_lens, out, part_o, part_ml,
-                Hq: int, Hkv: int, scale: float, num_splits: int = 1) -> None:
-    B = out.shape[0]
-    G = Hq // Hkv
-    for b in range(B):
-        n = int(context_lens[b])
-        k = _gather_kv(k_cache, block_tables[b], n).float()   # [Hkv, n, D]
-        v = _gather_kv(v_cache, block_tables[b], n).float()
-        qb = q[b, : Hq * 128].view(Hkv, G, 128).float()
-        s = torch.einsum("hgd,hnd->hgn", qb, k) * scale
-        p = torch.softmax(s, -1)
-        o = torch.einsum("hgn,hnd->hgd", p, v)
-        out[b, : Hq * 128].copy_(o.reshape(-1).to(out.dtype))
-
-
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
                  work_seq, work_qblk, out, Hq: int, Hkv: int, scale: float) -> None:
     G = Hq // Hkv

@@ -89,11 +89,15 @@ def test_graph_replay_matches_eager_forward(gpu):
     i32 = dict(dtype=torch.int32, device=gpu)
     st = dict(ids=torch.zeros(B, **i32), pos=torch.zeros(B, **i32),
               slots=torch.zeros(B, **i32), bt=torch.zeros(B, 8, **i32), ctx=torch.ones(B, **i32))
+    ar = torch.arange(B, **i32)
+    one = torch.ones(B, **i32)
+    zero = torch.zeros(B, **i32)
 
     def meta():
         return ForwardMeta(input_ids=st["ids"], positions=st["pos"], slot_mapping=st["slots"],
-                           num_decode=B, dec_block_tables=st["bt"], dec_context_lens=st["ctx"],
-                           decode_splits=4)
+                           num_decode=B, dec_block_tables=st["bt"], dec_q_start=ar,
+                           dec_q_len=one, dec_kv_len=st["ctx"], dec_work_seq=ar,
+                           dec_work_ct=zero, decode_splits=4)
 
     def fill(seed):
         g = torch.Generator().manual_seed(seed)

@@ -107,22 +107,35 @@ def _block_tables(lens, nblocks, device, seed=0):
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
 @pytest.mark.parametrize("splits", [1, 4])
 def test_attn_decode(gpu, Hq, Hkv, splits):
+    """Decode rows (q=1) and short extend rows (q>1, causal inside the extend)."""
     torch.manual_seed(4)
-    lens = [1, 31, 32, 33, 700, 129, 2049]
-    B = len(lens)
+    G = Hq // Hkv
+    cases = [(1, 1), (1, 31), (1, 32), (1, 33), (1, 700), (5, 129), (9, 2049), (3, 3), (1, 64)]
+    qlens = [c[0] for c in cases]
+    kvlens = [c[1] for c in cases]
     k, v = _paged_cache(512, Hkv, gpu, seed=5)
-    bt = _block_tables(lens, 512, gpu)
-    cl = torch.tensor(lens, dtype=torch.int32, device=gpu)
-    q = torch.randn(B, Hq * 128, device=gpu, dtype=BF)
-    out = torch.empty(B, Hq * 128, device=gpu, dtype=BF)
-    po = torch.empty(B * Hq * splits * 128, device=gpu)
-    pm = torch.empty(B * Hq * splits * 2, device=gpu)
+    bt = _block_tables(kvlens, 512, gpu)
+    T = sum(qlens)
+    qs = [sum(qlens[:i]) for i in range(len(qlens))]
+    ws, wct = [], []
+    for i, ql in enumerate(qlens):
+        for ct in range((ql * G + 15) // 16):
+            ws.append(i)
+            wct.append(ct)
+    ws.append(-1)          # a padding work item must be ignored
+    wct.append(0)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
+    q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
+    out = torch.empty(T, Hq * 128, device=gpu, dtype=BF)
+    po = torch.empty(T * Hq * splits * 128, device=gpu)
+    pm = torch.empty(T * Hq * splits * 2, device=gpu)
     scale = 1 / math.sqrt(128)
-    ops.attn_decode(q, k, v, bt, cl, out, po, pm, Hq, Hkv, scale, splits)
-    exp_c = torch.empty(out.shape, dtype=BF)
-    ref.attn_decode(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), cl.cpu(), exp_c, None, None, Hq, Hkv,
-                    scale)
-    _close(out, exp_c, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits}")
+    ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct), out, po,
+                    pm, Hq, Hkv, scale, splits)
+    exp = torch.zeros(T, Hq * 128, dtype=BF)
+    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
+                     torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
+    _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits}")
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
