@@ -33,9 +33,9 @@ import torch
 import torch.distributed as dist
 
 from replisense_rfq_amd.engine.engine import LLMEngine
-from replisense_rfq_amd.engine.sequence import SamplingParams
 from replisense_rfq_amd.parallel.tp import init_distributed, split_groups
 from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
+from replisense_rfq_amd.service.hints import estimate_line_items
 from replisense_rfq_amd.utils import synth
 from replisense_rfq_amd.utils.config import EngineConfig
 
@@ -80,10 +80,10 @@ class Replica:
         msgs = [build_messages(d.text) for d in docs]
         prompts = [self.tok.chat_ids(m) for m in msgs]
         eng = self.engine
-        params = SamplingParams(temperature=eng.cfg.temperature, max_tokens=eng.cfg.max_tokens,
-                                grammar=eng.grammar is not None)
-        seqs = eng.generate(prompts, params, seeds=[hash((self.wave, i)) & 0xFFFF
-                                                    for i in range(n)])
+        params = [eng.default_params(seed=(self.wave * 100_003 + i) & 0xFFFFFF,
+                                     min_items=estimate_line_items(d.text))
+                  for i, d in enumerate(docs)]
+        seqs = eng.generate(prompts, params)
         ok = 0
         for s in seqs:
             out = parse_and_validate_response(eng.decode_text(s), "direct_text_input")
@@ -104,7 +104,7 @@ class Replica:
             d = synth.make_rfq(10_000_000 + self.dp_rank * 1000 + i)
             t0 = time.perf_counter()
             ids = self.tok.chat_ids(build_messages(d.text))
-            s, = eng.generate([ids])
+            s, = eng.generate([ids], eng.default_params(min_items=estimate_line_items(d.text)))
             parse_and_validate_response(eng.decode_text(s), "direct_text_input")
             out.append(time.perf_counter() - t0)
             eng.runner.tp.enabled and eng.shutdown()

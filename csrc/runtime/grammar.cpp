@@ -2,18 +2,21 @@
 
 namespace rfqrt {
 
-State Grammar::enter(int32_t pc, int32_t cnt, int32_t sub) const {
+State Grammar::enter(int32_t pc, int32_t cnt, int32_t minv, int32_t sub) const {
   const Op& op = ops[pc];
-  if (op.code == OP_STR) return State{pc, 0, cnt, op.a};
-  return State{pc, sub, cnt, 0};
+  if (op.code == OP_STR) return State{pc, 0, cnt, op.a, minv};
+  return State{pc, sub, cnt, 0, minv};
 }
 
-int Grammar::enabled(int32_t ci, int32_t cnt, const Alt** out) const {
+int Grammar::enabled(int32_t ci, int32_t cnt, int32_t minv, const Alt** out) const {
   int n = 0;
   const int32_t lim = max_items[ci];
+  const bool at_max = lim > 0 && cnt >= lim;
+  const bool below_min = !at_max && honors_min[ci] && cnt < minv;
   for (int32_t i = choice_off[ci]; i < choice_off[ci + 1]; ++i) {
     const Alt& a = alts[i];
-    if (lim > 0 && cnt >= lim && a.is_continue) continue;
+    if (at_max && a.is_continue) continue;
+    if (below_min && a.is_close) continue;
     out[n++] = &a;
   }
   return n;
@@ -26,7 +29,7 @@ void Grammar::take(const Alt& a, State& st, std::vector<int32_t>& forced, bool s
   int32_t cnt = st.cnt;
   if (a.cnt == CNT_SET1) cnt = 1;
   else if (a.cnt == CNT_INC) cnt += 1;
-  st = enter(a.target, cnt);
+  st = enter(a.target, cnt, st.minv);
 }
 
 void Grammar::settle(State& st, std::vector<int32_t>& forced) const {
@@ -38,22 +41,22 @@ void Grammar::settle(State& st, std::vector<int32_t>& forced) const {
         const auto& off = st.sub ? lit1_off : lit_off;
         const auto& tok = st.sub ? lit1_tok : lit_tok;
         forced.insert(forced.end(), tok.begin() + off[op.a], tok.begin() + off[op.a + 1]);
-        st = enter(st.pc + 1, st.cnt);
+        st = enter(st.pc + 1, st.cnt, st.minv);
         break;
       }
       case OP_CHOICE: {
-        if (enabled(op.a, st.cnt, en) != 1) return;
+        if (enabled(op.a, st.cnt, st.minv, en) != 1) return;
         take(*en[0], st, forced, false);
         break;
       }
       case OP_STR:
         if (st.rem > 0) return;
         forced.push_back(quote);
-        st = enter(st.pc + 1, st.cnt);
+        st = enter(st.pc + 1, st.cnt, st.minv);
         break;
       case OP_NUM:
         if (st.sub == 5 || (st.sub == 4 && op.a != NUM_DEC)) {
-          st = enter(st.pc + 1, st.cnt);
+          st = enter(st.pc + 1, st.cnt, st.minv);
           break;
         }
         return;
@@ -63,8 +66,8 @@ void Grammar::settle(State& st, std::vector<int32_t>& forced) const {
   }
 }
 
-State Grammar::initial(std::vector<int32_t>& forced) const {
-  State st = enter(start_pc, 0);
+State Grammar::initial(std::vector<int32_t>& forced, int32_t min_items) const {
+  State st = enter(start_pc, 0, min_items);
   settle(st, forced);
   return st;
 }
@@ -90,7 +93,7 @@ bool Grammar::num(const Op& op, State& st, int32_t token, std::vector<int32_t>& 
   if (ph == 0) {
     if (nullable && token == null_first) {
       forced.insert(forced.end(), null_rest.begin(), null_rest.end());
-      st = enter(st.pc + 1, st.cnt);
+      st = enter(st.pc + 1, st.cnt, st.minv);
       return true;
     }
     if (!is_dig) return false;
@@ -105,7 +108,7 @@ bool Grammar::num(const Op& op, State& st, int32_t token, std::vector<int32_t>& 
     return true;
   }
   if ((ph == 1 || ph == 3 || ph == 4) && token == end_tok[e]) {
-    st = enter(st.pc + 1, st.cnt, 1);
+    st = enter(st.pc + 1, st.cnt, st.minv, 1);
     return true;
   }
   if (kind == NUM_DEC && (ph == 1 || ph == 4) && token == dot) {
@@ -134,13 +137,13 @@ bool Grammar::advance(State& st, int32_t token, std::vector<int32_t>& forced) co
   switch (op.code) {
     case OP_CHOICE: {
       const Alt* en[16];
-      const int n = enabled(op.a, s.cnt, en);
+      const int n = enabled(op.a, s.cnt, s.minv, en);
       for (int i = 0; i < n; ++i)
         if (en[i]->first == token) { take(*en[i], s, forced, true); ok = true; break; }
       break;
     }
     case OP_STR:
-      if (token == quote) { s = enter(s.pc + 1, s.cnt); ok = true; }
+      if (token == quote) { s = enter(s.pc + 1, s.cnt, s.minv); ok = true; }
       else if (token >= 0 && token < (int32_t)tok_class.size() && (tok_class[token] & 1)) {
         s.rem -= tok_chars[token] > 0 ? tok_chars[token] : 1;
         ok = true;

@@ -16,9 +16,10 @@ enum NumKind : int32_t { NUM_INT = 0, NUM_DEC = 1, NUM_FRAC = 2 };
 enum CntOp : int32_t { CNT_NONE = 0, CNT_SET1 = 1, CNT_INC = 2 };
 
 struct Op { int32_t code, a, b, c, d; };
-struct Alt { int32_t first, rest_off, rest_len, target, cnt, is_continue; };
+struct Alt { int32_t first, rest_off, rest_len, target, cnt, is_continue, is_close; };
 
-struct State { int32_t pc, sub, cnt, rem; };
+// minv: the request's minimum line-item count (schema hint for choices that honor it)
+struct State { int32_t pc, sub, cnt, rem, minv; };
 
 class Grammar {
  public:
@@ -27,7 +28,7 @@ class Grammar {
   std::vector<int32_t> choice_off;                             // CSR into alts
   std::vector<Alt> alts;
   std::vector<int32_t> alt_rest;                               // rest tokens of alternatives
-  std::vector<int32_t> choice_mask, choice_mask_close, max_items;
+  std::vector<int32_t> choice_mask, choice_mask_close, max_items, honors_min;
   std::vector<int32_t> num_masks;                              // [3 kinds][5 phases][3 end][2 null]
   std::vector<int32_t> null_rest;
   std::vector<uint8_t> tok_class, tok_chars, tok_digits;
@@ -35,16 +36,16 @@ class Grammar {
   int32_t end_tok[3] = {-1, -1, -1};
   int32_t start_pc = 0;
 
-  State initial(std::vector<int32_t>& forced) const;
+  State initial(std::vector<int32_t>& forced, int32_t min_items = 0) const;
   // Consume a sampled token.  Returns false if the token is illegal (state unchanged).
   bool advance(State& st, int32_t token, std::vector<int32_t>& forced) const;
   int32_t mask(const State& st) const;  // -1 when finished
   bool done(const State& st) const { return ops[st.pc].code == OP_END; }
 
  private:
-  State enter(int32_t pc, int32_t cnt, int32_t sub = 0) const;
+  State enter(int32_t pc, int32_t cnt, int32_t minv, int32_t sub = 0) const;
   void settle(State& st, std::vector<int32_t>& forced) const;
-  int enabled(int32_t ci, int32_t cnt, const Alt** out) const;
+  int enabled(int32_t ci, int32_t cnt, int32_t minv, const Alt** out) const;
   void take(const Alt& a, State& st, std::vector<int32_t>& forced, bool sampled) const;
   bool num(const Op& op, State& st, int32_t token, std::vector<int32_t>& forced) const;
 };

@@ -29,12 +29,14 @@ static Grammar* make_grammar(const py::dict& d) {
   g->lit1_tok = vec<int32_t>(d, "lit1_tok");
   g->choice_off = vec<int32_t>(d, "choice_off");
   auto alts = vec<int32_t>(d, "alts");
-  for (size_t i = 0; i + 6 <= alts.size(); i += 6)
-    g->alts.push_back(Alt{alts[i], alts[i + 1], alts[i + 2], alts[i + 3], alts[i + 4], alts[i + 5]});
+  for (size_t i = 0; i + 7 <= alts.size(); i += 7)
+    g->alts.push_back(Alt{alts[i], alts[i + 1], alts[i + 2], alts[i + 3], alts[i + 4], alts[i + 5],
+                          alts[i + 6]});
   g->alt_rest = vec<int32_t>(d, "alt_rest");
   g->choice_mask = vec<int32_t>(d, "choice_mask");
   g->choice_mask_close = vec<int32_t>(d, "choice_mask_close");
   g->max_items = vec<int32_t>(d, "max_items");
+  g->honors_min = vec<int32_t>(d, "honors_min");
   g->num_masks = vec<int32_t>(d, "num_masks");
   g->null_rest = vec<int32_t>(d, "null_rest");
   g->tok_class = vec<uint8_t>(d, "tok_class");
@@ -51,30 +53,30 @@ PYBIND11_MODULE(_runtime, m) {
 
   py::class_<Grammar>(m, "Grammar")
       .def(py::init(&make_grammar))
-      .def("initial", [](const Grammar& g) {
+      .def("initial", [](const Grammar& g, int32_t min_items) {
         std::vector<int32_t> forced;
-        State s = g.initial(forced);
-        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem), forced);
-      })
+        State s = g.initial(forced, min_items);
+        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem, s.minv), forced);
+      }, py::arg("min_items") = 0)
       .def("advance", [](const Grammar& g, py::tuple st, int32_t tok) {
         State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
-                st[3].cast<int32_t>()};
+                st[3].cast<int32_t>(), st[4].cast<int32_t>()};
         std::vector<int32_t> forced;
         if (!g.advance(s, tok, forced)) throw py::value_error("token not allowed by grammar");
-        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem), forced);
+        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem, s.minv), forced);
       })
       .def("mask", [](const Grammar& g, py::tuple st) {
         State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
-                st[3].cast<int32_t>()};
+                st[3].cast<int32_t>(), st[4].cast<int32_t>()};
         return g.mask(s);
       })
-      // states: int32 [n, 4] updated in place; tokens: int32 [n]
+      // states: int32 [n, 5] updated in place; tokens: int32 [n]
       // returns (mask_idx[n] (-1 = finished), forced_offsets[n+1], forced_tokens, ok[n])
       .def("batch_advance", [](const Grammar& g, py::array_t<int32_t, py::array::c_style> states,
                                arr<int32_t> tokens) {
         const py::ssize_t n = tokens.size();
-        if (states.ndim() != 2 || states.shape(0) != n || states.shape(1) != 4)
-          throw py::value_error("states must be int32 [n, 4]");
+        if (states.ndim() != 2 || states.shape(0) != n || states.shape(1) != 5)
+          throw py::value_error("states must be int32 [n, 5]");
         auto S = states.mutable_unchecked<2>();
         const int32_t* tk = tokens.data();
         py::array_t<int32_t> masks(n), offs(n + 1);
@@ -88,10 +90,10 @@ PYBIND11_MODULE(_runtime, m) {
           py::gil_scoped_release nogil;
           for (py::ssize_t i = 0; i < n; ++i) {
             O(i) = (int32_t)forced.size();
-            State s{S(i, 0), S(i, 1), S(i, 2), S(i, 3)};
+            State s{S(i, 0), S(i, 1), S(i, 2), S(i, 3), S(i, 4)};
             const bool good = g.advance(s, tk[i], forced);
             K(i) = good;
-            S(i, 0) = s.pc; S(i, 1) = s.sub; S(i, 2) = s.cnt; S(i, 3) = s.rem;
+            S(i, 0) = s.pc; S(i, 1) = s.sub; S(i, 2) = s.cnt; S(i, 3) = s.rem; S(i, 4) = s.minv;
             M(i) = g.mask(s);
           }
           O(n) = (int32_t)forced.size();

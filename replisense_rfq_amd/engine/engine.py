@@ -106,7 +106,7 @@ class LLMEngine:
             params.max_tokens = max(1, self.cfg.max_model_len - len(prompt_ids))
         seq = Sequence(list(prompt_ids), params, callback=callback)
         if params.grammar and self.grammar is not None:
-            seq.gstate, forced = self.grammar.initial()
+            seq.gstate, forced = self.grammar.initial(params.min_items)
             seq.tokens += forced
             seq.num_forced += len(forced)
             seq.mask_idx = self.grammar.mask(seq.gstate)
@@ -135,7 +135,7 @@ class LLMEngine:
         finished: list[Sequence] = []
         gseqs = [(s, t) for s, t in samp if s.gstate is not None]
         if gseqs:
-            states = np.array([s.gstate for s, _ in gseqs], np.int32).reshape(-1, 4)
+            states = np.array([s.gstate for s, _ in gseqs], np.int32).reshape(-1, 5)
             tokens = np.array([t for _, t in gseqs], np.int32)
             masks, offs, forced, ok = self.grammar.batch_advance(states, tokens)
             for i, (s, t) in enumerate(gseqs):
@@ -179,21 +179,27 @@ class LLMEngine:
     def has_work(self) -> bool:
         return self.scheduler.has_work
 
-    def generate(self, prompts: list[list[int]], params: SamplingParams | None = None,
+    def generate(self, prompts: list[list[int]], params=None,
                  seeds: list[int] | None = None) -> list[Sequence]:
+        """Blocking batch generation.  `params`: one SamplingParams for all, or a list."""
         seqs = []
         for i, p in enumerate(prompts):
-            sp = None
-            if params is not None or seeds is not None:
-                base = params or SamplingParams(temperature=self.cfg.temperature,
-                                                max_tokens=self.cfg.max_tokens,
-                                                grammar=self.grammar is not None)
-                sp = SamplingParams(base.temperature, base.max_tokens,
-                                    seeds[i] if seeds else base.seed, base.grammar)
+            sp = params[i] if isinstance(params, (list, tuple)) else params
+            if seeds is not None:
+                base = sp or self.default_params()
+                sp = SamplingParams(base.temperature, base.max_tokens, seeds[i], base.grammar,
+                                    base.min_items)
             seqs.append(self.add_request(p, sp))
         while self.has_work():
             self.step()
         return seqs
+
+    def default_params(self, **kw) -> SamplingParams:
+        p = SamplingParams(temperature=self.cfg.temperature, max_tokens=self.cfg.max_tokens,
+                           grammar=self.grammar is not None)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
 
     def decode_text(self, seq: Sequence) -> str:
         return self.tokenizer.decode(seq.output_ids)

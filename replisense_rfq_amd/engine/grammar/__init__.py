@@ -4,9 +4,11 @@
 the native C++ automaton (csrc/runtime/grammar.cpp) when the runtime module is
 built, else the Python twin (:mod:`.fsm`).  Both expose::
 
-    initial() -> (state, forced_tokens)
+    initial(min_items=0) -> (state, forced_tokens)
     advance(state, token) -> (state, forced_tokens)
-    batch_advance(states[n,4], tokens[n]) -> (mask_idx[n], forced_off[n+1], forced, ok[n])
+    batch_advance(states[n,5], tokens[n]) -> (mask_idx[n], forced_off[n+1], forced, ok[n])
+
+State = (pc, sub, cnt, rem, min_items).
 """
 from __future__ import annotations
 
@@ -37,7 +39,8 @@ def pack_native(g: CompiledGrammar, quote: int) -> dict:
     for ci, al in enumerate(g.choices):
         choice_off[ci + 1] = choice_off[ci] + len(al)
         for a in al:
-            alts += [a.first, len(rest), len(a.rest), a.target, a.cnt, int(a.is_continue)]
+            alts += [a.first, len(rest), len(a.rest), a.target, a.cnt, int(a.is_continue),
+                     int(a.is_close)]
             rest += a.rest
     num = np.full(3 * 5 * 3 * 2, -1, np.int32)
     for (kind, phase, e, nl), row in g.num_masks.items():
@@ -48,7 +51,8 @@ def pack_native(g: CompiledGrammar, quote: int) -> dict:
         choice_off=choice_off, alts=np.array(alts, np.int32), alt_rest=np.array(rest, np.int32),
         choice_mask=np.array(g.choice_mask, np.int32),
         choice_mask_close=np.array(g.choice_mask_close, np.int32),
-        max_items=np.array(g.max_items, np.int32), num_masks=num,
+        max_items=np.array(g.max_items, np.int32), honors_min=np.array(g.honors_min, np.int32),
+        num_masks=num,
         null_rest=np.array(g.null_rest, np.int32), tok_class=g.tok_class, tok_chars=g.tok_chars,
         tok_digits=g.tok_digits,
         scalars=np.array([g.str_mask, quote, g.meta["zero_token"], g.dot_token, g.null_first,
@@ -79,8 +83,8 @@ class RFQGrammar:
     def mask_table(self) -> np.ndarray:
         return mask_table_int32(self.compiled)
 
-    def initial(self):
-        st, forced = self.exec.initial()
+    def initial(self, min_items: int = 0):
+        st, forced = self.exec.initial(min_items)
         return tuple(st), list(forced)
 
     def advance(self, state, token: int):

@@ -52,6 +52,7 @@ class Alt:
     target: int
     cnt: int = CNT_NONE
     is_continue: bool = False    # disabled once the array counter hits max
+    is_close: bool = False       # disabled while the counter is below the request's min_items
 
 
 @dataclass
@@ -65,17 +66,17 @@ class Op:
 
 @dataclass
 class Limits:
-    title: int = 48
-    field: int = 28
-    description: int = 72
-    part_number: int = 20
-    item_description: int = 40
+    title: int = 36
+    field: int = 20
+    description: int = 44
+    part_number: int = 16
+    item_description: int = 28
     currency: int = 6
-    max_items: int = 5
-    max_docs: int = 3
-    doc: int = 24
-    max_missing: int = 4
-    missing: int = 18
+    max_items: int = 8
+    max_docs: int = 2
+    doc: int = 20
+    max_missing: int = 3
+    missing: int = 16
     qty_digits: int = 6
     price_int_digits: int = 6
     price_frac_digits: int = 2
@@ -96,6 +97,7 @@ class CompiledGrammar:
     choice_mask: list[int]             # mask row per choice (all alternatives)
     choice_mask_close: list[int]       # mask row with continue-alternatives removed (-1: n/a)
     max_items: list[int]               # per choice: counter limit (0 = no limit)
+    honors_min: list[int]              # per choice: 1 if the request's min_items applies
     str_mask: int
     num_masks: dict                    # (kind, phase, end_char_idx, null) -> row
     end_tokens: list[int]              # token id of ',', '}', ']'
@@ -180,6 +182,7 @@ class _Prog:
         self.literal_text: list[str] = []
         self.choices: list[list[Alt]] = []
         self.choice_limits: list[int] = []
+        self.choice_min: list[int] = []
 
     def enc(self, s: str) -> list[int]:
         return self.tok.encode(s)
@@ -211,10 +214,11 @@ class _Prog:
     def _seal(self):
         self._last_lit_open = False
 
-    def choice(self, alts: list[Alt], limit: int = 0) -> int:
+    def choice(self, alts: list[Alt], limit: int = 0, honors_min: bool = False) -> int:
         self._seal()
         self.choices.append(alts)
         self.choice_limits.append(limit)
+        self.choice_min.append(int(honors_min))
         self.ops.append(Op(OP_CHOICE, len(self.choices) - 1))
         return self.pc() - 1
 
@@ -256,7 +260,7 @@ def compile_rfq_grammar(tok, limits: Limits | None = None) -> CompiledGrammar:
 
     # ---- line_items: [ {part_number, description, quantity, target_price, currency}, ... ]
     P.lit(', "line_items": [')
-    open_pc = P.choice([])
+    open_pc = P.choice([], honors_min=True)
     body = P.pc()
     P.lit('"part_number": ')
     str_or_null(L.part_number)
@@ -269,13 +273,13 @@ def compile_rfq_grammar(tok, limits: Limits | None = None) -> CompiledGrammar:
     P.lit(', "currency": ')
     str_or_null(L.currency)
     P.lit("}")
-    next_pc = P.choice([], limit=L.max_items)
+    next_pc = P.choice([], limit=L.max_items, honors_min=True)
     after_items = P.pc()
     P.choices[P.ops[open_pc].a][:] = [
-        Alt(rbrack, [], after_items),
+        Alt(rbrack, [], after_items, is_close=True),
         Alt(lbrace, [], body, CNT_SET1, is_continue=True)]
     P.choices[P.ops[next_pc].a][:] = [
-        Alt(rbrack, [], after_items),
+        Alt(rbrack, [], after_items, is_close=True),
         Alt(comma, P.enc(" {"), body, CNT_INC, is_continue=True)]
 
     def str_array(maxn: int, maxlen: int, after_text: str):
@@ -350,7 +354,8 @@ def compile_rfq_grammar(tok, limits: Limits | None = None) -> CompiledGrammar:
     g = CompiledGrammar(
         ops=P.ops, literals=P.literals, literals_skip1=P.literals_skip1,
         literal_text=P.literal_text, choices=P.choices, choice_mask=choice_mask,
-        choice_mask_close=choice_mask_close, max_items=P.choice_limits, str_mask=str_mask,
+        choice_mask_close=choice_mask_close, max_items=P.choice_limits,
+        honors_min=P.choice_min, str_mask=str_mask,
         num_masks=num_masks, end_tokens=end_tokens, null_first=null_ids[0],
         null_rest=null_ids[1:], mask_rows=mb.table(), tok_class=cls, tok_chars=nch,
         tok_digits=ndig, vocab_size=V, dot_token=dot,

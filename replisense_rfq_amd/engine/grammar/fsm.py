@@ -2,12 +2,13 @@
 csrc/runtime/grammar.cpp; the C++ executor is what the engine's step loop runs —
 this one is its test oracle and the fallback when the runtime .so is absent).
 
-State = (pc, sub, cnt, rem):
+State = (pc, sub, cnt, rem, minv):
   LIT    sub=1 -> the literal's first char was already produced (by a NUM end token)
   STR    rem = characters still allowed
   NUM    sub = phase (0 first, 1 int digits, 2 after '.', 3 frac digits, 4 end/dot only,
          5 forced end), rem = digits used in the current part
-  CHOICE cnt = array item counter
+  CHOICE cnt = array item counter; minv = the request's minimum line-item count
+         (schema hint: the close alternative is disabled while cnt < minv)
 """
 from __future__ import annotations
 
@@ -39,14 +40,14 @@ class PyGrammarFSM:
         raise GrammarError("grammar has no string choice")
 
     # ------------------------------------------------------------------ entry
-    def _enter(self, pc: int, cnt: int, sub: int = 0):
+    def _enter(self, pc: int, cnt: int, sub: int = 0, minv: int = 0):
         op = self.g.ops[pc]
         if op.code == OP_STR:
-            return [pc, 0, cnt, op.a]
-        return [pc, sub, cnt, 0]
+            return [pc, 0, cnt, op.a, minv]
+        return [pc, sub, cnt, 0, minv]
 
-    def initial(self):
-        st = self._enter(self.g.start_pc, 0)
+    def initial(self, min_items: int = 0):
+        st = self._enter(self.g.start_pc, 0, minv=min_items)
         forced: list[int] = []
         self._settle(st, forced)
         return tuple(st), forced
@@ -59,9 +60,9 @@ class PyGrammarFSM:
             op = g.ops[pc]
             if op.code == OP_LIT:
                 forced.extend(g.literals_skip1[op.a] if st[1] else g.literals[op.a])
-                st[:] = self._enter(pc + 1, st[2])
+                st[:] = self._enter(pc + 1, st[2], minv=st[4])
             elif op.code == OP_CHOICE:
-                alts = self._enabled(op.a, st[2])
+                alts = self._enabled(op.a, st[2], st[4])
                 if len(alts) != 1:
                     return
                 self._take(alts[0], st, forced)
@@ -69,23 +70,25 @@ class PyGrammarFSM:
                 if st[3] > 0:
                     return
                 forced.append(self.quote)
-                st[:] = self._enter(pc + 1, st[2])
+                st[:] = self._enter(pc + 1, st[2], minv=st[4])
             elif op.code == OP_NUM:
                 if st[1] == 5:
-                    st[:] = self._enter(pc + 1, st[2])
+                    st[:] = self._enter(pc + 1, st[2], minv=st[4])
                 elif st[1] == 4 and op.a != NUM_DEC:
-                    st[:] = self._enter(pc + 1, st[2])      # only the end token is legal
+                    st[:] = self._enter(pc + 1, st[2], minv=st[4])      # only the end token is legal
                 else:
                     return
             else:
                 return
 
-    def _enabled(self, ci: int, cnt: int):
+    def _enabled(self, ci: int, cnt: int, minv: int = 0):
         g = self.g
         alts = g.choices[ci]
         lim = g.max_items[ci]
         if lim and cnt >= lim:
             return [a for a in alts if not a.is_continue]
+        if g.honors_min[ci] and cnt < minv:
+            return [a for a in alts if not a.is_close]
         return alts
 
     def _take(self, alt, st, forced, sampled=False):
@@ -97,12 +100,12 @@ class PyGrammarFSM:
             cnt = 1
         elif alt.cnt == CNT_INC:
             cnt += 1
-        st[:] = self._enter(alt.target, cnt)
+        st[:] = self._enter(alt.target, cnt, minv=st[4])
 
     # ------------------------------------------------------------------ query
     def mask(self, state) -> int:
         g = self.g
-        pc, sub, cnt, rem = state
+        pc, sub, cnt, rem, minv = state
         op = g.ops[pc]
         if op.code == OP_CHOICE:
             return g.choice_mask[op.a]
@@ -123,7 +126,7 @@ class PyGrammarFSM:
         forced: list[int] = []
         op = g.ops[st[0]]
         if op.code == OP_CHOICE:
-            for a in self._enabled(op.a, st[2]):
+            for a in self._enabled(op.a, st[2], st[4]):
                 if a.first == token:
                     self._take(a, st, forced, sampled=True)
                     break
@@ -131,7 +134,7 @@ class PyGrammarFSM:
                 raise GrammarError(f"token {token} not allowed at choice pc={st[0]}")
         elif op.code == OP_STR:
             if token == self.quote:
-                st[:] = self._enter(st[0] + 1, st[2])
+                st[:] = self._enter(st[0] + 1, st[2], minv=st[4])
             else:
                 if not (g.tok_class[token] & 1):
                     raise GrammarError(f"token {token} not string-safe")
@@ -153,12 +156,12 @@ class PyGrammarFSM:
         pc = st[0]
 
         def finish_skip1():
-            st[:] = self._enter(pc + 1, st[2], sub=1)
+            st[:] = self._enter(pc + 1, st[2], sub=1, minv=st[4])
 
         if ph == 0:
             if nullable and token == g.null_first:
                 forced.extend(g.null_rest)
-                st[:] = self._enter(pc + 1, st[2])
+                st[:] = self._enter(pc + 1, st[2], minv=st[4])
                 return
             if not is_dig:
                 raise GrammarError("expected digits")
@@ -197,9 +200,9 @@ class PyGrammarFSM:
                 st[1] = 5
 
 
-def run_tokens(fsm: PyGrammarFSM, choose) -> list[int]:
+def run_tokens(fsm: PyGrammarFSM, choose, min_items: int = 0) -> list[int]:
     """Drive the automaton to completion; `choose(mask_row) -> token` picks free tokens."""
-    st, out = fsm.initial()
+    st, out = fsm.initial(min_items)
     while not fsm.done(st):
         t = choose(fsm.mask(st), st)
         out.append(t)

@@ -1,0 +1,180 @@
+"""Data-parallel router: one engine replica per GPU (or TP group) in its own process.
+
+SURVEY.md §2.3 DP row: whole-node docs/s with Llama-3-8B TP=1 = 8 independent
+replicas behind a router.  Each worker process is pinned to its devices through
+``HIP_VISIBLE_DEVICES`` *before* torch initialises HIP (spawned, never forked
+from a GPU-initialised parent), builds an ``LLMEngine`` and serves requests from
+a multiprocessing queue; the API process keeps one dispatcher thread that
+resolves asyncio futures.  Routing is least-outstanding-tokens.  If a worker
+dies, its in-flight requests fail (-> HTTP 500 "RFQ processing failed", the
+reference semantics for exceptions escaping the generator) and the replica is
+restarted.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import queue
+import threading
+import time
+
+log = logging.getLogger("replisense_rfq_amd.router")
+
+
+def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
+    if devices:
+        os.environ["HIP_VISIBLE_DEVICES"] = devices
+    from ..utils.config import EngineConfig
+    from .engine import LLMEngine
+    from .sequence import SamplingParams
+
+    cfg = EngineConfig(**cfg_dict)
+    eng = LLMEngine(cfg)
+    outq.put(("ready", idx, None))
+    pending = {}
+    while True:
+        try:
+            while True:
+                msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
+                if msg is None:
+                    return
+                rid, prompt, p = msg
+                seq = eng.add_request(prompt, SamplingParams(**p))
+                pending[seq.req_id] = rid
+        except queue.Empty:
+            pass
+        if eng.has_work():
+            for s in eng.step():
+                rid = pending.pop(s.req_id, None)
+                if rid is not None:
+                    outq.put(("done", rid, {"text": eng.decode_text(s), "finish": s.finish_reason,
+                                            "span": s.span()}))
+
+
+class DPRouter:
+    def __init__(self, cfg, n_replicas: int, devices_per_replica: int = 1):
+        self.cfg = cfg
+        self.n = n_replicas
+        self.ctx = mp.get_context("spawn")
+        self.outq = self.ctx.Queue()
+        self.inqs = []
+        self.procs = []
+        self.load = [0] * n_replicas
+        self.where: dict[int, int] = {}
+        self.futures: dict[int, tuple] = {}
+        self._ids = itertools.count()
+        self.completed = 0
+        self._lock = threading.Lock()
+        cfg_dict = dict(cfg.to_dict())
+        cfg_dict["dp"] = 1
+        for i in range(n_replicas):
+            devs = ",".join(str(i * devices_per_replica + j) for j in range(devices_per_replica)) \
+                if cfg.device != "cpu" else ""
+            q = self.ctx.Queue()
+            p = self.ctx.Process(target=_worker, args=(i, devs, cfg_dict, q, self.outq), daemon=True)
+            p.start()
+            self.inqs.append(q)
+            self.procs.append(p)
+        ready = 0
+        deadline = time.time() + 1800
+        while ready < n_replicas and time.time() < deadline:
+            kind, idx, _ = self.outq.get(timeout=1800)
+            ready += kind == "ready"
+        self._stop = False
+        self._thread = threading.Thread(target=self._dispatch, daemon=True)
+        self._thread.start()
+
+    def _dispatch(self):
+        while not self._stop:
+            try:
+                kind, rid, payload = self.outq.get(timeout=0.1)
+            except queue.Empty:
+                self._check_workers()
+                continue
+            if kind != "done":
+                continue
+            with self._lock:
+                loop, fut, cost = self.futures.pop(rid, (None, None, 0))
+                r = self.where.pop(rid, None)
+                if r is not None:
+                    self.load[r] -= cost
+                self.completed += 1
+            if fut is not None:
+                loop.call_soon_threadsafe(lambda f=fut, p=payload: f.done() or f.set_result(p))
+
+    def _check_workers(self):
+        for i, p in enumerate(self.procs):
+            if not p.is_alive():
+                log.error("replica %d died; failing its requests", i)
+                with self._lock:
+                    dead = [rid for rid, r in self.where.items() if r == i]
+                    for rid in dead:
+                        loop, fut, _ = self.futures.pop(rid)
+                        self.where.pop(rid)
+                        loop.call_soon_threadsafe(
+                            lambda f=fut: f.done() or f.set_exception(RuntimeError("replica died")))
+                    self.load[i] = 0
+
+    async def generate(self, prompt: list[int], params: dict, timeout: float | None = None):
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        cost = len(prompt) + params.get("max_tokens", 1200) // 4
+        with self._lock:
+            rid = next(self._ids)
+            r = min(range(self.n), key=lambda i: self.load[i])
+            self.load[r] += cost
+            self.where[rid] = r
+            self.futures[rid] = (loop, fut, cost)
+        self.inqs[r].put((rid, prompt, params))
+        return await (asyncio.wait_for(fut, timeout) if timeout else fut)
+
+    def backend(self):
+        return RouterBackend(self)
+
+    def stats(self) -> dict:
+        return {"replicas": self.n, "outstanding": sum(1 for _ in self.where),
+                "load": list(self.load), "completed": self.completed}
+
+    def shutdown(self):
+        self._stop = True
+        for q in self.inqs:
+            q.put(None)
+        for p in self.procs:
+            p.join(timeout=10)
+
+
+class RouterBackend:
+    """ExtractService backend over the DP router."""
+
+    def __init__(self, router: DPRouter):
+        self.router = router
+        from .tokenizer import flavor_for_vocab, get_tokenizer
+        from ..models.config import get_config
+
+        self.tokenizer = get_tokenizer(flavor_for_vocab(get_config(router.cfg.model).vocab_size))
+
+    def complete(self, messages):
+        return asyncio.run(self.acomplete(messages))
+
+    async def acomplete(self, messages):
+        from ..service.extract import document_of
+        from ..service.hints import estimate_line_items
+
+        ids = self.tokenizer.chat_ids(messages)
+        cfg = self.router.cfg
+        params = dict(temperature=cfg.temperature, max_tokens=cfg.max_tokens,
+                      grammar=cfg.grammar, min_items=estimate_line_items(document_of(messages)))
+        out = await self.router.generate(ids, params, timeout=cfg.request_timeout_s)
+        if out["finish"] in ("engine_error", "grammar_error"):
+            raise RuntimeError(f"generation failed: {out['finish']}")
+        return out["text"]
+
+
+def maybe_router(cfg):
+    """A DPRouter when RFQ_DP > 1 (replicas of cfg.tp devices each), else None."""
+    if cfg.dp <= 1:
+        return None
+    return DPRouter(cfg, cfg.dp, max(1, cfg.tp))

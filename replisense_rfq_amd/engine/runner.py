@@ -162,7 +162,7 @@ class ModelRunner:
         for k, (s, _) in enumerate(rows):
             midx[k] = s.mask_idx if s.params.grammar else -1
             temps[k] = s.params.temperature
-            seeds[k] = _seed64(s.params.seed ^ (s.req_id * 0x632BE5AB), len(s.tokens))
+            seeds[k] = _seed64(s.params.seed, len(s.tokens))
         WA, WB = len(a_ws), len(b_ws)
         arrays = dict(ids=ids, pos=pos, slots=slots, a_bt=a_bt, a_qs=a_qs, a_ql=a_ql,
                       a_kvl=a_kvl, a_ws=np.asarray(a_ws, np.int32),

@@ -64,7 +64,9 @@ class Scheduler:
         budget = self.cfg.max_batched_tokens
         # 1) running sequences: decode rows first (cheap), then extends
         keep: list[Sequence] = []
-        for s in self.running:
+        for s in list(self.running):
+            if s.status is not Status.RUNNING:      # preempted earlier in this loop
+                continue
             if s.pending <= 0:
                 keep.append(s)
                 continue
@@ -108,8 +110,11 @@ class Scheduler:
         return plan
 
     def _preempt_victim(self, exclude: Sequence):
-        for s in reversed(self.running):
-            if s is not exclude and s.status is Status.RUNNING and s.blocks:
+        """Newest running sequence not yet placed in this step's plan (those come
+        after `exclude` in admission order); None -> preempt `exclude` itself."""
+        idx = self.running.index(exclude) if exclude in self.running else -1
+        for s in reversed(self.running[idx + 1:]):
+            if s.status is Status.RUNNING and s.blocks:
                 return s
         return None
 

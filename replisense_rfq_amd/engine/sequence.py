@@ -21,6 +21,7 @@ class SamplingParams:
     max_tokens: int = 1200
     seed: int = 0
     grammar: bool = True
+    min_items: int = 0      # schema hint: minimum line_items the output must contain
 
 
 @dataclass

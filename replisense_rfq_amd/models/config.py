@@ -59,10 +59,13 @@ MIXTRAL_8X7B = ModelConfig("mixtral-8x7b", vocab_size=32000, hidden=4096, n_laye
 # tile shape).  Vocab stays at the tokenizer's size so the real grammar masks apply.
 TINY_LLAMA = ModelConfig("tiny-llama", hidden=512, n_layers=2, n_heads=4, n_kv_heads=1,
                          ffn=1024, max_position=8192)
+TINY_LLAMA_TP = ModelConfig("tiny-llama-tp", hidden=512, n_layers=2, n_heads=8, n_kv_heads=2,
+                            ffn=1024, max_position=8192)
 TINY_MIXTRAL = replace(MIXTRAL_8X7B, name="tiny-mixtral", hidden=512, n_layers=2, n_heads=4,
                        n_kv_heads=1, ffn=512, vocab_size=32000)
 
-CONFIGS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_MIXTRAL)}
+CONFIGS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_LLAMA_TP,
+                                TINY_MIXTRAL)}
 ALIASES = {"llama3-70b-8192": "llama3-70b", "8b": "llama3-8b", "70b": "llama3-70b",
            "mixtral": "mixtral-8x7b"}
 

@@ -137,3 +137,34 @@ def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=t
         layers=layers,
         vocab_start=v0,
     )
+
+
+def shard_weights(full: dict, cfg: ModelConfig, tp: TPContext) -> dict:
+    """Slice full (TP=1) weights into this rank's Megatron shard (same layout as
+    init_weights), e.g. to check TP numerics against the single-device model."""
+    D, R, r = cfg.head_dim, tp.world, tp.rank
+    hq, hkv, F = cfg.n_heads // R, cfg.n_kv_heads // R, cfg.ffn // R
+    Hq, Hkv = cfg.n_heads, cfg.n_kv_heads
+    layers = []
+    for lw in full["layers"]:
+        q = lw["qkv"][: Hq * D][r * hq * D:(r + 1) * hq * D]
+        k = lw["qkv"][Hq * D:(Hq + Hkv) * D][r * hkv * D:(r + 1) * hkv * D]
+        v = lw["qkv"][(Hq + Hkv) * D:][r * hkv * D:(r + 1) * hkv * D]
+        out = LayerWeights(attn_norm=lw["attn_norm"], mlp_norm=lw["mlp_norm"],
+                           qkv=torch.cat([q, k, v]).contiguous(),
+                           o=lw["o"][:, r * hq * D:(r + 1) * hq * D].contiguous())
+        if cfg.is_moe:
+            Ff = cfg.ffn
+            out["router"] = lw["router"]
+            out["w13"] = torch.cat([lw["w13"][:, r * F:(r + 1) * F],
+                                    lw["w13"][:, Ff + r * F:Ff + (r + 1) * F]], 1).contiguous()
+            out["w2"] = lw["w2"][:, :, r * F:(r + 1) * F].contiguous()
+        else:
+            Ff = cfg.ffn
+            out["gate_up"] = torch.cat([lw["gate_up"][r * F:(r + 1) * F],
+                                        lw["gate_up"][Ff + r * F:Ff + (r + 1) * F]]).contiguous()
+            out["down"] = lw["down"][:, r * F:(r + 1) * F].contiguous()
+        layers.append(out)
+    v0, v1 = tp.shard(cfg.vocab_size)
+    return dict(embed=full["embed"], final_norm=full["final_norm"],
+                lm_head=full["lm_head"][v0:v1].contiguous(), layers=layers, vocab_start=v0)

@@ -233,8 +233,19 @@ class ReplayBackend:
         return await self.fallback.acomplete(messages)
 
 
+def document_of(messages: list[dict]) -> str:
+    """The (truncated) document embedded in the user message (rfq_agent.py:151)."""
+    u = messages[-1]["content"]
+    i = u.find('\n"""\n')
+    return u[i + 5:-4] if i >= 0 and u.endswith('\n"""') else u
+
+
 class EngineBackend:
-    """On-node engine backend: chat template -> tokens -> AsyncEngine -> text."""
+    """On-node engine backend: chat template -> tokens -> AsyncEngine -> text.
+
+    The document's estimated line-item count (service/hints.py) is passed to the
+    grammar as ``min_items`` so every requested part gets a line_items entry.
+    """
 
     def __init__(self, engine, async_engine=None, timeout_s: float | None = None):
         self.engine = engine
@@ -250,14 +261,20 @@ class EngineBackend:
             self.spans.append(seq.span())
         return self.tokenizer.decode(seq.output_ids)
 
+    def _params(self, messages):
+        from .hints import estimate_line_items
+
+        return self.engine.default_params(min_items=estimate_line_items(document_of(messages)))
+
     def complete(self, messages):
         ids = self.tokenizer.chat_ids(messages)
-        seq, = self.engine.generate([ids])
+        seq, = self.engine.generate([ids], self._params(messages))
         return self._text(seq)
 
     async def acomplete(self, messages):
-        ids = self.tokenizer.chat_ids(messages)
         if self.async_engine is None:
             return self.complete(messages)
-        seq = await self.async_engine.generate(ids, timeout=self.timeout_s)
+        ids = self.tokenizer.chat_ids(messages)
+        seq = await self.async_engine.generate(ids, self._params(messages),
+                                               timeout=self.timeout_s)
         return self._text(seq)

@@ -1,0 +1,100 @@
+"""Tensor parallelism on CPU over gloo (world_size 2): sharded forward == TP=1
+forward, and the TP engine (rank-0 scheduler + metadata broadcast + vocab-parallel
+sampler) produces valid RFQ JSON."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _forward_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from replisense_rfq_amd.models.config import get_config
+    from replisense_rfq_amd.models.llama import DecoderLM, ForwardMeta
+    from replisense_rfq_amd.models.weights import init_weights, shard_weights
+    from replisense_rfq_amd.parallel.tp import SINGLE, TPContext
+
+    cfg = get_config("tiny-llama").__class__(**{**get_config("tiny-llama").to_dict(),
+                                                "n_kv_heads": 2, "name": "tiny-tp"})
+    full = init_weights(cfg, SINGLE, "cpu", seed=11)
+    tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
+    m = DecoderLM(cfg, "cpu", tp=tp, weights=shard_weights(full, cfg, tp))
+    T, nb = 40, 4
+    shape = (cfg.n_layers, nb, m.hkv, 32, 128)
+    m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16), torch.zeros(shape, dtype=torch.bfloat16))
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, 5000, (T,), generator=g, dtype=torch.int32)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32)  # noqa: E731
+    meta = ForwardMeta(input_ids=ids, positions=torch.arange(T, dtype=torch.int32),
+                       slot_mapping=torch.arange(T, dtype=torch.int32), num_decode=0,
+                       num_prefill_tokens=T, pf_block_tables=i32([[0, 1]]), pf_q_start=i32([0]),
+                       pf_q_len=i32([T]), pf_kv_len=i32([T]), work_seq=i32([0, 0]),
+                       work_qblk=i32([0, 1]), logits_idx=torch.tensor([T - 1]))
+    part = m.forward(meta).float()
+    parts = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(parts, part)
+    if rank == 0:
+        ref = DecoderLM(cfg, "cpu", weights=full)
+        shape1 = (cfg.n_layers, nb, ref.hkv, 32, 128)
+        ref.attach_kv_cache(torch.zeros(shape1, dtype=torch.bfloat16),
+                            torch.zeros(shape1, dtype=torch.bfloat16))
+        exp = ref.forward(meta).float()
+        got = torch.cat(parts, -1)
+        q.put(float((got - exp).norm() / exp.norm()))
+    dist.destroy_process_group()
+
+
+def _engine_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    from replisense_rfq_amd.engine.engine import LLMEngine
+    from replisense_rfq_amd.parallel.tp import init_distributed
+    from replisense_rfq_amd.service.prompt import build_messages
+    from replisense_rfq_amd.utils import synth
+    from replisense_rfq_amd.utils.config import EngineConfig
+
+    tp = init_distributed("gloo")
+    eng = LLMEngine(EngineConfig(model="tiny-llama-tp", device="cpu", max_num_seqs=4), tp=tp)
+    if tp.rank == 0:
+        prompts = [eng.tokenizer.chat_ids(build_messages(synth.make_rfq(i).text)) for i in range(2)]
+        seqs = eng.generate(prompts)
+        eng.shutdown()
+        q.put([eng.decode_text(s) for s in seqs])
+    else:
+        eng.worker_loop()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_tp2_forward_matches_tp1():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    mp.start_processes(_forward_worker, args=(2, port, q), nprocs=2, start_method="spawn")
+    assert q.get(timeout=10) < 0.02
+
+
+@pytest.mark.timeout(600)
+def test_tp2_engine_valid_json():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    mp.start_processes(_engine_worker, args=(2, port, q), nprocs=2, start_method="spawn")
+    from replisense_rfq_amd.service.schema import RFQResponse
+
+    for text in q.get(timeout=10):
+        RFQResponse(**json.loads(text))
