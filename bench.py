@@ -13,8 +13,12 @@ detokenise -> JSON recovery + pydantic validation (rfq_agent.py:185-206).
 Weights are random-init (no checkpoints offline); documents are synthetic with
 the reference's length distribution.
 
-Timed region: exactly --steps waves, bracketed by barrier + cuda synchronize on
-both sides; the max over ranks is reported.  After it, the single-request p50
+Timed region: exactly --steps steps (= steps x docs-per-step documents per replica),
+bracketed by barrier + cuda synchronize on both sides; the max over ranks is
+reported.  Default ``--mode stream`` feeds those documents as one continuous
+stream (at most --max-num-seqs in flight, new documents admitted as others
+finish — production continuous batching); ``--mode wave`` drains each step's
+batch before starting the next.  After it, the single-request p50
 latency of the same path (the reference's 0.883 s p50 Groq server time,
 BASELINE.md) is measured on replica 0.
 
@@ -58,6 +62,10 @@ def parse():
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--prefill-chunk", type=int, default=16384)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--mode", choices=("stream", "wave"), default="stream",
+                    help="stream: the K*docs-per-step documents of the timed region are one "
+                         "continuous-batching stream (max-num-seqs in flight); wave: each step "
+                         "is a closed batch that drains before the next starts")
     return ap.parse_args()
 
 
@@ -75,8 +83,9 @@ class Replica:
         self.wave += 1
         return [synth.make_rfq(base + i) for i in range(n)]
 
-    def run_wave(self, n: int) -> int:
-        docs = self.docs(n)
+    def run_wave(self, n: int, waves: int = 1) -> int:
+        docs = [d for _ in range(waves) for d in self.docs(n)]
+        n = len(docs)
         msgs = [build_messages(d.text) for d in docs]
         prompts = [self.tok.chat_ids(m) for m in msgs]
         eng = self.engine
@@ -151,8 +160,11 @@ def main():
     barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        phase(lambda: rep.run_wave(args.docs_per_step))
+    if args.mode == "stream":
+        phase(lambda: rep.run_wave(args.docs_per_step, waves=args.steps))
+    else:
+        for _ in range(args.steps):
+            phase(lambda: rep.run_wave(args.docs_per_step))
     sync()
     barrier()
     dt = time.perf_counter() - t0
@@ -191,7 +203,8 @@ def main():
                        "parallelism": f"dp{dp_world}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
                        "docs_per_step_per_replica": args.docs_per_step,
                        "temperature": cfg.temperature, "grammar": cfg.grammar,
-                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs},
+                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
+                       "mode": args.mode, "max_num_seqs": args.max_num_seqs},
             "p50_parse_text_latency_s": round(p50, 4) if p50 is not None else None,
             "latency_vs_baseline_p50": round(BASELINE_P50_S / p50, 2) if p50 else None,
             "baseline": "vs_baseline = docs/s / (1 / 0.883 s), the reference's single-stream "
