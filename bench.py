@@ -212,7 +212,9 @@ def main():
             "per_doc": {k: round(v, 2) for k, v in rep.last.items()},
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
                        "engine_steps": steps_before, "graph_steps": st.get("graph_steps"),
-                       "kv_blocks": st.get("blocks"), "preempted": st.get("preempted")},
+                       "kv_blocks": st.get("blocks"), "preempted": st.get("preempted"),
+                       "host_s": {k: round(st.get(k, 0), 2) for k in
+                                  ("schedule_s", "pack_s", "forward_s", "post_s")}},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -77,6 +77,7 @@ class LLMEngine:
                 self.capture_s = self.runner.capture_graphs(buckets)
         self.num_steps = 0
         self.step_times: list[float] = []
+        self.timers = {"schedule_s": 0.0, "execute_s": 0.0, "post_s": 0.0}
 
     # ------------------------------------------------------------------ setup
     def _num_blocks(self) -> int:
@@ -115,12 +116,15 @@ class LLMEngine:
 
     # ------------------------------------------------------------------- step
     def step(self) -> list[Sequence]:
+        ts = time.perf_counter()
         plan = self.scheduler.schedule()
         if plan.empty:
             return []
         t0 = time.perf_counter()
         rows, toks = self.runner.execute(plan)
         now = time.perf_counter()
+        self.timers["schedule_s"] += t0 - ts
+        self.timers["execute_s"] += now - t0
         self.step_times.append(now - t0)
         self.num_steps += 1
         for s in plan.decode:
@@ -165,6 +169,7 @@ class LLMEngine:
                 self._finish(s, "stop", finished)
             elif s.num_generated >= s.params.max_tokens:
                 self._finish(s, "length", finished)
+        self.timers["post_s"] += time.perf_counter() - now
         return finished
 
     def _finish(self, s: Sequence, reason: str, out: list):
@@ -215,6 +220,7 @@ class LLMEngine:
 
     def stats(self) -> dict:
         st = dict(self.runner.stats)
+        st.update({k: round(v, 3) for k, v in self.timers.items()})
         st.update(self.kv.stats())
         st["preempted"] = self.scheduler.num_preempted
         st["running"] = len(self.scheduler.running)

@@ -41,7 +41,7 @@ HEADER = 16
 SAMPLE_SPLITS = 8
 EXT_MAX = 32                 # extends up to this many tokens use the decode kernel
 TOKEN_MULTS = (1, 2, 3, 4, 6, 8)
-MAX_GRAPH_TOKENS = 2048
+MAX_GRAPH_TOKENS = 4096
 
 
 def _seed64(req_seed: int, pos: int) -> int:
@@ -84,7 +84,8 @@ class ModelRunner:
         self.graphs: dict[tuple, object] = {}
         self._pinned = None
         self._dev = None
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0}
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
+                      "pack_s": 0.0}
 
     # ---------------------------------------------------------------- packing
     def _graph_key(self, NA: int, T: int):
@@ -249,7 +250,9 @@ class ModelRunner:
     # ---------------------------------------------------------------- execute
     def execute(self, plan: StepPlan) -> tuple[list, np.ndarray]:
         """Rank-0 entry: run one step, return (rows, sampled ids per logits row)."""
+        t0 = time.perf_counter()
         pk = self.pack(plan)
+        self.stats["pack_s"] += time.perf_counter() - t0
         if self.tp.enabled:
             self._broadcast(pk.header, pk.payload)
         toks = self._run(pk.header, pk.payload)

@@ -33,7 +33,8 @@ class EngineConfig:
     max_num_seqs: int = 256
     max_batched_tokens: int = 16384      # prefill chunk budget per step
     max_model_len: int = 8192            # llama3-70b-8192 context
-    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384,
+                            448, 512, 640, 768, 896, 1024)
     use_graphs: bool = True
     grammar: bool = True
     jump_forward: bool = True
