@@ -50,17 +50,19 @@ BASELINE_DOCS_PER_S = 1.0 / BASELINE_P50_S
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--docs-per-step", type=int, default=256)
-    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--docs-per-step", type=int, default=1024)
+    ap.add_argument("--max-num-seqs", type=int, default=1024)
     ap.add_argument("--latency-runs", type=int, default=5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump-forward", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--prefill-chunk", type=int, default=16384)
+    ap.add_argument("--kv-fraction", type=float, default=0.7,
+                    help="fraction of free HBM for the paged KV pool (288 GB per MI355X)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--mode", choices=("stream", "wave"), default="stream",
                     help="stream: the K*docs-per-step documents of the timed region are one "
@@ -136,7 +138,8 @@ def main():
     cfg = EngineConfig.from_env(
         model=args.model, tp=args.tp, seed=args.seed, max_num_seqs=args.max_num_seqs,
         use_graphs=not args.no_graphs, jump_forward=not args.no_jump_forward,
-        prefix_cache=not args.no_prefix_cache, max_batched_tokens=args.prefill_chunk)
+        prefix_cache=not args.no_prefix_cache, max_batched_tokens=args.prefill_chunk,
+        kv_fraction=args.kv_fraction)
     t_init = time.perf_counter()
     engine = LLMEngine(cfg, tp=tp)
     t_init = time.perf_counter() - t_init
