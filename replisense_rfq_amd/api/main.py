@@ -59,14 +59,28 @@ _engine_handles: dict = {}
 
 
 def build_generator() -> ExtractService:
-    """Select the inference backend (RFQ_BACKEND = engine | mock | replay)."""
-    from ..service.extract import EngineBackend, MockBackend, ReplayBackend
-
+    """Select the inference backend (RFQ_BACKEND = engine | mock | replay), optionally
+    behind the exact-request response cache (RFQ_RESPONSE_CACHE)."""
     backend = os.getenv("RFQ_BACKEND", "")
     if not backend:
         import torch
 
         backend = "engine" if torch.cuda.is_available() else "mock"
+    svc = _build_backend(backend)
+    cache_path = os.getenv("RFQ_RESPONSE_CACHE")
+    if cache_path:                        # reference: ag2 diskcache, cache_seed 42
+        from ..service.cache import CachedBackend, ResponseCache
+        from ..utils.config import EngineConfig
+
+        cfg = EngineConfig.from_env()
+        svc.backend = CachedBackend(svc.backend, ResponseCache(cache_path), cfg.model,
+                                    cfg.temperature, cfg.max_tokens)
+    return svc
+
+
+def _build_backend(backend: str) -> ExtractService:
+    from ..service.extract import EngineBackend, MockBackend, ReplayBackend
+
     if backend == "mock":
         return ExtractService(MockBackend())
     if backend == "replay":
@@ -199,7 +213,8 @@ async def health_check():
     status = {
         "api": "healthy",
         "file_parser": "healthy" if parser else "unhealthy",
-        "field_generator": "healthy" if field_generator else "unhealthy",
+        "field_generator": "healthy" if field_generator and field_generator.healthy
+        else "unhealthy",
         "temp_dir": str(TEMP_DIR),
         "max_file_size_mb": MAX_FILE_SIZE_MB,
         "supported_extensions": list(ALLOWED_EXTENSIONS),

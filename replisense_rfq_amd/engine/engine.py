@@ -29,6 +29,8 @@ from ..models.config import get_config
 from ..models.llama import DecoderLM
 from ..parallel.tp import SINGLE, TPContext
 from ..utils.config import EngineConfig
+from ..utils.faults import FaultInjector
+from ..utils.trace import trace_range
 from .grammar import get_grammar
 from .kv_cache import KVCache
 from .runner import ModelRunner
@@ -78,6 +80,7 @@ class LLMEngine:
         self.num_steps = 0
         self.step_times: list[float] = []
         self.timers = {"schedule_s": 0.0, "execute_s": 0.0, "post_s": 0.0}
+        self.faults = FaultInjector()
 
     # ------------------------------------------------------------------ setup
     def _num_blocks(self) -> int:
@@ -117,12 +120,20 @@ class LLMEngine:
     # ------------------------------------------------------------------- step
     def step(self) -> list[Sequence]:
         ts = time.perf_counter()
-        plan = self.scheduler.schedule()
+        with trace_range("schedule"):
+            plan = self.scheduler.schedule()
         if plan.empty:
             return []
+        if self.faults.active:
+            self.faults.on_step(self.num_steps)
         t0 = time.perf_counter()
-        rows, toks = self.runner.execute(plan)
+        with trace_range("execute"):
+            rows, toks = self.runner.execute(plan)
         now = time.perf_counter()
+        with trace_range("post"):
+            return self._post(plan, rows, toks, now, t0, ts)
+
+    def _post(self, plan, rows, toks, now, t0, ts) -> list[Sequence]:
         self.timers["schedule_s"] += t0 - ts
         self.timers["execute_s"] += now - t0
         self.step_times.append(now - t0)
@@ -184,6 +195,15 @@ class LLMEngine:
     def has_work(self) -> bool:
         return self.scheduler.has_work
 
+    def abort_all(self, reason: str) -> list[Sequence]:
+        """Finish every queued/running sequence (releasing its KV blocks)."""
+        out: list[Sequence] = []
+        for s in list(self.scheduler.running) + list(self.scheduler.waiting):
+            if s in self.scheduler.waiting:
+                self.scheduler.waiting.remove(s)
+            self._finish(s, reason, out)
+        return out
+
     def generate(self, prompts: list[list[int]], params=None,
                  seeds: list[int] | None = None) -> list[Sequence]:
         """Blocking batch generation.  `params`: one SamplingParams for all, or a list."""
@@ -242,8 +262,28 @@ class AsyncEngine:
         self._stop = threading.Event()
         self._wake = threading.Event()
         self.error: BaseException | None = None
+        self.step_started = 0.0
+        self.stalled = False
         self._thread = threading.Thread(target=self._loop, name="rfq-engine", daemon=True)
         self._thread.start()
+        self._watchdog = threading.Thread(target=self._watch, name="rfq-watchdog", daemon=True)
+        self._watchdog.start()
+
+    def _watch(self):
+        """Step watchdog: a step running longer than ``step_timeout_s`` marks the
+        engine stalled (``/health`` -> 503) so an orchestrator can restart it.
+        A GPU step cannot be interrupted safely, so in-flight requests are left
+        to their own request timeouts."""
+        limit = self.engine.cfg.step_timeout_s
+        while not self._stop.wait(min(1.0, limit / 4)):
+            t = self.step_started
+            if t and time.monotonic() - t > limit and not self.stalled:
+                self.stalled = True
+                log.error("engine step exceeded %.1fs watchdog", limit)
+
+    @property
+    def healthy(self) -> bool:
+        return not self.stalled and self._thread.is_alive()
 
     def _loop(self):
         eng = self.engine
@@ -255,17 +295,15 @@ class AsyncEngine:
             except queue.Empty:
                 pass
             if eng.has_work():
+                self.step_started = time.monotonic()
                 try:
                     eng.step()
                 except BaseException as e:  # engine failure: fail every in-flight request
                     log.exception("engine step failed")
                     self.error = e
-                    for s in list(eng.scheduler.running) + list(eng.scheduler.waiting):
-                        if s.callback:
-                            s.finish_reason = "engine_error"
-                            s.callback(s)
-                    eng.scheduler.running.clear()
-                    eng.scheduler.waiting.clear()
+                    eng.abort_all("engine_error")
+                finally:
+                    self.step_started = 0.0
             else:
                 self._wake.wait(0.005)
                 self._wake.clear()

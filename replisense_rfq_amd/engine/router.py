@@ -28,13 +28,16 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices
     from ..utils.config import EngineConfig
+    from ..utils.faults import FaultInjector
     from .engine import LLMEngine
     from .sequence import SamplingParams
 
     cfg = EngineConfig(**cfg_dict)
     eng = LLMEngine(cfg)
+    exit_after = FaultInjector().replica_exit_after()
     outq.put(("ready", idx, None))
     pending = {}
+    served = 0
     while True:
         try:
             while True:
@@ -46,46 +49,65 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
                 pending[seq.req_id] = rid
         except queue.Empty:
             pass
-        if eng.has_work():
-            for s in eng.step():
-                rid = pending.pop(s.req_id, None)
-                if rid is not None:
-                    outq.put(("done", rid, {"text": eng.decode_text(s), "finish": s.finish_reason,
-                                            "span": s.span()}))
+        if not eng.has_work():
+            continue
+        try:
+            finished = eng.step()
+        except Exception:                      # fail this replica's in-flight work
+            log.exception("replica %d step failed", idx)
+            finished = eng.abort_all("engine_error")
+        for s in finished:
+            rid = pending.pop(s.req_id, None)
+            if rid is not None:
+                outq.put(("done", rid, {"text": eng.decode_text(s), "finish": s.finish_reason,
+                                        "span": s.span()}))
+                served += 1
+        if exit_after is not None and served >= exit_after:
+            outq.close()                       # flush what was served, then crash
+            outq.join_thread()
+            os._exit(3)                        # injected replica crash
 
 
 class DPRouter:
-    def __init__(self, cfg, n_replicas: int, devices_per_replica: int = 1):
+    def __init__(self, cfg, n_replicas: int, devices_per_replica: int = 1,
+                 restart: bool = True):
         self.cfg = cfg
         self.n = n_replicas
+        self.dpr = devices_per_replica
+        self.restart = restart
         self.ctx = mp.get_context("spawn")
         self.outq = self.ctx.Queue()
-        self.inqs = []
-        self.procs = []
+        self.inqs = [None] * n_replicas
+        self.procs = [None] * n_replicas
+        self.ready = [False] * n_replicas
         self.load = [0] * n_replicas
         self.where: dict[int, int] = {}
         self.futures: dict[int, tuple] = {}
         self._ids = itertools.count()
         self.completed = 0
+        self.restarts = 0
         self._lock = threading.Lock()
-        cfg_dict = dict(cfg.to_dict())
-        cfg_dict["dp"] = 1
+        self._cfg_dict = dict(cfg.to_dict())
+        self._cfg_dict["dp"] = 1
         for i in range(n_replicas):
-            devs = ",".join(str(i * devices_per_replica + j) for j in range(devices_per_replica)) \
-                if cfg.device != "cpu" else ""
-            q = self.ctx.Queue()
-            p = self.ctx.Process(target=_worker, args=(i, devs, cfg_dict, q, self.outq), daemon=True)
-            p.start()
-            self.inqs.append(q)
-            self.procs.append(p)
-        ready = 0
+            self._spawn(i)
         deadline = time.time() + 1800
-        while ready < n_replicas and time.time() < deadline:
+        while not all(self.ready) and time.time() < deadline:
             kind, idx, _ = self.outq.get(timeout=1800)
-            ready += kind == "ready"
+            if kind == "ready":
+                self.ready[idx] = True
         self._stop = False
         self._thread = threading.Thread(target=self._dispatch, daemon=True)
         self._thread.start()
+
+    def _spawn(self, i: int) -> None:
+        devs = ",".join(str(i * self.dpr + j) for j in range(self.dpr)) \
+            if self.cfg.device != "cpu" else ""
+        q = self.ctx.Queue()
+        p = self.ctx.Process(target=_worker, args=(i, devs, self._cfg_dict, q, self.outq),
+                             daemon=True)
+        p.start()
+        self.inqs[i], self.procs[i], self.ready[i] = q, p, False
 
     def _dispatch(self):
         while not self._stop:
@@ -94,7 +116,9 @@ class DPRouter:
             except queue.Empty:
                 self._check_workers()
                 continue
-            if kind != "done":
+            if kind == "ready":
+                self.ready[rid] = True             # (rid is the replica index here)
+                log.info("replica %d ready", rid)
                 continue
             with self._lock:
                 loop, fut, cost = self.futures.pop(rid, (None, None, 0))
@@ -104,27 +128,42 @@ class DPRouter:
                 self.completed += 1
             if fut is not None:
                 loop.call_soon_threadsafe(lambda f=fut, p=payload: f.done() or f.set_result(p))
+            self._check_workers()
 
     def _check_workers(self):
         for i, p in enumerate(self.procs):
-            if not p.is_alive():
-                log.error("replica %d died; failing its requests", i)
-                with self._lock:
-                    dead = [rid for rid, r in self.where.items() if r == i]
-                    for rid in dead:
-                        loop, fut, _ = self.futures.pop(rid)
-                        self.where.pop(rid)
-                        loop.call_soon_threadsafe(
-                            lambda f=fut: f.done() or f.set_exception(RuntimeError("replica died")))
-                    self.load[i] = 0
+            if p is None or p.is_alive() or self._stop:
+                continue
+            log.error("replica %d died (exit %s); failing its requests", i, p.exitcode)
+            with self._lock:
+                self.ready[i] = False
+                dead = [rid for rid, r in self.where.items() if r == i]
+                for rid in dead:
+                    loop, fut, _ = self.futures.pop(rid)
+                    self.where.pop(rid)
+                    loop.call_soon_threadsafe(
+                        lambda f=fut: f.done() or f.set_exception(RuntimeError("replica died")))
+                self.load[i] = 0
+                if self.restart:
+                    self.restarts += 1
+                    self._spawn(i)
+                else:
+                    self.procs[i] = None
+
+    @property
+    def healthy(self) -> bool:
+        return any(self.ready)
 
     async def generate(self, prompt: list[int], params: dict, timeout: float | None = None):
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         cost = len(prompt) + params.get("max_tokens", 1200) // 4
         with self._lock:
+            live = [i for i in range(self.n) if self.ready[i]]
+            if not live:
+                raise RuntimeError("no live engine replica")
             rid = next(self._ids)
-            r = min(range(self.n), key=lambda i: self.load[i])
+            r = min(live, key=lambda i: self.load[i])
             self.load[r] += cost
             self.where[rid] = r
             self.futures[rid] = (loop, fut, cost)
@@ -135,15 +174,18 @@ class DPRouter:
         return RouterBackend(self)
 
     def stats(self) -> dict:
-        return {"replicas": self.n, "outstanding": sum(1 for _ in self.where),
-                "load": list(self.load), "completed": self.completed}
+        return {"replicas": self.n, "ready": sum(self.ready), "restarts": self.restarts,
+                "outstanding": len(self.where), "load": list(self.load),
+                "completed": self.completed}
 
     def shutdown(self):
         self._stop = True
-        for q in self.inqs:
-            q.put(None)
+        for q, p in zip(self.inqs, self.procs):
+            if p is not None and p.is_alive():
+                q.put(None)
         for p in self.procs:
-            p.join(timeout=10)
+            if p is not None:
+                p.join(timeout=10)
 
 
 class RouterBackend:
@@ -155,6 +197,10 @@ class RouterBackend:
         from ..models.config import get_config
 
         self.tokenizer = get_tokenizer(flavor_for_vocab(get_config(router.cfg.model).vocab_size))
+
+    @property
+    def healthy(self) -> bool:
+        return self.router.healthy
 
     def complete(self, messages):
         return asyncio.run(self.acomplete(messages))

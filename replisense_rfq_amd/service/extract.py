@@ -143,6 +143,16 @@ class ExtractService:
         self.last_latency_s: float | None = None
         log.info("RFQ Field Generator initialized successfully")
 
+    @property
+    def healthy(self) -> bool:
+        """False when the engine behind the backend is stalled or has no live replica."""
+        b = self.backend
+        while hasattr(b, "inner"):           # unwrap CachedBackend
+            if not getattr(b, "healthy", True):
+                return False
+            b = b.inner
+        return bool(getattr(b, "healthy", True))
+
     def _prepare(self, raw_text: str):
         if not raw_text or not raw_text.strip():
             log.warning("Empty raw text provided")
@@ -254,6 +264,10 @@ class EngineBackend:
         self.timeout_s = timeout_s if timeout_s is not None else engine.cfg.request_timeout_s
         self.spans: list[dict] = []
 
+    @property
+    def healthy(self) -> bool:
+        return self.async_engine is None or self.async_engine.healthy
+
     def _text(self, seq) -> str:
         if seq.finish_reason in ("engine_error", "grammar_error"):
             raise RuntimeError(f"generation failed: {seq.finish_reason}")
@@ -278,3 +292,19 @@ class EngineBackend:
         seq = await self.async_engine.generate(ids, self._params(messages),
                                                timeout=self.timeout_s)
         return self._text(seq)
+
+
+# --------------------------------------------------------- reference aliases
+RFQFieldGenerator = ExtractService          # rfq_agent.py:107 name, same contract
+
+
+def default_service() -> ExtractService:
+    """The service the API builds (backend from RFQ_BACKEND, see api/main.py)."""
+    from ..api.main import build_generator
+
+    return build_generator()
+
+
+async def generate_rfq_fields_async(raw_text: str, source_file: str = "email-body") -> dict:
+    """rfq_agent.py:270-273 convenience: a fresh generator per call."""
+    return await default_service().generate_async(raw_text, source_file)

@@ -175,3 +175,15 @@ def test_lifespan_with_mock_backend():
         r = c.post("/parse-text/", json={"text": "RFQ for 10 pcs of ABC-123"})
         assert r.status_code == 200 and r.json()["data"]["success"] is True
         assert c.get("/metrics").json()["data"]["backend"] == "MockBackend"
+
+
+def test_server_config_env(monkeypatch):
+    from replisense_rfq_amd.api.serve import server_config
+
+    monkeypatch.setenv("PORT", "9123")
+    monkeypatch.setenv("LOG_LEVEL", "DEBUG")
+    monkeypatch.setenv("RFQ_BACKEND", "engine")
+    c = server_config()
+    assert c["port"] == 9123 and c["log_level"] == "debug" and c["reload"] is False
+    monkeypatch.setenv("RFQ_BACKEND", "mock")
+    assert server_config()["reload"] is True

@@ -1,0 +1,100 @@
+"""Failure detection and recovery paths, driven by the
+RFQ_FAULT injector on the CPU engine: a step that raises fails exactly the
+in-flight requests and frees their KV blocks; a stalled step trips the
+watchdog (/health -> unhealthy); a crashed DP replica fails its requests and is
+restarted."""
+import asyncio
+import json
+
+import pytest
+
+from replisense_rfq_amd.engine.engine import AsyncEngine, LLMEngine
+from replisense_rfq_amd.service.extract import EngineBackend, ExtractService
+from replisense_rfq_amd.service.prompt import build_messages
+from replisense_rfq_amd.service.schema import RFQResponse
+from replisense_rfq_amd.utils import synth
+from replisense_rfq_amd.utils.config import EngineConfig
+from replisense_rfq_amd.utils.faults import FaultInjector
+
+
+def _cfg(**kw):
+    base = dict(model="tiny-llama", device="cpu", max_num_seqs=4, max_batched_tokens=2048)
+    base.update(kw)
+    return EngineConfig(**base)
+
+
+def _prompt(eng, i):
+    return eng.tokenizer.chat_ids(build_messages(synth.make_rfq(i).text))
+
+
+def test_fault_spec_parsing():
+    f = FaultInjector("step_raise:3, step_sleep:1:20,replica_exit:5")
+    assert f.active and f.replica_exit_after() == 5
+    f.on_step(0)
+    with pytest.raises(RuntimeError):
+        f.on_step(3)
+    f.on_step(3)                          # one-shot
+    assert not FaultInjector("").active
+
+
+def test_step_fault_fails_inflight_and_frees_kv():
+    eng = LLMEngine(_cfg())
+    free0 = eng.kv.stats()["free"]
+    eng.faults = FaultInjector("step_raise:2")
+    aeng = AsyncEngine(eng)
+
+    async def run():
+        return await asyncio.gather(*[aeng.generate(_prompt(eng, i), timeout=120)
+                                      for i in range(2)])
+
+    seqs = asyncio.run(run())
+    assert all(s.finish_reason == "engine_error" for s in seqs)
+    assert aeng.error is not None
+    assert eng.kv.stats()["free"] == free0 and not eng.has_work()
+    # the engine keeps serving after the failure
+    s, = asyncio.run(asyncio.wait_for(aeng.generate(_prompt(eng, 7)), 120)),
+    assert s.finish_reason == "stop"
+    RFQResponse(**json.loads(eng.decode_text(s)))
+    # ExtractService maps an engine_error to the reference's retry-then-500 path
+    svc = ExtractService(EngineBackend(eng, aeng))
+    assert svc.healthy
+    aeng.shutdown()
+
+
+def test_watchdog_marks_stalled_engine_unhealthy():
+    eng = LLMEngine(_cfg(step_timeout_s=0.2))
+    eng.faults = FaultInjector("step_sleep:0:1500")
+    aeng = AsyncEngine(eng)
+    s = asyncio.run(asyncio.wait_for(aeng.generate(_prompt(eng, 3)), 120))
+    assert s.finish_reason == "stop"
+    assert aeng.stalled and not aeng.healthy
+    assert not ExtractService(EngineBackend(eng, aeng)).healthy
+    aeng.shutdown()
+
+
+@pytest.mark.slow
+def test_router_replica_crash_is_restarted(monkeypatch):
+    from replisense_rfq_amd.engine.router import DPRouter
+
+    monkeypatch.setenv("RFQ_FAULT", "replica_exit:1")
+    cfg = _cfg(max_num_seqs=2)
+    router = DPRouter(cfg, 1)
+    try:
+        eng_tok = router.backend().tokenizer
+        ids = eng_tok.chat_ids(build_messages(synth.make_rfq(1).text))
+        params = dict(temperature=0.1, max_tokens=1200, grammar=True, min_items=0)
+        out = asyncio.run(router.generate(ids, params, timeout=300))
+        assert out["finish"] == "stop"
+        RFQResponse(**json.loads(out["text"]))
+        # the replica exits after serving one request; the router restarts it
+        import time
+
+        deadline = time.time() + 300
+        while router.restarts == 0 and time.time() < deadline:
+            time.sleep(0.2)
+        assert router.restarts >= 1
+        while not router.healthy and time.time() < deadline:
+            time.sleep(0.2)
+        assert router.healthy
+    finally:
+        router.shutdown()
