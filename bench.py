@@ -214,11 +214,16 @@ def main():
                         "Groq llama3-70b p50 server time (BASELINE.md)",
             "per_doc": {k: round(v, 2) for k, v in rep.last.items()},
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
+                       "gemm_tune_s": round(engine.tune_s, 1),
                        "engine_steps": steps_before, "graph_steps": st.get("graph_steps"),
                        "kv_blocks": st.get("blocks"), "preempted": st.get("preempted"),
                        "host_s": {k: round(st.get(k, 0), 2) for k in
                                   ("schedule_s", "pack_s", "forward_s", "post_s")}},
         }
+        for r in getattr(engine, "gemm_plan", None) or []:
+            print("[bench] gemm plan %s M=%d N=%d K=%d hipblaslt %.1fus -> %s %.1fus"
+                  % (r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6]),
+                  file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

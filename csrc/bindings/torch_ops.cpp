@@ -14,6 +14,8 @@ typedef uint16_t bf16_t;
 void launch_rms_norm(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
 void launch_fused_add_rms_norm(const bf16_t*, int64_t, bf16_t*, int64_t, const bf16_t*, bf16_t*,
                                int64_t, int, int, float, hipStream_t);
+void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
+                        hipStream_t);
 void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
@@ -74,6 +76,22 @@ void fused_add_rms_norm(const Tensor& x, const Tensor& residual, const Tensor& w
   TORCH_CHECK(residual.size(0) == x.size(0) && out.size(0) == x.size(0), "row mismatch");
   rfq::launch_fused_add_rms_norm(bp(x), x.stride(0), bpm(residual), residual.stride(0), bp(w),
                                  bpm(out), out.stride(0), x.size(0), d, (float)eps, cur_stream());
+}
+
+// out[M, N] = x[M, K] . w[N, K]^T for M <= 64 (weight-streaming latency path)
+void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm: w must be contiguous [N, K]");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  const int nt = (cfg & 1) ? 2 : 1;  // bits 2-3 select the load variant
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny_gemm: M must be in [1, 64]");
+  TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N % (16 * nt) == 0,
+              "skinny_gemm: K % 128 and N % tile required");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "skinny_gemm: out shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "skinny_gemm: alignment");
+  rfq::launch_skinny_gemm(bp(x), x.stride(0), bp(w), N, K, bpm(out), out.stride(0), M, (int)cfg,
+                          cur_stream());
 }
 
 void silu_mul(const Tensor& gate_up, const Tensor& out) {
@@ -283,6 +301,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("rms_norm(Tensor x, Tensor w, float eps, Tensor(a!) out) -> ()");
   m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
+  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start) -> ()");
   m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()");
@@ -309,6 +328,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("rms_norm", &rms_norm);
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_mul", &silu_mul);
+  m.impl("skinny_gemm", &skinny_gemm);
   m.impl("embed", &embed);
   m.impl("rope_kv", &rope_kv);
   m.impl("attn_decode", &attn_decode);

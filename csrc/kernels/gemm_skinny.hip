@@ -1,0 +1,181 @@
+// Skinny-M GEMM for the latency path: Y[M, N] = X[M, K] . W[N, K]^T, M <= 64.
+//
+// At small batch (a single /parse-text/ request decodes 1 sampled token plus a
+// few jump-forward tokens per step) every projection is a weight stream: the
+// step is bound by reading the 16 GB of Llama-3-8B weights from HBM3E, and the
+// library GEMMs tile for large M and leave most of that bandwidth idle.  This
+// kernel is shaped for the stream instead of the FLOPs:
+//
+//   * W is the MFMA A operand (16 output features x 32 k per
+//     mfma_f32_16x16x32_bf16), X^T the B operand (k x 16 tokens).  Because the
+//     k-reduction is order independent, lane-group g = lane>>4 owns a contiguous
+//     32-element (64 B) slice of each W row per 128-k step and feeds it to four
+//     MFMAs (j = 0..3): every lane issues 4 x 16 B loads per row per step — full
+//     64 B segments, no LDS staging, no shuffles.
+//   * A workgroup owns NT*16 output features; its NW waves split K, and the
+//     partial 16x16 tiles are reduced through LDS and written as bf16 once
+//     (no second pass, no atomics).  U k-steps are in flight per wave so every
+//     CU keeps enough bytes outstanding to cover HBM latency.
+//   * X (a few KB to ~1 MB) is read straight from L2; NT > 1 reuses each X
+//     fragment for several W tiles to keep the L2 traffic well below the W stream.
+//
+// Requires K % 128 == 0, N % (16*NT) == 0, 16-byte aligned rows.
+#include "common.h"
+
+namespace rfq {
+
+template <bool NTL>
+__device__ __forceinline__ s16x8 ldw(const bf16_t* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p));
+  else return *reinterpret_cast<const s16x8*>(p);
+}
+
+// CMAP: k-permutation.  false: lane-group g owns 32 contiguous k (4 x 16 B, one per
+// MFMA j); true: MFMA j reads k [j*32, j*32+32) and group g the 8-element slice g
+// of it, so the 4 groups of one row read 64 contiguous bytes per load instruction.
+template <int MT, int NT, int NW, int U, bool CMAP, bool NTL>
+__global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
+    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
+    bf16_t* __restrict__ Y, int64_t ldy, int M) {
+  __shared__ f32x4 red[NW][NT * MT][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (16 * NT);
+  const int nks = K >> 7;
+  const int ks0 = wave * nks / NW, ks1 = (wave + 1) * nks / NW;
+
+  const bf16_t* wp[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) wp[a] = W + (int64_t)(n0 + a * 16 + r) * K + g * (CMAP ? 8 : 32);
+  constexpr int JS = CMAP ? 32 : 8;                 // element stride between MFMA chunks
+  const bf16_t* xp[MT];
+  bool xv[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = t * 16 + r;
+    xv[t] = m < M;
+    xp[t] = X + (int64_t)(xv[t] ? m : 0) * ldx + g * (CMAP ? 8 : 32);
+  }
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  int ks = ks0;
+  for (; ks + U <= ks1; ks += U) {
+    s16x8 w[U][NT][4], x[U][MT][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * 128 + j * JS);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[u][t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + (ks + u) * 128 + j * JS)
+                             : zero;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                as_bf16x8(w[u][a][j]), as_bf16x8(x[u][t][j]), acc[a][t], 0, 0, 0);
+  }
+  for (; ks < ks1; ++ks) {
+    s16x8 w[NT][4], x[MT][4];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[a][j] = ldw<NTL>(wp[a] + (int64_t)ks * 128 + j * JS);
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        x[t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + ks * 128 + j * JS) : zero;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              as_bf16x8(w[a][j]), as_bf16x8(x[t][j]), acc[a][t], 0, 0, 0);
+  }
+
+  if (NW > 1) {
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) red[wave][a * MT + t][lane] = acc[a][t];
+    __syncthreads();
+  }
+  // D layout (16x16): lane holds rows (g*4 + i) = output features, col r = token.
+  for (int tile = wave; tile < NT * MT; tile += NW) {
+    const int a = tile / MT, t = tile % MT;
+    f32x4 s = red[0][tile][lane];
+    if (NW == 1) s = acc[a][t];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) s += red[w2][tile][lane];
+    const int m = t * 16 + r;
+    if (m < M) {
+      uint2 v;
+      v.x = pack_bf16x2(s[0], s[1]);
+      v.y = pack_bf16x2(s[2], s[3]);
+      *reinterpret_cast<uint2*>(Y + (int64_t)m * ldy + n0 + a * 16 + g * 4) = v;
+    }
+  }
+}
+
+template <int MT, int NT, int NW, int U>
+static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                       int64_t ldy, int M, int variant, hipStream_t s) {
+  dim3 grid(N / (16 * NT));
+#define SK_LAUNCH(cm, nt)                                                                   \
+  hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, cm, nt>), grid, dim3(NW * 64), 0, s, \
+                     X, ldx, W, K, Y, ldy, M)
+  switch (variant) {
+    case 0: SK_LAUNCH(false, true); break;
+    case 1: SK_LAUNCH(true, true); break;
+    case 2: SK_LAUNCH(false, false); break;
+    default: SK_LAUNCH(true, false); break;
+  }
+#undef SK_LAUNCH
+}
+
+// cfg bits: [1:0] tile (0: NT=1 NW=4, 1: NT=2 NW=4, 2: NT=1 NW=8, 3: NT=2 NW=8),
+// [3:2] variant (bit2 contiguous k-map, bit3 plain loads instead of non-temporal).
+void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                        int64_t ldy, int M, int cfg, hipStream_t s) {
+  const int MT = (M + 15) / 16;
+  const int v = (cfg >> 2) & 3;
+#define SK_CASE(mt, u1, u2)                                                              \
+  case mt:                                                                               \
+    switch (cfg & 3) {                                                                   \
+      case 0: launch_cfg<mt, 1, 4, u1>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
+      case 1: launch_cfg<mt, 2, 4, u2>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
+      case 2: launch_cfg<mt, 1, 8, u1>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
+      default: launch_cfg<mt, 2, 8, u2>(X, ldx, W, N, K, Y, ldy, M, v, s); break;        \
+    }                                                                                    \
+    break;
+  switch (MT) {
+    SK_CASE(1, 4, 2)
+    SK_CASE(2, 3, 2)
+    SK_CASE(3, 2, 1)
+    default: SK_CASE(4, 2, 1)
+  }
+#undef SK_CASE
+}
+
+}  // namespace rfq

@@ -73,6 +73,9 @@ class LLMEngine:
                                   self.grammar.mask_table() if self.grammar else None, tp)
         self.scheduler = Scheduler(self.cfg, self.kv)
         self.capture_s = 0.0
+        self.tune_s = 0.0
+        if self.device.type == "cuda" and self.cfg.tune_gemm:
+            self._tune_gemms()
         if capture and self.device.type == "cuda" and self.cfg.use_graphs:
             buckets = [b for b in self.cfg.graph_buckets if b <= self.cfg.max_num_seqs]
             if buckets:
@@ -83,6 +86,16 @@ class LLMEngine:
         self.faults = FaultInjector()
 
     # ------------------------------------------------------------------ setup
+    def _tune_gemms(self) -> None:
+        from ..ops.autotune import tune_model
+        from .runner import TOKEN_MULTS
+
+        t0 = time.perf_counter()
+        nbs = [b for b in self.cfg.graph_buckets if b <= min(64, self.cfg.max_num_seqs)] or [1]
+        ms = sorted({nb * m for nb in nbs for m in TOKEN_MULTS if nb * m <= 64})
+        self.gemm_plan = tune_model(self.model, ms, nbs)
+        self.tune_s = time.perf_counter() - t0
+
     def _num_blocks(self) -> int:
         cfg = self.cfg
         per_seq = (cfg.max_model_len + 31) // 32

@@ -120,7 +120,7 @@ class DecoderLM:
         for li in range(L):
             lw = w["layers"][li]
             kc, vc = self.kv_k[li], self.kv_v[li]
-            qkv = x @ lw["qkv"].t()
+            qkv = ops.linear(x, lw["qkv"])
             ops.rope_kv(qkv, m.positions, self.cos_sin, m.slot_mapping, kc, vc, hq, hkv)
             if D > 0:
                 po, pm = dec_parts if dec_parts is not None else (attn, attn)
@@ -132,20 +132,20 @@ class DecoderLM:
                 ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                                  m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
                                  self.scale)
-            o = attn @ lw["o"].t()
+            o = ops.linear(attn, lw["o"])
             self.tp.all_reduce_(o)
             ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
             if cfg.is_moe:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs)
             else:
-                gu = x @ lw["gate_up"].t()
+                gu = ops.linear(x, lw["gate_up"])
                 a = ops.silu_mul(gu)
-                mo = a @ lw["down"].t()
+                mo = ops.linear(a, lw["down"])
             self.tp.all_reduce_(mo)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
             ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
-        return xs @ w["lm_head"].t()
+        return ops.linear(xs, w["lm_head"])
 
     # ------------------------------------------------------------- conveniences
     def weight_bytes(self) -> int:

@@ -14,8 +14,12 @@ from . import reference as ref
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
-    "moe_combine", "native_available",
+    "moe_combine", "native_available", "linear", "linear_plan", "set_linear_plan",
 ]
+
+# Tokens per step up to which projections use the skinny weight-streaming GEMM
+# (csrc/kernels/gemm_skinny.hip) instead of hipBLASLt; 0 disables it.
+SKINNY_MAX_M = int(__import__("os").environ.get("RFQ_SKINNY_MAX_M", "64"))
 
 
 def native_available() -> bool:
@@ -24,6 +28,58 @@ def native_available() -> bool:
 
 def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
+
+
+# (M, N, K) -> skinny cfg, or -1 for hipBLASLt.  Filled by ops.autotune at engine
+# start (measured on the model's own weights); _default_plan covers untuned shapes.
+_LINEAR_PLAN: dict[tuple[int, int, int], int] = {}
+_TUNED_MS: list[int] = []
+
+
+def set_linear_plan(plan: dict, ms) -> None:
+    _LINEAR_PLAN.clear()
+    _LINEAR_PLAN.update(plan)
+    _TUNED_MS[:] = sorted(set(ms))
+
+
+def _default_plan(M: int, N: int, K: int) -> int:
+    """Measured on MI355X (profiles/skinny_gemm.md): the contiguous-k, plain-load
+    variants beat hipBLASLt up to M=16 on every 8B/70B projection except down."""
+    if M > 16:
+        return -1
+    return 14 if N <= 4096 else 13
+
+
+def linear_plan(M: int, N: int, K: int) -> int:
+    if M > SKINNY_MAX_M or K % 128 or N % 16:
+        return -1
+    if _TUNED_MS:
+        for m in _TUNED_MS:
+            if m >= M:
+                c = _LINEAR_PLAN.get((m, N, K))
+                if c is not None:
+                    return c if (c < 0 or c & 1 == 0 or N % 32 == 0) else -1
+                break
+    return _default_plan(M, N, K)
+
+
+def linear(x, w, out=None, plan: int | None = None):
+    """out[M, N] = x[M, K] . w[N, K]^T (bf16).  Small M streams W through the skinny
+    MFMA kernel (csrc/kernels/gemm_skinny.hip) when the tuning plan says it beats
+    hipBLASLt; otherwise the plain library GEMM."""
+    M, K = x.shape
+    N = w.shape[0]
+    if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+        cfg = linear_plan(M, N, K) if plan is None else plan
+        if cfg >= 0:
+            if out is None:
+                out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            _native.ops().skinny_gemm(x, w, out, cfg)
+            return out
+    if out is None:
+        return x @ w.t()
+    torch.matmul(x, w.t(), out=out)
+    return out
 
 
 def rms_norm(x, w, eps, out=None):

@@ -1,0 +1,79 @@
+"""Per-shape GEMM selection for the latency path: skinny MFMA kernel vs hipBLASLt.
+
+Run once at engine start, before hipGraph capture, on the model's own weights:
+for every projection shape (N, K) and every token count M the captured graphs
+use (<= 64), time hipBLASLt and each skinny-kernel config over the real
+per-layer weight list (32-80 distinct matrices, so every call streams from HBM
+exactly as in a forward pass) and keep the fastest.  The plan is installed with
+:func:`replisense_rfq_amd.ops.set_linear_plan` and read by :func:`ops.linear`.
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+
+from . import _native, set_linear_plan
+
+log = logging.getLogger("replisense_rfq_amd.ops")
+
+# tile configs (bits 0-1) on the contiguous-k / plain-load variant (bits 2-3 = 3)
+CANDIDATES = (12, 13, 14, 15)
+
+
+def _time(fn, ws, reps: int) -> float:
+    fn(ws[0])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        for w in ws:
+            fn(w)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * len(ws))
+
+
+def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, list[int]],
+                reps: int = 2, margin: float = 0.97) -> dict:
+    """groups: name -> per-layer weights [N, K]; ms_by_group: name -> token counts."""
+    ops = _native.ops()
+    plan, report = {}, []
+    for name, ws in groups.items():
+        N, K = ws[0].shape
+        if K % 128 or N % 16:
+            continue
+        for M in ms_by_group.get(name, []):
+            if M > 64:
+                continue
+            x = torch.randn(M, K, device=ws[0].device, dtype=ws[0].dtype)
+            out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+            t_lib = _time(lambda w: torch.matmul(x, w.t(), out=out), ws, reps)
+            best, t_best = -1, t_lib * margin
+            for c in CANDIDATES:
+                if c & 1 and N % 32:
+                    continue
+                t = _time(lambda w, c=c: ops.skinny_gemm(x, w, out, c), ws, reps)
+                if t < t_best:
+                    best, t_best = c, t
+            plan[(M, N, K)] = best
+            report.append((name, M, N, K, round(t_lib, 1), best, round(min(t_best, t_lib), 1)))
+    return plan, report
+
+
+def tune_model(model, ms: list[int], lm_ms: list[int]) -> list:
+    """Tune every projection of a DecoderLM and install the plan."""
+    w = model.w
+    groups = {"qkv": [l["qkv"] for l in w["layers"]], "o": [l["o"] for l in w["layers"]]}
+    if "gate_up" in w["layers"][0]:
+        groups["gate_up"] = [l["gate_up"] for l in w["layers"]]
+        groups["down"] = [l["down"] for l in w["layers"]]
+    groups["lm_head"] = [w["lm_head"]] * 4
+    msg = {k: ms for k in groups}
+    msg["lm_head"] = lm_ms
+    plan, report = tune_linear(groups, msg)
+    set_linear_plan(plan, sorted(set(ms) | set(lm_ms)))
+    for r in report:
+        log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
+                 r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6])
+    return report

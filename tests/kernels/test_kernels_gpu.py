@@ -203,3 +203,29 @@ def test_moe_pipeline(gpu):
     logits = (x @ router.t()).cpu()
     exp = ref.moe_forward(x.cpu(), w13.cpu(), w2.cpu(), logits, k)
     _close(out, exp, 3e-2, 2e-2, "moe")
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(512, 4096), (256, 14336), (1024, 3584)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_skinny_gemm(gpu, M, N, K, cfg):
+    torch.manual_seed(M * 7 + cfg)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(BF)
+    out = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm(x, w, out, cfg)
+    exp = x.float() @ w.float().t()
+    _close(out, exp, 1e-2, 1e-2, f"skinny_gemm M={M} cfg={cfg}")
+
+
+def test_skinny_gemm_strided_rows(gpu):
+    """x / out as row-slices of wider buffers (the runner's packed activations)."""
+    torch.manual_seed(3)
+    big = torch.randn(8, 4096 + 256, device=gpu, dtype=BF)
+    x = big[:, :4096]
+    w = (torch.randn(1024, 4096, device=gpu) * 0.02).to(BF)
+    obuf = torch.zeros(8, 1024 + 64, device=gpu, dtype=BF)
+    out = obuf[:, :1024]
+    ops.linear(x, w, out=out)
+    _close(out, x.float() @ w.float().t(), 1e-2, 1e-2, "linear strided")
+    assert torch.all(obuf[:, 1024:] == 0)
