@@ -118,7 +118,7 @@ class Replica:
             s, = eng.generate([ids], eng.default_params(min_items=estimate_line_items(d.text)))
             parse_and_validate_response(eng.decode_text(s), "direct_text_input")
             out.append(time.perf_counter() - t0)
-            eng.runner.tp.enabled and eng.shutdown()
+        eng.runner.tp.enabled and eng.shutdown()      # release the TP workers' loop
         return out
 
 
