@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "block_manager.h"
+#include "engine_core.h"
 #include "grammar.h"
 
 using namespace rfqrt;
@@ -188,6 +189,86 @@ static int grammar_walks(const Grammar& g, const std::vector<uint32_t>& masks, i
   return longest;
 }
 
+// ------------------------------------------------------------ engine core
+// Continuous batching with grammar-masked random tokens over a small KV pool
+// (forces chunked prefill, prefix sharing and preemption), checking the packed
+// layout's invariants every step and that every request retires with a valid
+// reason and all blocks return to the pool.
+static void fuzz_engine_core(std::shared_ptr<const Grammar> g, const std::vector<uint32_t>& masks,
+                             int32_t words, uint32_t seed) {
+  std::mt19937 rng(seed);
+  CoreConfig cfg;
+  cfg.num_blocks = 48;
+  cfg.scratch_block = 48;
+  cfg.max_num_seqs = 6;
+  cfg.max_batched_tokens = 256;
+  cfg.max_model_len = 2048;
+  cfg.group = 4;
+  cfg.hkv = 2;
+  cfg.is_cuda = true;
+  EngineCore core(cfg, g);
+  std::vector<std::pair<int32_t, int32_t>> keys;
+  for (int nb : {1, 2, 4, 8})
+    for (int m : {1, 2, 3, 4, 6, 8}) keys.push_back({nb, nb * m});
+  core.set_graph_keys(keys);
+  std::vector<int32_t> header(HEADER), payload(core.payload_bound() + 2);
+  int32_t* pay = payload.data() + ((reinterpret_cast<uintptr_t>(payload.data()) & 7) ? 1 : 0);
+  const int nreq = 24;
+  std::vector<int32_t> shared(300);
+  for (auto& t : shared) t = (int32_t)(rng() % 1000);
+  for (int i = 0; i < nreq; ++i) {
+    std::vector<int32_t> prompt(shared.begin(), shared.begin() + 200 + rng() % 100);
+    for (int j = 0; j < (int)(rng() % 200); ++j) prompt.push_back((int32_t)(rng() % 1000));
+    SeqParams p;
+    p.seed = i;
+    p.min_items = (int32_t)(rng() % 4);
+    p.max_tokens = 1200;
+    core.add(prompt.data(), (int32_t)prompt.size(), p, 0.0);
+  }
+  int finished = 0, steps = 0;
+  while (core.has_work()) {
+    CHECK(++steps < 200000);
+    const int64_t n = core.schedule_and_pack(header.data(), pay, (int64_t)payload.size() - 1, 0.0);
+    std::vector<int32_t> done;
+    if (n == 0) {
+      done = core.drain_finished();
+    } else {
+      const int32_t T = header[H_T], NA = header[H_NA], S = header[H_S], maxb = header[H_MAXB];
+      CHECK(header[H_PAYLOAD] == n && T > 0 && S >= 0 && maxb > 0);
+      // midx sits 2 words before the end of the payload's last three arrays
+      const int32_t* midx = pay + n - 2 * S;
+      const int32_t* slots = pay + 2 * S + 2 * T;
+      for (int32_t i = 0; i < T; ++i) CHECK(slots[i] >= -1 && slots[i] < 49 * 32);
+      (void)NA;
+      std::vector<int32_t> toks(S);
+      for (int32_t k = 0; k < S; ++k) {
+        const int32_t m = midx[k];
+        if (m < 0) { toks[k] = 0; continue; }
+        const uint32_t* row = masks.data() + (size_t)m * words;
+        std::vector<int32_t> allowed;
+        for (int32_t wd = 0; wd < words; ++wd)
+          for (uint32_t bits = row[wd]; bits; bits &= bits - 1)
+            allowed.push_back(wd * 32 + __builtin_ctz(bits));
+        CHECK(!allowed.empty());
+        toks[k] = allowed[rng() % allowed.size()];
+      }
+      done = core.post(toks.data(), S, 0.0);
+    }
+    for (int32_t id : done) {
+      const Seq& s = core.seq(id);
+      CHECK(s.status == S_FINISHED);
+      CHECK(s.finish == F_STOP || s.finish == F_LENGTH);
+      core.release(id);
+      ++finished;
+    }
+  }
+  CHECK(finished == nreq);
+  CHECK(core.num_preempted > 0);                     // the small pool must have forced it
+  CHECK(core.bm().num_free() == cfg.num_blocks);
+  std::printf("engine core fuzz ok: steps=%d preempted=%lld prefix_hits=%llu\n", steps,
+              (long long)core.num_preempted, (unsigned long long)core.bm().hits);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s grammar.bin [walks] [seed]\n", argv[0]);
@@ -198,12 +279,13 @@ int main(int argc, char** argv) {
   fuzz_block_manager(seed);
   std::printf("block manager fuzz ok\n");
   Blob b = read_blob(argv[1]);
-  Grammar g = build(b);
+  auto g = std::make_shared<Grammar>(build(b));
   auto masks = b.get<uint32_t>("mask_rows");
   int32_t words = b.get<int32_t>("mask_words")[0];
   int32_t budget = b.get<int32_t>("max_tokens")[0];
-  int32_t longest = grammar_walks(g, masks, words, walks, seed);
+  int32_t longest = grammar_walks(*g, masks, words, walks, seed);
   CHECK(longest <= budget);
+  fuzz_engine_core(g, masks, words, seed);
   std::printf("OK\n");
   return 0;
 }

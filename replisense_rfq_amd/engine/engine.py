@@ -32,13 +32,15 @@ from ..utils.config import EngineConfig
 from ..utils.faults import FaultInjector
 from ..utils.trace import trace_range
 from .grammar import get_grammar
+from .. import runtime
 from .kv_cache import KVCache
-from .runner import ModelRunner
-from .scheduler import Scheduler
+from .runner import EXT_MAX, TOKEN_MULTS, ModelRunner
 from .sequence import SamplingParams, Sequence, Status
 from .tokenizer import flavor_for_vocab, get_tokenizer
 
 log = logging.getLogger("replisense_rfq_amd.engine")
+
+FINISH_REASONS = {1: "stop", 2: "length", 3: "grammar_error", 4: "abort", 5: "engine_error"}
 
 
 def resolve_device(spec: str, tp: TPContext) -> torch.device:
@@ -71,7 +73,9 @@ class LLMEngine:
         self.grammar = get_grammar(self.tokenizer.flavor) if self.cfg.grammar else None
         self.runner = ModelRunner(self.model, self.kv, self.cfg,
                                   self.grammar.mask_table() if self.grammar else None, tp)
-        self.scheduler = Scheduler(self.cfg, self.kv)
+        self.core = self._make_core()
+        self.kv.core = self.core
+        self._live: dict[int, Sequence] = {}
         self.capture_s = 0.0
         self.tune_s = 0.0
         if self.device.type == "cuda" and self.cfg.tune_gemm:
@@ -80,12 +84,28 @@ class LLMEngine:
             buckets = [b for b in self.cfg.graph_buckets if b <= self.cfg.max_num_seqs]
             if buckets:
                 self.capture_s = self.runner.capture_graphs(buckets)
+                self.core.set_graph_keys(sorted(self.runner.graphs))
         self.num_steps = 0
         self.step_times: list[float] = []
-        self.timers = {"schedule_s": 0.0, "execute_s": 0.0, "post_s": 0.0}
+        self.timers = {"execute_s": 0.0, "post_s": 0.0}
         self.faults = FaultInjector()
 
     # ------------------------------------------------------------------ setup
+    def _make_core(self):
+        """Native scheduler / packer / post-processor (csrc/runtime/engine_core.cpp)."""
+        c = self.cfg
+        conf = dict(block_size=self.kv.block_size, num_blocks=self.kv.num_blocks - 1,
+                    scratch_block=self.kv.scratch_block, max_num_seqs=c.max_num_seqs,
+                    max_batched_tokens=c.max_batched_tokens, max_model_len=c.max_model_len,
+                    ext_max=EXT_MAX, group=self.model.hq // self.model.hkv, hkv=self.model.hkv,
+                    jump_forward=c.jump_forward, prefix_cache=c.prefix_cache,
+                    is_cuda=self.device.type == "cuda", use_graphs=c.use_graphs,
+                    token_mults=list(TOKEN_MULTS), eos_ids=list(self.tokenizer.eos_ids))
+        g = self.grammar.native if self.grammar is not None else None
+        if self.grammar is not None and g is None:
+            raise RuntimeError("the native grammar automaton failed to build")
+        return runtime.load().EngineCore(conf, g)
+
     def _tune_gemms(self) -> None:
         from ..ops.autotune import tune_model
         from .runner import TOKEN_MULTS
@@ -122,100 +142,64 @@ class LLMEngine:
         if len(prompt_ids) + params.max_tokens > self.cfg.max_model_len:
             params.max_tokens = max(1, self.cfg.max_model_len - len(prompt_ids))
         seq = Sequence(list(prompt_ids), params, callback=callback)
-        if params.grammar and self.grammar is not None:
-            seq.gstate, forced = self.grammar.initial(params.min_items)
-            seq.tokens += forced
-            seq.num_forced += len(forced)
-            seq.mask_idx = self.grammar.mask(seq.gstate)
-        self.scheduler.add(seq)
+        seq.status = Status.WAITING
+        seq.core_id = self.core.add(np.asarray(prompt_ids, np.int32), float(params.temperature),
+                                    int(params.max_tokens), int(params.seed),
+                                    bool(params.grammar and self.grammar is not None),
+                                    int(params.min_items), seq.t_arrival)
+        self._live[seq.core_id] = seq
         return seq
 
     # ------------------------------------------------------------------- step
     def step(self) -> list[Sequence]:
         ts = time.perf_counter()
-        with trace_range("schedule"):
-            plan = self.scheduler.schedule()
-        if plan.empty:
-            return []
-        if self.faults.active:
+        if self.faults.active and self.core.has_work:
             self.faults.on_step(self.num_steps)
-        t0 = time.perf_counter()
         with trace_range("execute"):
-            rows, toks = self.runner.execute(plan)
+            toks = self.runner.execute(self.core, ts)
+        if toks is None:
+            return [self._finalize(i) for i in self.core.drain_finished()]
         now = time.perf_counter()
-        with trace_range("post"):
-            return self._post(plan, rows, toks, now, t0, ts)
-
-    def _post(self, plan, rows, toks, now, t0, ts) -> list[Sequence]:
-        self.timers["schedule_s"] += t0 - ts
-        self.timers["execute_s"] += now - t0
-        self.step_times.append(now - t0)
+        self.timers["execute_s"] += now - ts
+        self.step_times.append(now - ts)
         self.num_steps += 1
-        for s in plan.decode:
-            s.num_cached += 1
-        for s, q in plan.extend:
-            s.num_cached += q
-            self.kv.publish(s)
-            if not s.t_prefill_done and not s.in_prefill:
-                s.t_prefill_done = now
-        # gather sequences that sample this step
-        samp = [(s, int(toks[k])) for k, (s, do) in enumerate(rows) if do]
-        finished: list[Sequence] = []
-        gseqs = [(s, t) for s, t in samp if s.gstate is not None]
-        if gseqs:
-            states = np.array([s.gstate for s, _ in gseqs], np.int32).reshape(-1, 5)
-            tokens = np.array([t for _, t in gseqs], np.int32)
-            masks, offs, forced, ok = self.grammar.batch_advance(states, tokens)
-            for i, (s, t) in enumerate(gseqs):
-                f = forced[offs[i]:offs[i + 1]].tolist()
-                s.tokens.append(t)
-                s.tokens.extend(f)
-                s.num_sampled += 1
-                s.num_forced += len(f)
-                s.gstate = tuple(int(x) for x in states[i])
-                s.mask_idx = int(masks[i])
-                if not s.t_first_token:
-                    s.t_first_token = now
-                if not ok[i]:
-                    self._finish(s, "grammar_error", finished)
-                elif masks[i] < 0:
-                    self._finish(s, "stop", finished)
-                elif s.num_generated >= s.params.max_tokens:
-                    self._finish(s, "length", finished)
-        for s, t in samp:
-            if s.gstate is not None:
-                continue
-            s.tokens.append(t)
-            s.num_sampled += 1
-            if not s.t_first_token:
-                s.t_first_token = now
-            if t in self.tokenizer.eos_ids:
-                self._finish(s, "stop", finished)
-            elif s.num_generated >= s.params.max_tokens:
-                self._finish(s, "length", finished)
+        with trace_range("post"):
+            done = self.core.post(np.ascontiguousarray(toks, np.int32), now)
+            finished = [self._finalize(i) for i in done]
         self.timers["post_s"] += time.perf_counter() - now
         return finished
 
-    def _finish(self, s: Sequence, reason: str, out: list):
-        self.scheduler.finish(s, reason)
-        out.append(s)
+    def _finalize(self, cid: int) -> Sequence:
+        """Copy a finished sequence out of the core, release its record, notify."""
+        s = self._live.pop(cid)
+        info = self.core.info(cid)
+        s.tokens = self.core.tokens(cid).tolist()
+        s.num_cached = info["num_cached"]
+        s.prefix_hit_tokens = info["prefix_hit"]
+        s.num_sampled = info["num_sampled"]
+        s.num_forced = info["num_forced"]
+        s.mask_idx = info["mask_idx"]
+        s.finish_reason = FINISH_REASONS.get(info["finish"], "abort")
+        s.status = Status.FINISHED
+        s.t_first_sched = info["t_first_sched"]
+        s.t_prefill_done = info["t_prefill_done"]
+        s.t_first_token = info["t_first_token"]
+        s.t_finish = info["t_finish"] or time.perf_counter()
+        self.core.release(cid)
         if s.callback is not None:
             try:
                 s.callback(s)
             except Exception:  # pragma: no cover - callbacks must not kill the loop
                 log.exception("sequence callback failed")
+        return s
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work
+        return self.core.has_work
 
     def abort_all(self, reason: str) -> list[Sequence]:
         """Finish every queued/running sequence (releasing its KV blocks)."""
-        out: list[Sequence] = []
-        for s in list(self.scheduler.running) + list(self.scheduler.waiting):
-            if s in self.scheduler.waiting:
-                self.scheduler.waiting.remove(s)
-            self._finish(s, reason, out)
-        return out
+        code = {v: k for k, v in FINISH_REASONS.items()}.get(reason, 4)
+        return [self._finalize(i) for i in self.core.abort_all(code, time.perf_counter())]
 
     def generate(self, prompts: list[list[int]], params=None,
                  seeds: list[int] | None = None) -> list[Sequence]:
@@ -254,10 +238,10 @@ class LLMEngine:
     def stats(self) -> dict:
         st = dict(self.runner.stats)
         st.update({k: round(v, 3) for k, v in self.timers.items()})
-        st.update(self.kv.stats())
-        st["preempted"] = self.scheduler.num_preempted
-        st["running"] = len(self.scheduler.running)
-        st["waiting"] = len(self.scheduler.waiting)
+        st.update(self.kv.stats(self.core))
+        st["preempted"] = self.core.num_preempted
+        st["running"] = self.core.num_running
+        st["waiting"] = self.core.num_waiting
         return st
 
 

@@ -1,5 +1,5 @@
-"""Model runner: StepPlan -> one H2D metadata upload -> forward -> grammar-masked
-sampling -> one D2H of the sampled ids.
+"""Model runner: packed step (from the native EngineCore) -> one H2D metadata
+upload -> forward -> grammar-masked sampling -> one D2H of the sampled ids.
 
 A step's rows are laid out in two sections:
 
@@ -24,8 +24,6 @@ A step's rows are laid out in two sections:
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass
-
 import numpy as np
 import torch
 
@@ -33,7 +31,6 @@ from .. import ops
 from ..models.llama import DecoderLM, ForwardMeta
 from ..parallel.tp import TPContext
 from .kv_cache import KVCache
-from .scheduler import StepPlan
 
 (H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_GNB, H_GTB, H_SPLITS, H_PAYLOAD,
  H_STOP) = range(13)
@@ -59,13 +56,6 @@ def _layout(T, NA, WA, NB, WB, S, maxb):
             ("b_ws", WB), ("b_wq", WB), ("lidx", S), ("midx", S), ("temps", S)]
 
 
-@dataclass
-class Packed:
-    header: np.ndarray
-    payload: np.ndarray            # int32
-    rows: list                     # (seq, samples?) per logits row (rank 0 only)
-
-
 class ModelRunner:
     def __init__(self, model: DecoderLM, kv: KVCache, cfg, mask_table: np.ndarray | None,
                  tp: TPContext):
@@ -84,118 +74,11 @@ class ModelRunner:
         self.graphs: dict[tuple, object] = {}
         self._pinned = None
         self._dev = None
+        self._stage_t = None                 # pinned staging tensor the core packs into
+        self._stage = None                   # its numpy view
+        self._header = np.zeros(HEADER, np.int32)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
                       "pack_s": 0.0}
-
-    # ---------------------------------------------------------------- packing
-    def _graph_key(self, NA: int, T: int):
-        if not self.graphs:
-            return None
-        for nb in self._nb_buckets:
-            if nb < NA:
-                continue
-            for m in TOKEN_MULTS:
-                tb = nb * m
-                if tb >= T and (nb, tb) in self.graphs:
-                    return nb, tb
-            return None
-        return None
-
-    def pack(self, plan: StepPlan) -> Packed:
-        kv, bs, G = self.kv, self.kv.block_size, self.G
-        secA = [(s, 1) for s in plan.decode] + [(s, q) for s, q in plan.extend if q <= EXT_MAX]
-        secB = [(s, q) for s, q in plan.extend if q > EXT_MAX]
-        TA = sum(q for _, q in secA)
-        T = TA + sum(q for _, q in secB)
-        NA, NB = len(secA), len(secB)
-        key = self._graph_key(NA, T) if (self.is_cuda and self.cfg.use_graphs and NB == 0) else None
-        if key:
-            nbk, tbk = key
-            TA_p, NA_p, WA_p, S_p, maxb = tbk, nbk, tbk, nbk, self.max_blocks
-        else:
-            maxb = max([len(s.blocks) for s, _ in secA + secB] + [1])
-        ids = np.zeros(T, np.int32)
-        pos = np.zeros(T, np.int32)
-        slots = np.full(T, -1, np.int32)
-        a_bt = np.full((NA, maxb), kv.scratch_block, np.int32)
-        a_qs, a_ql, a_kvl = (np.zeros(NA, np.int32) for _ in range(3))
-        a_ws, a_wct = [], []
-        rows, lidx = [], []
-        t = 0
-        for j, (s, q) in enumerate(secA):
-            p0 = s.num_cached
-            ids[t:t + q] = s.tokens[p0:p0 + q]
-            pp = np.arange(p0, p0 + q)
-            pos[t:t + q] = pp
-            blk = np.asarray(s.blocks, np.int64)
-            slots[t:t + q] = blk[pp // bs] * bs + pp % bs
-            a_bt[j, : len(s.blocks)] = s.blocks
-            a_qs[j], a_ql[j], a_kvl[j] = t, q, p0 + q
-            nct = (q * G + 15) // 16
-            a_ws += [j] * nct
-            a_wct += list(range(nct))
-            lidx.append(t + q - 1)
-            rows.append((s, p0 + q == len(s.tokens)))
-            t += q
-        b_bt = np.full((NB, maxb), kv.scratch_block, np.int32)
-        b_qs, b_ql, b_kvl = (np.zeros(NB, np.int32) for _ in range(3))
-        b_ws, b_wq = [], []
-        for j, (s, q) in enumerate(secB):
-            p0 = s.num_cached
-            ids[t:t + q] = s.tokens[p0:p0 + q]
-            pp = np.arange(p0, p0 + q)
-            pos[t:t + q] = pp
-            blk = np.asarray(s.blocks, np.int64)
-            slots[t:t + q] = blk[pp // bs] * bs + pp % bs
-            b_bt[j, : len(s.blocks)] = s.blocks
-            b_qs[j], b_ql[j], b_kvl[j] = t - TA, q, p0 + q
-            nqb = (q + 31) // 32
-            b_ws += [j] * nqb
-            b_wq += list(range(nqb))
-            if p0 + q == len(s.tokens):
-                lidx.append(t + q - 1)
-                rows.append((s, True))
-            t += q
-        S = len(lidx)
-        midx = np.full(S, -1, np.int32)
-        temps = np.zeros(S, np.float32)
-        seeds = np.zeros(S, np.int64)
-        for k, (s, _) in enumerate(rows):
-            midx[k] = s.mask_idx if s.params.grammar else -1
-            temps[k] = s.params.temperature
-            seeds[k] = _seed64(s.params.seed, len(s.tokens))
-        WA, WB = len(a_ws), len(b_ws)
-        arrays = dict(ids=ids, pos=pos, slots=slots, a_bt=a_bt, a_qs=a_qs, a_ql=a_ql,
-                      a_kvl=a_kvl, a_ws=np.asarray(a_ws, np.int32),
-                      a_wct=np.asarray(a_wct, np.int32), b_bt=b_bt, b_qs=b_qs, b_ql=b_ql,
-                      b_kvl=b_kvl, b_ws=np.asarray(b_ws, np.int32),
-                      b_wq=np.asarray(b_wq, np.int32), lidx=np.asarray(lidx, np.int32),
-                      midx=midx, temps=temps.view(np.int32), seeds=seeds.view(np.int32))
-        header = np.zeros(HEADER, np.int32)
-        if key:
-            # pad every array to the captured bucket shape
-            pads = dict(ids=(TA_p, 0), pos=(TA_p, 0), slots=(TA_p, -1),
-                        a_qs=(NA_p, 0), a_ql=(NA_p, 0), a_kvl=(NA_p, 1),
-                        a_ws=(WA_p, -1), a_wct=(WA_p, 0), lidx=(S_p, 0), midx=(S_p, -1),
-                        temps=(S_p, 0), seeds=(2 * S_p, 0))
-            for name, (n, fill) in pads.items():
-                a = arrays[name]
-                if a.size < n:
-                    arrays[name] = np.concatenate([a, np.full(n - a.size, fill, np.int32)])
-            bt = np.full((NA_p, maxb), kv.scratch_block, np.int32)
-            bt[:NA] = a_bt
-            arrays["a_bt"] = bt
-            T_h, TA_h, NA_h, WA_h, S_h = TA_p, TA_p, NA_p, WA_p, S_p
-            splits = self._decode_splits(NA_p, 0, graph=True)
-            header[H_GNB], header[H_GTB] = key
-        else:
-            T_h, TA_h, NA_h, WA_h, S_h = T, TA, NA, WA, S
-            splits = self._decode_splits(NA, int(a_kvl.max()) if NA else 0, graph=False)
-        lay = _layout(T_h, NA_h, WA_h, NB, WB, S_h, maxb)
-        payload = np.concatenate([arrays[n].reshape(-1) for n, _ in lay])
-        header[[H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_SPLITS, H_PAYLOAD]] = \
-            [T_h, TA_h, NA_h, WA_h, NB, WB, S_h, maxb, splits, payload.size]
-        return Packed(header, payload, rows)
 
     def _decode_splits(self, NA: int, max_ctx: int, graph: bool) -> int:
         if NA == 0 or not self.is_cuda:
@@ -234,29 +117,49 @@ class ModelRunner:
             pf_q_len=v["b_ql"], pf_kv_len=v["b_kvl"], work_seq=v["b_ws"], work_qblk=v["b_wq"],
             logits_idx=v["lidx"], decode_splits=int(h[H_SPLITS]))
 
+    def _staging(self, words: int) -> np.ndarray:
+        if self._stage is None or self._stage.size < words:
+            if self.is_cuda:
+                self._stage_t = torch.empty(words, dtype=torch.int32, pin_memory=True)
+                self._stage = self._stage_t.numpy()
+            else:
+                self._stage = np.zeros(words, np.int32)
+        return self._stage
+
     def _upload(self, payload: np.ndarray, dst: torch.Tensor | None = None) -> torch.Tensor:
         n = payload.size
         if not self.is_cuda:
             return torch.from_numpy(payload.copy())
-        if self._pinned is None or self._pinned.numel() < n:
-            size = max(n, 1 << 20)
-            self._pinned = torch.empty(size, dtype=torch.int32, pin_memory=True)
-            self._dev = torch.empty(size, dtype=torch.int32, device=self.device)
-        self._pinned[:n].numpy()[:] = payload
+        if self._dev is None or self._dev.numel() < n:
+            self._dev = torch.empty(max(n, 1 << 20), dtype=torch.int32, device=self.device)
+        staged = (self._stage is not None and n > 0
+                  and payload.ctypes.data == self._stage.ctypes.data)
+        if staged:
+            src = self._stage_t[:n]
+        else:
+            if self._pinned is None or self._pinned.numel() < n:
+                self._pinned = torch.empty(max(n, 1 << 20), dtype=torch.int32, pin_memory=True)
+            self._pinned[:n].numpy()[:] = payload
+            src = self._pinned[:n]
         dst = self._dev if dst is None else dst
-        dst[:n].copy_(self._pinned[:n], non_blocking=True)
+        dst[:n].copy_(src, non_blocking=True)
         return dst[:n]
 
     # ---------------------------------------------------------------- execute
-    def execute(self, plan: StepPlan) -> tuple[list, np.ndarray]:
-        """Rank-0 entry: run one step, return (rows, sampled ids per logits row)."""
+    def execute(self, core, now: float):
+        """Rank-0 entry: the native core schedules and packs the step straight into
+        the pinned staging buffer; run it and return the sampled id per logits row
+        (None when there is nothing to run)."""
         t0 = time.perf_counter()
-        pk = self.pack(plan)
+        buf = self._staging(core.payload_bound())
+        n = core.schedule_and_pack(self._header, buf, now)
         self.stats["pack_s"] += time.perf_counter() - t0
+        if n == 0:
+            return None
+        header, payload = self._header, buf[:n]
         if self.tp.enabled:
-            self._broadcast(pk.header, pk.payload)
-        toks = self._run(pk.header, pk.payload)
-        return pk.rows, toks[: len(pk.rows)]
+            self._broadcast(header, payload)
+        return self._run(header, payload)
 
     def _broadcast(self, header, payload):
         dev = self.device if self.is_cuda else "cpu"
@@ -342,8 +245,7 @@ class ModelRunner:
         if not self.is_cuda or not self.cfg.use_graphs:
             return 0.0
         t0 = time.perf_counter()
-        self._nb_buckets = sorted(buckets)
-        keys = [(nb, nb * m) for nb in self._nb_buckets for m in TOKEN_MULTS
+        keys = [(nb, nb * m) for nb in sorted(buckets) for m in TOKEN_MULTS
                 if nb * m <= max(MAX_GRAPH_TOKENS, nb)]
         maxb = self.max_blocks
         pool = torch.cuda.graph_pool_handle()

@@ -89,27 +89,88 @@ def test_chunked_prefill_and_preemption():
         assert s.finish_reason == "stop", s.finish_reason
         RFQResponse(**json.loads(eng.decode_text(s)))
     assert eng.num_steps > 4 * (550 // 96)             # prompts were chunked
-    assert eng.scheduler.num_preempted > 0              # 60 blocks cannot hold 4 sequences
+    assert eng.stats()["preempted"] > 0                 # 60 blocks cannot hold 4 sequences
+    assert eng.stats()["free"] == 59 and not eng.has_work()
 
 
-def test_runner_sections(engine):
-    """Decode rows and short extends go to the paged-decode section, long chunks to prefill."""
-    from replisense_rfq_amd.engine.runner import H_NA, H_NB, H_TA
-    from replisense_rfq_amd.engine.scheduler import StepPlan
-    from replisense_rfq_amd.engine.sequence import SamplingParams, Sequence
+def _core(**kw):
+    conf = dict(block_size=32, num_blocks=64, scratch_block=64, max_num_seqs=8,
+                max_batched_tokens=512, max_model_len=2048, ext_max=EXT_MAX, group=4, hkv=1,
+                jump_forward=True, prefix_cache=True, is_cuda=False, use_graphs=False,
+                eos_ids=[7])
+    conf.update(kw)
+    return runtime.load().EngineCore(conf, None)
 
-    kv = engine.kv
-    mk = lambda n, cached: Sequence(list(range(1, n + 1)), SamplingParams())  # noqa: E731
-    a, b, c = mk(40, 39), mk(50, 45), mk(300, 0)
-    a.num_cached, b.num_cached = 39, 45
-    for s in (a, b, c):
-        kv.grow(s, len(s.tokens))
-    pk = engine.runner.pack(StepPlan(decode=[a], extend=[(b, 5), (c, 300)]))
-    h = pk.header
-    assert (h[H_NA], h[H_TA], h[H_NB]) == (2, 6, 1)
-    assert 5 <= EXT_MAX < 300
-    for s in (a, b, c):
-        kv.free(s)
+
+def _views(header, payload):
+    import torch
+
+    from replisense_rfq_amd.engine.runner import ModelRunner
+
+    return {k: v.numpy() for k, v in ModelRunner._views(torch.from_numpy(payload), header).items()}
+
+
+def test_core_sections_and_layout():
+    """Prefill chunks go to section B, decode rows and short extends to section A;
+    the packed arrays follow runner._layout."""
+    from replisense_rfq_amd.engine.runner import (H_NA, H_NB, H_PAYLOAD, H_S, H_T, H_TA,
+                                                  HEADER, _seed64)
+
+    core = _core()
+    h = np.zeros(HEADER, np.int32)
+    buf = np.zeros(core.payload_bound(), np.int32)
+    a = core.add(np.arange(100, 400, dtype=np.int32), 0.5, 50, 11, False, 0, 0.0)
+    b = core.add(np.arange(1, 11, dtype=np.int32), 0.5, 50, 12, False, 0, 0.0)
+    n = core.schedule_and_pack(h, buf, 0.0)
+    assert n == h[H_PAYLOAD] > 0
+    assert (h[H_T], h[H_TA], h[H_NA], h[H_NB], h[H_S]) == (310, 10, 1, 1, 2)
+    v = _views(h, buf[:n])
+    assert list(v["ids"][:10]) == list(range(1, 11))          # short prompt: section A
+    assert v["ids"][10] == 100 and v["pos"][309] == 299        # long prompt: section B
+    assert list(v["lidx"]) == [9, 309]
+    assert v["seeds"][0] == _seed64(12, 10) and v["seeds"][1] == _seed64(11, 300)
+    assert abs(v["temps"][0] - 0.5) < 1e-7
+    assert list(v["midx"]) == [-1, -1]
+    # slots: contiguous pages starting at the blocks the core handed out
+    assert v["slots"][0] == v["a_bt"][0, 0] * 32
+    done = core.post(np.array([5, 6], np.int32), 1.0)
+    assert done == []
+    n = core.schedule_and_pack(h, buf, 1.0)                    # both decode now
+    assert (h[H_T], h[H_NA], h[H_NB]) == (2, 2, 0)
+    v = _views(h, buf[:n])
+    assert sorted(v["ids"].tolist()) == [5, 6] and sorted(v["a_kvl"].tolist()) == [11, 301]
+    done = core.post(np.array([7, 7], np.int32), 2.0)          # eos for both
+    assert sorted(done) == sorted([a, b])
+    assert core.info(a)["finish"] == 1 and core.tokens(a)[-2:].tolist() == [6, 7]
+    assert core.tokens(b)[-2:].tolist() == [5, 7]
+    assert not core.has_work
+    for i in done:
+        core.release(i)
+
+
+def test_core_prefix_cache_and_preemption():
+    core = _core(num_blocks=24, max_batched_tokens=4096)
+    h = np.zeros(16, np.int32)
+    buf = np.zeros(core.payload_bound(), np.int32)
+    prompt = np.arange(1, 300, dtype=np.int32)
+    a = core.add(prompt, 0.1, 600, 1, False, 0, 0.0)
+    core.schedule_and_pack(h, buf, 0.0)
+    core.post(np.array([9], np.int32), 0.0)
+    b = core.add(prompt, 0.1, 600, 2, False, 0, 0.0)          # shares 9 full prompt blocks
+    core.schedule_and_pack(h, buf, 0.0)
+    core.post(np.array([9, 9], np.int32), 0.0)
+    assert core.info(b)["prefix_hit"] == 9 * 32 and core.prefix_hits >= 1
+    # run until the pool (24 blocks) forces a preemption
+    steps = 0
+    while core.has_work and steps < 2000:
+        n = core.schedule_and_pack(h, buf, 0.0)
+        done = core.post(np.full(h[6], 9, np.int32), 0.0) if n else core.drain_finished()
+        for i in done:
+            assert core.info(i)["finish"] == 2                 # length (pool-bound)
+            core.release(i)
+        steps += 1
+    assert core.num_preempted > 0 and not core.has_work
+    assert core.num_free_blocks == 24
 
 
 def test_async_engine_and_extract_service(engine):

@@ -1,8 +1,9 @@
 """Host runtime under AddressSanitizer + UndefinedBehaviorSanitizer.
 
 GPU ASan is not available on the MI355X pool, so the sanitizer pass covers the
-native host code that runs on the scheduler hot path: the C++ grammar automaton
-and the KV block manager (csrc/runtime/test_runtime.cpp drives both)."""
+native host code that runs on the scheduler hot path: the C++ grammar automaton,
+the KV block manager and the engine core's scheduler / packer / post-processor
+(csrc/runtime/test_runtime.cpp drives all three)."""
 import os
 import shutil
 import subprocess
@@ -22,7 +23,8 @@ def test_runtime_asan_ubsan(tmp_path, flavor):
     subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
                     "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
                     os.path.join(SRC, "test_runtime.cpp"), os.path.join(SRC, "grammar.cpp"),
-                    os.path.join(SRC, "block_manager.cpp"), "-o", str(exe)],
+                    os.path.join(SRC, "block_manager.cpp"), os.path.join(SRC, "engine_core.cpp"),
+                    "-o", str(exe)],
                    check=True, capture_output=True, timeout=300)
     blob = tmp_path / "grammar.bin"
     from tools.dump_grammar import dump
