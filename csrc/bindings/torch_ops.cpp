@@ -23,7 +23,7 @@ void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
-                        float, int, hipStream_t);
+                        float, int, int, hipStream_t);
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                          const int32_t*, int, bf16_t*, int64_t, int, int, float, hipStream_t);
@@ -140,8 +140,9 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
                  const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
-                 int64_t Hkv, double scale, int64_t num_splits) {
+                 int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode: tiles_per_item in {1, 2}");
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
   CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
   CHECK_I32(work_seq); CHECK_I32(work_ct);
@@ -155,7 +156,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   TORCH_CHECK(block_tables.size(0) >= seq_q_len.numel() && seq_kv_len.numel() >= seq_q_len.numel()
                   && seq_q_start.numel() >= seq_q_len.numel(),
               "attn_decode: per-sequence arrays mismatch");
-  TORCH_CHECK(num_splits >= 1 && num_splits <= 64, "attn_decode: num_splits in [1, 64]");
+  TORCH_CHECK(num_splits >= 1 && num_splits <= 16, "attn_decode: num_splits in [1, 16]");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
@@ -170,7 +171,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
-                          (float)scale, num_splits, cur_stream());
+                          (float)scale, num_splits, tiles_per_item, cur_stream());
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
@@ -308,7 +309,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
-        "int num_splits) -> ()");
+        "int num_splits, int tiles_per_item=1) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale) -> ()");

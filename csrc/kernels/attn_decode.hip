@@ -32,7 +32,9 @@ namespace rfq {
 constexpr int kD = 128;
 constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
 
-__global__ __launch_bounds__(64) void attn_decode_kernel(
+// (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over
+template <int NT>
+__global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     int bt_stride, const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
@@ -50,31 +52,47 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
   if (seq < 0) return;       // padding work item (graph-captured buckets)
   const int ql = seq_q_len[seq];
   const int kvl = seq_kv_len[seq];
-  const int col = work_ct[w] * 16 + c;
-  const bool cvalid = col < ql * G;
-  const int qi = cvalid ? col / G : 0;
-  const int h = kvh * G + (cvalid ? col % G : 0);
-  const int qrow = seq_q_start[seq] + qi;
-  const int lim = kvl - ql + qi + 1;  // keys [0, lim) visible to this column
+  // NT column tiles per work item share every K fragment and V tile they load
+  bool act[NT], cvalid[NT];
+  int h[NT], qrow[NT], lim[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tile = work_ct[w] * NT + t;
+    act[t] = tile * 16 < ql * G;                       // wave-uniform
+    const int col = tile * 16 + c;
+    cvalid[t] = col < ql * G;
+    const int qi = cvalid[t] ? col / G : 0;
+    h[t] = kvh * G + (cvalid[t] ? col % G : 0);
+    qrow[t] = seq_q_start[seq] + qi;
+    lim[t] = kvl - ql + qi + 1;                        // keys [0, lim) visible
+  }
 
   int tps = (kvl + num_splits - 1) / num_splits;
   tps = (tps + kPage - 1) / kPage * kPage;
   const int start = split * tps;
   const int end = min(kvl, start + tps);
 
-  float m_run = -INFINITY, l_run = 0.f;
-  f32x4 o[8];
+  float m_run[NT], l_run[NT];
+  f32x4 o[NT][8];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) o[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NT; ++t) {
+    m_run[t] = -INFINITY;
+    l_run[t] = 0.f;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) o[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
   if (start < end && ql > 0) {
     // Q^T fragments: B[k = dh][col]; lane holds Q[qrow, h][32ks + 8g .. +7]
-    s16x8 qf[4];
-    const bf16_t* qp = q + (int64_t)qrow * q_stride + (int64_t)h * kD;
+    s16x8 qf[NT][4];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qf[ks] = reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
-      if (!cvalid) qf[ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < NT; ++t) {
+      const bf16_t* qp = q + (int64_t)qrow[t] * q_stride + (int64_t)h[t] * kD;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        qf[t][ks] = reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
+        if (!cvalid[t]) qf[t][ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
     const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
 
@@ -102,50 +120,55 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         reinterpret_cast<s16x8*>(v_lds + row * kD)[pch] = v;
       }
 
-      // ---- S^T = K Q^T ----
-      f32x4 s[2];
+      s16x8 pb[NT];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        s[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < NT; ++t) {
+        if (!act[t]) continue;
+        // ---- S^T = K Q^T ----
+        f32x4 s[2];
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[mt][ks]), as_bf16x8(qf[ks]),
-                                                          s[mt], 0, 0, 0);
-      }
-      // lane holds S^T[key = 16mt + 4g + i][column c]
-      float mx = -INFINITY;
+        for (int mt = 0; mt < 2; ++mt) {
+          s[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = 16 * mt + 4 * g + i;
-          float v = s[mt][i] * scale_log2;
-          if (key >= nvalid || kt + key >= lim) v = -INFINITY;
-          s[mt][i] = v;
-          mx = fmaxf(mx, v);
+          for (int ks = 0; ks < 4; ++ks)
+            s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[mt][ks]),
+                                                            as_bf16x8(qf[t][ks]), s[mt], 0, 0, 0);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;  // fully-masked column so far
-      const float alpha = fast_exp2(m_run - m_use);
-      float psum = 0.f;
-      float p[8];
+        // lane holds S^T[key = 16mt + 4g + i][column c]
+        float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        p[j] = fast_exp2(s[j >> 2][j & 3] - m_use);
-        psum += p[j];
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = 16 * mt + 4 * g + i;
+            float v = s[mt][i] * scale_log2;
+            if (key >= nvalid || kt + key >= lim[t]) v = -INFINITY;
+            s[mt][i] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_run[t], mx);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;  // fully-masked column so far
+        const float alpha = fast_exp2(m_run[t] - m_use);
+        float psum = 0.f;
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          p[j] = fast_exp2(s[j >> 2][j & 3] - m_use);
+          psum += p[j];
+        }
+        l_run[t] = l_run[t] * alpha + psum;
+        m_run[t] = m_new;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) o[t][m] *= alpha;
+        // P^T as B operand: element j <-> key pi(g,j) = (j<4 ? 4g+j : 16+4g+j-4)
+        pb[t] = pack8(p);
       }
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) o[m] *= alpha;
-      // P^T as B operand: element j <-> key pi(g,j) = (j<4 ? 4g+j : 16+4g+j-4)
-      s16x8 pb = pack8(p);
 
       __syncthreads();  // V tile visible (single wave: orders the LDS writes)
 
-      // ---- O^T += V^T P^T ----
+      // ---- O^T += V^T P^T (one transposed V read feeds every tile) ----
       const int q4 = c >> 2, p4 = c & 3;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -154,36 +177,42 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(
         const s16x4 a0 = ds_read_tr16(v_lds + r0 * kD + ((ch ^ ((r0 & 7) << 1)) * 8) + sub);
         const s16x4 a1 = ds_read_tr16(v_lds + r1 * kD + ((ch ^ ((r1 & 7) << 1)) * 8) + sub);
         const s16x8 a = (s16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        o[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb), o[m], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (act[t])
+            o[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb[t]),
+                                                              o[t][m], 0, 0, 0);
       }
       __syncthreads();  // before the next tile overwrites v_lds
     }
   }
 
-  // total softmax denominator for column c (lanes c, c+16, c+32, c+48)
-  float l_tot = l_run;
-  l_tot += __shfl_xor(l_tot, 16, 64);
-  l_tot += __shfl_xor(l_tot, 32, 64);
-  if (!cvalid) return;
-
-  if (num_splits == 1) {
-    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-    bf16_t* orow = out + (int64_t)qrow * out_stride + (int64_t)h * kD;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      uint2 wv;
-      wv.x = pack_bf16x2(o[m][0] * inv, o[m][1] * inv);
-      wv.y = pack_bf16x2(o[m][2] * inv, o[m][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
-    }
-  } else {
-    const int64_t pidx = ((int64_t)qrow * Hq + h) * num_splits + split;
-    float* po = part_o + pidx * kD;
+  for (int t = 0; t < NT; ++t) {
+    // total softmax denominator for column c (lanes c, c+16, c+32, c+48)
+    float l_tot = l_run[t];
+    l_tot += __shfl_xor(l_tot, 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    if (!cvalid[t]) continue;
+    if (num_splits == 1) {
+      const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+      bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[m];
-    if (g == 0) {
-      part_ml[pidx * 2 + 0] = m_run;
-      part_ml[pidx * 2 + 1] = l_tot;
+      for (int m = 0; m < 8; ++m) {
+        uint2 wv;
+        wv.x = pack_bf16x2(o[t][m][0] * inv, o[t][m][1] * inv);
+        wv.y = pack_bf16x2(o[t][m][2] * inv, o[t][m][3] * inv);
+        *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
+      }
+    } else {
+      const int64_t pidx = ((int64_t)qrow[t] * Hq + h[t]) * num_splits + split;
+      float* po = part_o + pidx * kD;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[t][m];
+      if (g == 0) {
+        part_ml[pidx * 2 + 0] = m_run[t];
+        part_ml[pidx * 2 + 1] = l_tot;
+      }
     }
   }
 }
@@ -195,17 +224,27 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
   const int bh = blockIdx.x;
   const int b = bh / Hq, h = bh % Hq;
   const int d = threadIdx.x;
+  __shared__ float ml_s[2 * 16];
   const float* ml = part_ml + (int64_t)bh * num_splits * 2;
+  if (d < 2 * num_splits) ml_s[d] = ml[d];     // num_splits <= 16: one load per lane
+  // issue every split's partial load before the LDS round trip
+  float po[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s)
+    po[s] = s < num_splits ? part_o[((int64_t)bh * num_splits + s) * kD + d] : 0.f;
+  __syncthreads();
   float gm = -INFINITY;
-  for (int s = 0; s < num_splits; ++s) gm = fmaxf(gm, ml[2 * s]);
+  for (int s = 0; s < num_splits; ++s) gm = fmaxf(gm, ml_s[2 * s]);
   float num = 0.f, den = 0.f;
   if (gm != -INFINITY) {
-    for (int s = 0; s < num_splits; ++s) {
-      const float ms = ml[2 * s];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s >= num_splits) break;
+      const float ms = ml_s[2 * s];
       if (ms == -INFINITY) continue;
       const float wgt = fast_exp2(ms - gm);
-      num += wgt * part_o[((int64_t)bh * num_splits + s) * kD + d];
-      den += wgt * ml[2 * s + 1];
+      num += wgt * po[s];
+      den += wgt * ml_s[2 * s + 1];
     }
   }
   out[(int64_t)b * out_stride + (int64_t)h * kD + d] = f2bf(den > 0.f ? num / den : 0.f);
@@ -218,14 +257,20 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
                         const int32_t* seq_kv_len, const int32_t* work_seq,
                         const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
                         float* part_o, float* part_ml, int Hq, int Hkv, float scale,
-                        int num_splits, hipStream_t s) {
+                        int num_splits, int tiles_per_item, hipStream_t s) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_splits, Hkv, W);
-  attn_decode_kernel<<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables, bt_stride,
-                                         seq_q_start, seq_q_len, seq_kv_len, work_seq, work_ct,
-                                         out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
-                                         num_splits);
+  if (tiles_per_item == 2)
+    attn_decode_kernel<2><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                              bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                              work_seq, work_ct, out, out_stride, part_o, part_ml,
+                                              Hq, Hkv, scale_log2, num_splits);
+  else
+    attn_decode_kernel<1><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                              bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                              work_seq, work_ct, out, out_stride, part_o, part_ml,
+                                              Hq, Hkv, scale_log2, num_splits);
   if (num_splits > 1)
     attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                         num_splits);

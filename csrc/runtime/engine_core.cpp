@@ -285,9 +285,11 @@ int64_t EngineCore::schedule_and_pack(int32_t* header, int32_t* payload, int64_t
   for (int32_t id : decode_) A.push_back({id, 1});
   for (auto& r : extend_) (r.q <= cfg_.ext_max ? A : B).push_back(r);
   int32_t TA = 0, TB = 0, WA = 0, WB = 0, maxb = 1, max_ctx = 0;
+  const int32_t NTL = std::max(1, cfg_.decode_tiles);
+  auto items = [&](int32_t q) { return ((q * G + 15) / 16 + NTL - 1) / NTL; };
   for (auto& r : A) {
     TA += r.q;
-    WA += (r.q * G + 15) / 16;
+    WA += items(r.q);
     maxb = std::max(maxb, (int32_t)seqs_[r.id].blocks.size());
     max_ctx = std::max(max_ctx, seqs_[r.id].num_cached + r.q);
   }
@@ -354,7 +356,7 @@ int64_t EngineCore::schedule_and_pack(int32_t* header, int32_t* payload, int64_t
     a_qs[j] = t;
     a_ql[j] = r.q;
     a_kvl[j] = p0 + r.q;
-    const int32_t nct = (r.q * G + 15) / 16;
+    const int32_t nct = items(r.q);
     for (int32_t c = 0; c < nct; ++c, ++w) {
       a_ws[w] = j;
       a_wct[w] = c;
@@ -413,7 +415,7 @@ int64_t EngineCore::schedule_and_pack(int32_t* header, int32_t* payload, int64_t
   }
   header[H_T] = Th; header[H_TA] = TAh; header[H_NA] = NAh; header[H_WA] = WAh;
   header[H_NB] = NB; header[H_WB] = WB; header[H_S] = Sh; header[H_MAXB] = maxb;
-  header[H_SPLITS] = splits; header[H_PAYLOAD] = (int32_t)need;
+  header[H_SPLITS] = splits; header[H_PAYLOAD] = (int32_t)need; header[H_TILES] = NTL;
   ++num_steps;
   return need;
 }

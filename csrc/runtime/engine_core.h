@@ -76,6 +76,7 @@ struct CoreConfig {
   int32_t ext_max = 32;                  // extends up to this many tokens go to section A
   int32_t group = 4;                     // q heads per kv head (decode work-item tiling)
   int32_t hkv = 8;                       // local kv heads (decode split heuristic)
+  int32_t decode_tiles = 1;              // 16-column tiles per decode attention work item
   bool jump_forward = true;
   bool prefix_cache = true;
   bool is_cuda = true;
@@ -87,7 +88,7 @@ struct CoreConfig {
 // header slots (must match runner.py)
 enum : int {
   H_T = 0, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_GNB, H_GTB, H_SPLITS, H_PAYLOAD, H_STOP,
-  HEADER = 16
+  H_TILES, HEADER = 16
 };
 
 class EngineCore {

@@ -154,6 +154,7 @@ PYBIND11_MODULE(_runtime, m) {
              geti("ext_max", cfg.ext_max);
              geti("group", cfg.group);
              geti("hkv", cfg.hkv);
+             geti("decode_tiles", cfg.decode_tiles);
              getb("jump_forward", cfg.jump_forward);
              getb("prefix_cache", cfg.prefix_cache);
              getb("is_cuda", cfg.is_cuda);

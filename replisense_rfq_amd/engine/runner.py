@@ -33,7 +33,7 @@ from ..parallel.tp import TPContext
 from .kv_cache import KVCache
 
 (H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_GNB, H_GTB, H_SPLITS, H_PAYLOAD,
- H_STOP) = range(13)
+ H_STOP, H_TILES) = range(14)
 HEADER = 16
 SAMPLE_SPLITS = 8
 EXT_MAX = 32                 # extends up to this many tokens use the decode kernel
@@ -77,6 +77,7 @@ class ModelRunner:
         self._stage_t = None                 # pinned staging tensor the core packs into
         self._stage = None                   # its numpy view
         self._header = np.zeros(HEADER, np.int32)
+        self.decode_tiles = int(getattr(cfg, "decode_tiles", 1))
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
                       "pack_s": 0.0}
 
@@ -115,7 +116,8 @@ class ModelRunner:
             dec_kv_len=v["a_kvl"], dec_work_seq=v["a_ws"], dec_work_ct=v["a_wct"],
             num_prefill_tokens=T - TA, pf_block_tables=v["b_bt"], pf_q_start=v["b_qs"],
             pf_q_len=v["b_ql"], pf_kv_len=v["b_kvl"], work_seq=v["b_ws"], work_qblk=v["b_wq"],
-            logits_idx=v["lidx"], decode_splits=int(h[H_SPLITS]))
+            logits_idx=v["lidx"], decode_splits=int(h[H_SPLITS]),
+            decode_tiles=max(1, int(h[H_TILES])))
 
     def _staging(self, words: int) -> np.ndarray:
         if self._stage is None or self._stage.size < words:
@@ -253,6 +255,7 @@ class ModelRunner:
             header = np.zeros(HEADER, np.int32)
             header[[H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_SPLITS]] = \
                 [tb, tb, nb, tb, 0, 0, nb, maxb, self._decode_splits(nb, 0, graph=True)]
+            header[H_TILES] = self.decode_tiles
             n = sum(k for _, k in _layout(tb, nb, tb, 0, 0, nb, maxb))
             gbuf = torch.zeros(n, dtype=torch.int32, device=self.device)
             v = self._views(gbuf, header)

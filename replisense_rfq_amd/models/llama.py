@@ -56,6 +56,7 @@ class ForwardMeta:
     work_qblk: torch.Tensor | None = None          # [W]
     logits_idx: torch.Tensor | None = None         # [S] int64 rows needing logits
     decode_splits: int = 1
+    decode_tiles: int = 1          # column tiles per decode work item (attn_decode.hip)
     extra: dict = field(default_factory=dict)
 
     @property
@@ -127,7 +128,8 @@ class DecoderLM:
                 ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                                 m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
                                 hq, hkv, self.scale,
-                                m.decode_splits if dec_parts is not None else 1)
+                                m.decode_splits if dec_parts is not None else 1,
+                                m.decode_tiles)
             if m.num_prefill_tokens > 0:
                 ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                                  m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,

@@ -106,8 +106,10 @@ def _block_tables(lens, nblocks, device, seed=0):
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
 @pytest.mark.parametrize("splits", [1, 4])
-def test_attn_decode(gpu, Hq, Hkv, splits):
-    """Decode rows (q=1) and short extend rows (q>1, causal inside the extend)."""
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_attn_decode(gpu, Hq, Hkv, splits, tiles):
+    """Decode rows (q=1) and short extend rows (q>1, causal inside the extend); a work
+    item covers `tiles` 16-column tiles of a sequence."""
     torch.manual_seed(4)
     G = Hq // Hkv
     cases = [(1, 1), (1, 31), (1, 32), (1, 33), (1, 700), (5, 129), (9, 2049), (3, 3), (1, 64)]
@@ -119,7 +121,7 @@ def test_attn_decode(gpu, Hq, Hkv, splits):
     qs = [sum(qlens[:i]) for i in range(len(qlens))]
     ws, wct = [], []
     for i, ql in enumerate(qlens):
-        for ct in range((ql * G + 15) // 16):
+        for ct in range(((ql * G + 15) // 16 + tiles - 1) // tiles):
             ws.append(i)
             wct.append(ct)
     ws.append(-1)          # a padding work item must be ignored
@@ -131,11 +133,11 @@ def test_attn_decode(gpu, Hq, Hkv, splits):
     pm = torch.empty(T * Hq * splits * 2, device=gpu)
     scale = 1 / math.sqrt(128)
     ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct), out, po,
-                    pm, Hq, Hkv, scale, splits)
+                    pm, Hq, Hkv, scale, splits, tiles)
     exp = torch.zeros(T, Hq * 128, dtype=BF)
     ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
                      torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
-    _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits}")
+    _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits} tiles={tiles}")
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
