@@ -187,3 +187,14 @@ def test_server_config_env(monkeypatch):
     assert c["port"] == 9123 and c["log_level"] == "debug" and c["reload"] is False
     monkeypatch.setenv("RFQ_BACKEND", "mock")
     assert server_config()["reload"] is True
+
+
+def test_process_time_header_and_http_exception_envelope():
+    r = client.get("/")
+    assert float(r.headers["X-Process-Time"]) >= 0.0
+    app.dependency_overrides[get_field_generator] = lambda: mock_generator()
+    r = client.post("/parse-text/", json={"text": "  "})  # HTTPException -> error envelope
+    assert r.status_code == 400
+    body = r.json()
+    assert set(body) == {"success", "error", "details", "timestamp"}
+    assert body["details"] == "POST /parse-text/"
