@@ -54,8 +54,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--docs-per-step", type=int, default=1024)
-    ap.add_argument("--max-num-seqs", type=int, default=1024)
+    ap.add_argument("--docs-per-step", type=int, default=2048)
+    ap.add_argument("--max-num-seqs", type=int, default=2048)
     ap.add_argument("--latency-runs", type=int, default=5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump-forward", action="store_true")
