@@ -39,6 +39,8 @@ void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_
                              int, int, int, int, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
                         int64_t, hipStream_t);
+void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
+                       int, bf16_t*, int64_t, int, int, int, bool, bool, hipStream_t);
 }  // namespace rfq
 
 namespace {
@@ -246,6 +248,25 @@ void moe_topk(const Tensor& router_logits, int64_t topk, bool renorm, const Tens
 // Sort (token, k) pairs by expert, pad each expert's segment to a multiple of
 // `block_m`.  Outputs: sorted_ids [max_padded] (token*k+slot, or -1 padding),
 // expert_of_block [max_blocks], expert_offsets [E+1], num_blocks [1].
+// Per-expert weight-streaming GEMM for small token counts (gemm_skinny.hip).
+void moe_skinny(const Tensor& x, const Tensor& sorted_ids, int64_t topk,
+                const Tensor& expert_offsets, const Tensor& w, const Tensor& out, bool gated,
+                bool gather, int64_t max_rows) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(out); CHECK_I32(sorted_ids); CHECK_I32(expert_offsets);
+  TORCH_CHECK(w.dim() == 3 && w.is_contiguous(), "moe_skinny: w must be [E, N, K] contiguous");
+  const int E = w.size(0), K = w.size(2);
+  const int n_out = out.size(1);
+  TORCH_CHECK(x.size(1) == K && K % 128 == 0, "moe_skinny: K mismatch or K % 128 != 0");
+  TORCH_CHECK(w.size(1) == (gated ? 2 : 1) * n_out && n_out % 16 == 0, "moe_skinny: N mismatch");
+  TORCH_CHECK(expert_offsets.numel() >= E + 1, "moe_skinny: expert_offsets too small");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "moe_skinny: alignment");
+  TORCH_CHECK(out.size(0) >= sorted_ids.numel() || !gather, "moe_skinny: out rows < sorted rows");
+  rfq::launch_moe_skinny(bp(x), x.stride(0), sorted_ids.data_ptr<int32_t>(), (int)topk,
+                         expert_offsets.data_ptr<int32_t>(), bp(w), K, bpm(out), out.stride(0), E,
+                         n_out, (int)max_rows, gated, gather, cur_stream());
+}
+
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
                const Tensor& inv_pos, const Tensor& expert_of_block,
                const Tensor& expert_offsets, const Tensor& num_blocks) {
@@ -303,6 +324,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("moe_skinny(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
+        "Tensor(a!) out, bool gated, bool gather, int max_rows) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start) -> ()");
   m.def("rope_kv(Tensor(a!) qkv, Tensor positions, Tensor cos_sin, Tensor slot_mapping, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv) -> ()");
@@ -330,6 +353,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);
   m.impl("rope_kv", &rope_kv);
   m.impl("attn_decode", &attn_decode);

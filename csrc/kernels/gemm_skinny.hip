@@ -178,4 +178,180 @@ void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, in
 #undef SK_CASE
 }
 
+// ---------------------------------------------------------------------------
+// MoE latency path: the same weight-streaming structure applied per expert.
+//
+// Rows are the (token, slot) pairs grouped by expert by moe_align (segments
+// [expert_offsets[e], expert_offsets[e+1]) padded to 16).  One workgroup owns a
+// 16-column output tile of one expert; experts with no rows return before
+// touching their weights, so a decode step streams only the routed experts
+// (2 of 8 for one token) instead of 128-row-padded tiles of every block.
+//   GATHER: X rows are looked up through sorted_ids (pair -> token), so the
+//           routed activations are never materialised.
+//   GATED:  the tile computes the gate rows [n0, n0+16) and the matching up rows
+//           [up_off + n0, ...) of w13 together and writes silu(gate) * up — the
+//           w13 GEMM, SwiGLU and its [rows, 2F] intermediate in one pass.
+template <int MT, bool GATED, bool GATHER, int NW, int U>
+__global__ __launch_bounds__(NW * 64) void moe_skinny_kernel(
+    const bf16_t* __restrict__ X, int64_t ldx, const int32_t* __restrict__ sorted_ids, int topk,
+    const int32_t* __restrict__ expert_offsets, const bf16_t* __restrict__ W,
+    int64_t w_expert_stride, int K, int up_off, bf16_t* __restrict__ Y, int64_t ldy,
+    int tiles_per_expert) {
+  constexpr int NT = GATED ? 2 : 1;
+  __shared__ f32x4 red[NW][NT * MT][64];
+  const int e = blockIdx.x / tiles_per_expert, tile = blockIdx.x % tiles_per_expert;
+  const int r0 = expert_offsets[e], r1 = expert_offsets[e + 1];
+  if (r0 >= r1) return;                              // expert not routed this step
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = tile * 16;
+  const int nks = K >> 7;
+  const int ks0 = wave * nks / NW, ks1 = (wave + 1) * nks / NW;
+  const bf16_t* we = W + (int64_t)e * w_expert_stride;
+  const bf16_t* wp[NT];
+  wp[0] = we + (int64_t)(n0 + r) * K + g * 8;
+  if (GATED) wp[NT - 1] = we + (int64_t)(up_off + n0 + r) * K + g * 8;
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  for (int mb = r0; mb < r1; mb += 16 * MT) {
+    const bf16_t* xp[MT];
+    bool xv[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int row = mb + t * 16 + r;
+      bool v = row < r1;
+      int src = row;
+      if (GATHER) {
+        const int sid = v ? sorted_ids[row] : -1;
+        v = sid >= 0;
+        src = v ? sid / topk : 0;
+      }
+      xv[t] = v;
+      xp[t] = X + (int64_t)(v ? src : 0) * ldx + g * 8;
+    }
+    f32x4 acc[NT][MT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int ks = ks0;
+    for (; ks + U <= ks1; ks += U) {
+      s16x8 w[U][NT][4], x[U][MT][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * 128 + j * 32);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            x[u][t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + (ks + u) * 128 + j * 32)
+                               : zero;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int a = 0; a < NT; ++a)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+              acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  as_bf16x8(w[u][a][j]), as_bf16x8(x[u][t][j]), acc[a][t], 0, 0, 0);
+    }
+    for (; ks < ks1; ++ks) {
+      s16x8 w[NT][4], x[MT][4];
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[a][j] = ldw<false>(wp[a] + (int64_t)ks * 128 + j * 32);
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + ks * 128 + j * 32) : zero;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                as_bf16x8(w[a][j]), as_bf16x8(x[t][j]), acc[a][t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) red[wave][a * MT + t][lane] = acc[a][t];
+    __syncthreads();
+    for (int t = wave; t < MT; t += NW) {
+      f32x4 s = red[0][t][lane];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) s += red[w2][t][lane];
+      if (GATED) {
+        f32x4 u = red[0][MT + t][lane];
+#pragma unroll
+        for (int w2 = 1; w2 < NW; ++w2) u += red[w2][MT + t][lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[i] = s[i] / (1.f + __expf(-s[i])) * u[i];
+      }
+      const int row = mb + t * 16 + r;
+      if (row < r1) {
+        uint2 v;
+        v.x = pack_bf16x2(s[0], s[1]);
+        v.y = pack_bf16x2(s[2], s[3]);
+        *reinterpret_cast<uint2*>(Y + (int64_t)row * ldy + n0 + g * 4) = v;
+      }
+    }
+    __syncthreads();                                   // red is reused by the next chunk
+  }
+}
+
+template <int MT, bool GATED, bool GATHER>
+static void moe_skinny_cfg(const bf16_t* X, int64_t ldx, const int32_t* sorted_ids, int topk,
+                           const int32_t* expert_offsets, const bf16_t* W, int64_t wstride,
+                           int K, int up_off, bf16_t* Y, int64_t ldy, int E, int n_out,
+                           hipStream_t s) {
+  constexpr int U = MT == 1 ? 4 : (MT == 2 ? 3 : 2);
+  const int tiles = n_out / 16;
+  hipLaunchKernelGGL((moe_skinny_kernel<MT, GATED, GATHER, 4, U>), dim3(E * tiles), dim3(256), 0,
+                     s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, up_off, Y, ldy,
+                     tiles);
+}
+
+// gated: W [E, 2*n_out, K] (gate | up), Y [rows, n_out] = silu(X W_g^T) * (X W_u^T)
+// else:  W [E, n_out, K], Y [rows, n_out]
+void launch_moe_skinny(const bf16_t* X, int64_t ldx, const int32_t* sorted_ids, int topk,
+                       const int32_t* expert_offsets, const bf16_t* W, int K, bf16_t* Y,
+                       int64_t ldy, int E, int n_out, int max_rows, bool gated, bool gather,
+                       hipStream_t s) {
+  const int MT = max_rows <= 16 ? 1 : (max_rows <= 32 ? 2 : (max_rows <= 48 ? 3 : 4));
+  const int64_t wstride = (int64_t)(gated ? 2 * n_out : n_out) * K;
+#define MS_CASE(mt)                                                                            \
+  case mt:                                                                                     \
+    if (gated && gather)                                                                       \
+      moe_skinny_cfg<mt, true, true>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K,  \
+                                     n_out, Y, ldy, E, n_out, s);                              \
+    else if (gated)                                                                            \
+      moe_skinny_cfg<mt, true, false>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, \
+                                      n_out, Y, ldy, E, n_out, s);                             \
+    else if (gather)                                                                           \
+      moe_skinny_cfg<mt, false, true>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, \
+                                      0, Y, ldy, E, n_out, s);                                 \
+    else                                                                                       \
+      moe_skinny_cfg<mt, false, false>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride,   \
+                                       K, 0, Y, ldy, E, n_out, s);                             \
+    break;
+  switch (MT) {
+    MS_CASE(1)
+    MS_CASE(2)
+    MS_CASE(3)
+    default: MS_CASE(4)
+  }
+#undef MS_CASE
+}
+
 }  // namespace rfq

@@ -18,6 +18,8 @@ from .. import ops
 from ..ops import reference as ref
 
 BLOCK_M = 128
+BLOCK_S = 16            # expert segment padding on the small-batch path
+SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
 
 
 @dataclass
@@ -51,7 +53,7 @@ class MoEBuffers:
             ids=torch.empty(max_tokens, topk, **i32),
             sorted_ids=torch.empty(cap, **i32),
             inv_pos=torch.empty(n, **i32),
-            expert_of_block=torch.empty(nb, **i32),
+            expert_of_block=torch.empty(max(nb, (n + E * (BLOCK_S - 1)) // BLOCK_S + 1), **i32),
             expert_offsets=torch.empty(E + 1, **i32),
             num_blocks=torch.empty(1, **i32),
             xs=torch.empty(cap, d, dtype=dtype, device=device),
@@ -74,9 +76,26 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     # buffers are sliced to this step's token count but keep their capacity-based
     # padding so the grouped GEMM grid is fixed for a given bucket
     n = T * topk
+    w, ids = bufs.weights[:T], bufs.ids[:T]
+    if T <= SKINNY_MAX_TOKENS:
+        # decode / short-extend steps: stream only the routed experts' weights,
+        # gather rows on the fly, SwiGLU fused into the w13 pass
+        ops.moe_topk(logits, topk, True, w, ids)
+        cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
+        sorted_ids = bufs.sorted_ids[:cap]
+        ops.moe_align(ids, E, BLOCK_S, sorted_ids, bufs.inv_pos[:n],
+                      bufs.expert_of_block[:cap // BLOCK_S], bufs.expert_offsets,
+                      bufs.num_blocks)
+        F = w2.shape[2]
+        act = bufs.act[:cap]
+        y = bufs.y[:cap]
+        ops.moe_skinny(x, sorted_ids, topk, bufs.expert_offsets, w13, act, True, True, n)
+        ops.moe_skinny(act, sorted_ids, topk, bufs.expert_offsets, w2, y, False, False, n)
+        assert act.shape[1] == F
+        ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
+        return out
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
     nb = cap // BLOCK_M
-    w, ids = bufs.weights[:T], bufs.ids[:T]
     ops.moe_topk(logits, topk, True, w, ids)
     sorted_ids, eob = bufs.sorted_ids[:cap], bufs.expert_of_block[:nb]
     ops.moe_align(ids, E, BLOCK_M, sorted_ids, bufs.inv_pos[:n], eob, bufs.expert_offsets,

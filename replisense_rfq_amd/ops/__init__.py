@@ -14,7 +14,7 @@ from . import reference as ref
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
-    "moe_combine", "native_available", "linear", "linear_plan", "set_linear_plan",
+    "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan", "set_linear_plan",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -201,6 +201,12 @@ def moe_gather(x, sorted_ids, topk, out):
 
 def moe_grouped_gemm(x, w, out, expert_of_block, num_blocks):
     _native.ops().moe_grouped_gemm(x, w, out, expert_of_block, num_blocks)
+
+
+def moe_skinny(x, sorted_ids, topk, expert_offsets, w, out, gated, gather, max_rows):
+    """Per-expert weight-streaming GEMM (small token counts); see gemm_skinny.hip."""
+    _native.ops().moe_skinny(x, sorted_ids, topk, expert_offsets, w, out, gated, gather,
+                             max_rows)
 
 
 def moe_combine(y, inv_pos, weights, topk, out):

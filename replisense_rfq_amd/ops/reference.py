@@ -152,7 +152,10 @@ def sample(logits: torch.Tensor, mask_table: torch.Tensor | None, mask_idx: torc
 
 def moe_topk(router_logits, topk: int, renorm: bool):
     p = torch.softmax(router_logits.float(), -1)
-    w, ids = torch.topk(p, topk, dim=-1)
+    # ties (equal bf16 logits) go to the lower expert index, as in moe_topk_kernel
+    order = torch.sort(router_logits.float(), dim=-1, descending=True, stable=True).indices
+    ids = order[..., :topk]
+    w = p.gather(-1, ids)
     if renorm:
         w = w / w.sum(-1, keepdim=True)
     return w, ids.int()
