@@ -8,6 +8,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstring>
 
 namespace rfq {
 typedef uint16_t bf16_t;
@@ -39,6 +40,10 @@ void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_
                              int, int, int, int, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
                         int64_t, hipStream_t);
+int64_t car_signal_bytes();
+hipError_t car_alloc(int64_t, void**);
+void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
+uint32_t car_read_error(const void*);
 void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
                        int, bf16_t*, int64_t, int, int, int, bool, bool, hipStream_t);
 }  // namespace rfq
@@ -267,6 +272,57 @@ void moe_skinny(const Tensor& x, const Tensor& sorted_ids, int64_t topk,
                          n_out, (int)max_rows, gated, gather, cur_stream());
 }
 
+// ---- custom all-reduce (csrc/comm/custom_ar.hip)
+int64_t car_alloc_op(int64_t data_bytes) {
+  void* p = nullptr;
+  TORCH_CHECK(rfq::car_alloc(data_bytes, &p) == hipSuccess, "car_alloc: hipExtMallocWithFlags failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_free_op(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>(ptr)); }
+
+Tensor car_ipc_handle(int64_t ptr) {
+  hipIpcMemHandle_t h;
+  TORCH_CHECK(hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr)) == hipSuccess,
+              "hipIpcGetMemHandle failed");
+  Tensor t = at::empty({(int64_t)sizeof(h)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &h, sizeof(h));
+  return t;
+}
+
+int64_t car_ipc_open(const Tensor& handle) {
+  TORCH_CHECK(handle.numel() == (int64_t)sizeof(hipIpcMemHandle_t) && !handle.is_cuda(),
+              "car_ipc_open: expects the 64-byte CPU handle");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data_ptr(), sizeof(h));
+  void* p = nullptr;
+  TORCH_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess,
+              "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void car_ipc_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)); }
+
+int64_t car_data_offset() { return rfq::car_signal_bytes(); }
+
+int64_t car_error(int64_t ptr) {
+  return (int64_t)rfq::car_read_error(reinterpret_cast<const void*>(ptr));
+}
+
+void car_allreduce(const Tensor& inp, const Tensor& out, c10::IntArrayRef bases, int64_t rank,
+                   int64_t capacity_bytes) {
+  CHECK_DEV(inp); CHECK_BF16(inp); CHECK_BF16(out);
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel(),
+              "car_allreduce: contiguous tensors of equal size required");
+  TORCH_CHECK(inp.numel() % 8 == 0, "car_allreduce: numel % 8 != 0");
+  TORCH_CHECK(inp.numel() * 2 <= capacity_bytes, "car_allreduce: message exceeds the buffer");
+  const int world = (int)bases.size();
+  TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "car_allreduce: world");
+  char* b[8];
+  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  rfq::launch_car_oneshot(b, (int)rank, world, bp(inp), bpm(out), inp.numel(), cur_stream());
+}
+
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
                const Tensor& inv_pos, const Tensor& expert_of_block,
                const Tensor& expert_offsets, const Tensor& num_blocks) {
@@ -324,6 +380,15 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes) -> ()");
+  // host-side setup of the custom all-reduce regions (no tensor dispatch)
+  m.def("car_alloc(int data_bytes) -> int", &car_alloc_op);
+  m.def("car_free(int ptr) -> ()", &car_free_op);
+  m.def("car_ipc_handle(int ptr) -> Tensor", &car_ipc_handle);
+  m.def("car_ipc_open(Tensor handle) -> int", &car_ipc_open);
+  m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
+  m.def("car_data_offset() -> int", &car_data_offset);
+  m.def("car_error(int ptr) -> int", &car_error);
   m.def("moe_skinny(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) out, bool gated, bool gather, int max_rows) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start) -> ()");
@@ -353,6 +418,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("car_allreduce", &car_allreduce);
   m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);
   m.impl("rope_kv", &rope_kv);

@@ -1,0 +1,141 @@
+// One-shot all-reduce over xGMI peer memory for tensor-parallel decode steps
+// (SURVEY.md §2.2 custom_allreduce, §2.5 C1/C2, §5.8).
+//
+// A decode step of Llama-3-70B at TP=8 issues 160 all-reduces of a few KB to
+// ~1 MB.  At that size the cost is latency, not bandwidth: every rank simply
+// reads the other ranks' copies over its 7 xGMI links at once and sums them —
+// one kernel, no ring, no second pass.
+//
+// Memory: each rank owns one uncached (hipDeviceMallocUncached) region,
+// exported with hipIpcGetMemHandle and opened by every peer:
+//
+//   [ Signal (flags + per-block counters) | data staging area ]
+//
+// Per call, workgroup b of every rank owns element slice b:
+//   1. copy its slice of the input into the rank's own staging area;
+//   2. release-store its block counter c into start[b][rank] of every peer;
+//   3. acquire-spin on its own start[b][p] == c for all p (slice b of every
+//      peer is now visible);
+//   4. sum slice b across all ranks' staging areas (fp32), write the output;
+//   5. release end[b][rank] = c to every peer and spin on end[b][p] == c, so no
+//      rank starts the next call (overwriting slice b) while a peer still reads.
+// The counter is per block and lives in device memory, so the kernel is
+// graph-capturable (replays keep counting).  Every spin is bounded: on timeout
+// the kernel records an error in its signal area and falls through instead of
+// hanging the GPU; the host checks it (car_check) and falls back to RCCL.
+#include <hip/hip_runtime.h>
+
+#include "../kernels/common.h"
+
+namespace rfq {
+
+constexpr int kCarMaxRanks = 8;
+constexpr int kCarMaxBlocks = 64;
+constexpr int kCarThreads = 512;
+
+struct CarSignal {
+  uint32_t start[kCarMaxBlocks][kCarMaxRanks];
+  uint32_t end[kCarMaxBlocks][kCarMaxRanks];
+  uint32_t counter[kCarMaxBlocks];
+  uint32_t error;
+  uint32_t pad[63];
+};
+
+constexpr int64_t kCarDataOffset = (sizeof(CarSignal) + 4095) / 4096 * 4096;
+
+struct CarPeers {
+  char* base[kCarMaxRanks];  // region base of every rank (own included)
+};
+
+__device__ __forceinline__ void car_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ bool car_wait(uint32_t* p, uint32_t v) {
+  for (int it = 0; it < (1 << 22); ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == v) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
+    CarPeers peers, int rank, int world, const bf16_t* __restrict__ in,
+    bf16_t* __restrict__ out, int64_t n8) {
+  CarSignal* self = reinterpret_cast<CarSignal*>(peers.base[rank]);
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int tid = threadIdx.x;
+  const int64_t per = (n8 + nb - 1) / nb;          // 16-byte chunks per block
+  const int64_t c0 = b * per, c1 = min(n8, c0 + per);
+  __shared__ uint32_t cnt_s;
+  __shared__ int fail_s;
+  if (tid == 0) {
+    cnt_s = self->counter[b] + 1;
+    fail_s = 0;
+  }
+  // 1. stage own slice
+  s16x8* own = reinterpret_cast<s16x8*>(peers.base[rank] + kCarDataOffset);
+  const s16x8* src = reinterpret_cast<const s16x8*>(in);
+  for (int64_t i = c0 + tid; i < c1; i += kCarThreads) own[i] = src[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: staged slice visible
+  __syncthreads();
+  const uint32_t c = cnt_s;
+  // 2-3. publish, then wait for every peer's slice b
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->start[b][rank], c);
+    if (!car_wait(&self->start[b][tid], c)) fail_s = 1;
+  }
+  __syncthreads();
+  // 4. reduce slice b
+  for (int64_t i = c0 + tid; i < c1; i += kCarThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < world; ++p) {
+      const s16x8 v = reinterpret_cast<const s16x8*>(peers.base[p] + kCarDataOffset)[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f_s(v[j]);
+    }
+    reinterpret_cast<s16x8*>(out)[i] = pack8(acc);
+  }
+  __syncthreads();
+  // 5. everyone is done reading slice b before anyone reuses it
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->end[b][rank], c);
+    if (!car_wait(&self->end[b][tid], c)) fail_s = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    self->counter[b] = c;
+    if (fail_s) atomicAdd(&self->error, 1u);
+  }
+}
+
+// ------------------------------------------------------------------ host side
+int64_t car_signal_bytes() { return kCarDataOffset; }
+
+hipError_t car_alloc(int64_t data_bytes, void** ptr) {
+  const int64_t bytes = kCarDataOffset + data_bytes;
+  hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return e;
+  return hipMemset(*ptr, 0, kCarDataOffset);
+}
+
+void launch_car_oneshot(char* const* bases, int rank, int world, const bf16_t* in, bf16_t* out,
+                        int64_t numel, hipStream_t s) {
+  CarPeers peers{};
+  for (int p = 0; p < world; ++p) peers.base[p] = bases[p];
+  const int64_t n8 = numel / 8;
+  int nb = (int)((n8 + kCarThreads * 2 - 1) / (kCarThreads * 2));
+  nb = nb < 1 ? 1 : (nb > kCarMaxBlocks ? kCarMaxBlocks : nb);
+  car_oneshot_kernel<<<nb, kCarThreads, 0, s>>>(peers, rank, world, in, out, n8);
+}
+
+uint32_t car_read_error(const void* base) {
+  uint32_t err = 0;
+  hipMemcpy(&err, reinterpret_cast<const char*>(base) + offsetof(CarSignal, error), 4,
+            hipMemcpyDeviceToHost);
+  return err;
+}
+
+}  // namespace rfq

@@ -62,6 +62,8 @@ class LLMEngine:
         self.device = resolve_device(self.cfg.device, tp)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        if tp.enabled and self.cfg.custom_allreduce and self.device.type == "cuda":
+            tp.enable_custom_allreduce()
         self.model_cfg = get_config(self.cfg.model)
         self.tokenizer = get_tokenizer(flavor_for_vocab(self.model_cfg.vocab_size))
         t0 = time.perf_counter()

@@ -1,0 +1,63 @@
+"""One-shot xGMI all-reduce (csrc/comm/custom_ar.hip) for small TP messages.
+
+Setup: every rank of the TP group allocates one uncached region (signal flags +
+staging buffer), exports it with hipIpcGetMemHandle, all-gathers the handles
+over the group's process group and opens its peers' regions (dmabuf IPC:
+``HSA_ENABLE_IPC_MODE_LEGACY=0``).  A call stages the local tensor, exchanges
+per-block flags with system-scope release/acquire and sums every rank's copy in
+one kernel — capturable in a hipGraph because the flag counters live in device
+memory.  Messages above the staging capacity go to RCCL.
+
+The kernel's spins are bounded; :meth:`CustomAllReduce.errors` reads the
+timeout counter so a broken peer path is detected instead of hanging the GPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _native
+
+
+class CustomAllReduce:
+    def __init__(self, rank: int, world: int, group=None, capacity_bytes: int = 8 << 20):
+        if world > 8:
+            raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
+        ops = _native.ops()
+        self.rank, self.world, self.group = rank, world, group
+        self.capacity = capacity_bytes
+        self.ptr = ops.car_alloc(capacity_bytes)
+        handle = ops.car_ipc_handle(self.ptr).numpy().tobytes()
+        handles = [None] * world
+        dist.all_gather_object(handles, handle, group=group)
+        self.bases, self._opened = [], []
+        for r in range(world):
+            if r == rank:
+                self.bases.append(self.ptr)
+            else:
+                p = ops.car_ipc_open(torch.frombuffer(bytearray(handles[r]), dtype=torch.uint8))
+                self.bases.append(p)
+                self._opened.append(p)
+        dist.barrier(group=group)
+        self.calls = 0
+
+    def eligible(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()
+                and t.numel() % 8 == 0 and t.numel() * 2 <= self.capacity)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        torch.ops.rfq_amd.car_allreduce(t, t, self.bases, self.rank, self.capacity)
+        self.calls += 1
+        return t
+
+    def errors(self) -> int:
+        return int(_native.ops().car_error(self.ptr))
+
+    def close(self) -> None:
+        ops = _native.ops()
+        for p in self._opened:
+            ops.car_ipc_close(p)
+        self._opened = []
+        if self.ptr:
+            ops.car_free(self.ptr)
+            self.ptr = 0

@@ -25,6 +25,7 @@ class TPContext:
     rank: int = 0
     world: int = 1
     group: object = None
+    car: object = None            # CustomAllReduce for small messages (RFQ_CUSTOM_AR=1)
 
     @property
     def enabled(self) -> bool:
@@ -39,8 +40,19 @@ class TPContext:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
+            if self.car is not None and self.car.eligible(t):
+                return self.car.all_reduce_(t)
             dist.all_reduce(t, group=self.group)
         return t
+
+    def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
+        """Switch small all-reduces to the xGMI one-shot kernel (GPU groups only)."""
+        if self.world <= 1 or not torch.cuda.is_available() or self.car is not None:
+            return self.car is not None
+        from .custom_ar import CustomAllReduce
+
+        self.car = CustomAllReduce(self.rank, self.world, self.group, capacity_bytes)
+        return True
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """out: [world, *inp.shape]"""
