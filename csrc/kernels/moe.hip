@@ -11,6 +11,8 @@
 //   --moe_combine--> out[T, d] = sum_j w[t,j] * y[inv_pos[t*k+j]]
 // Every buffer is sized by the host from upper bounds and the GEMM reads the
 // live block count from device memory, so the whole chain is graph-capturable.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rfq {
@@ -210,6 +212,126 @@ __global__ __launch_bounds__(256) void moe_grouped_gemm_kernel(
       }
 }
 
+// Same tile and MFMA schedule, staged by LDS-DMA: every operand chunk goes
+// global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no ds_write
+// pass), two LDS stages so tile k+1 streams in while tile k is multiplied, and
+// raw s_barrier + counted vmcnt so the in-flight stage survives the barrier
+// (a __syncthreads() would drain it).  The LDS image is written lane-linearly,
+// so the XOR swizzle is applied to the *source* address: the lane that fills
+// slot (row, c') fetches global chunk c' ^ ((row >> 1) & 7) — the involution the
+// ds_read side already uses.  All LDS lives in one __shared__ array.
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// 16-byte global -> LDS DMA (lane-linear destination: wave-uniform base + lane*16)
+__device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
+#endif
+}
+
+// BN = 128: 4 waves as 2x2 quadrants of 64x64 (4 MFMAs per 4 ds_read_b128).
+// BN = 256: 4 waves as 2x2 of 64x128 (8 MFMAs per 6 reads) — LDS read traffic per
+// MFMA drops by a third, which is what limits the 128-wide tile.
+template <int BN>
+__global__ __launch_bounds__(256) void moe_grouped_gemm_glds_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+    const int32_t* __restrict__ expert_of_block, const int32_t* __restrict__ num_blocks, int N,
+    int K) {
+  constexpr int NJ = BN / 64;                       // 32-col MFMA tiles per wave
+  constexpr int BI = BN / 32;                       // B glds instructions per thread per stage
+  constexpr int STAGE = (kBM + BN) * kBK;           // elements per stage
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int ntn = N / BN;
+  const int rb = blockIdx.x / ntn, cn = blockIdx.x % ntn;
+  if (rb >= *num_blocks) return;
+  const int e = expert_of_block[rb];
+  if (e < 0) return;
+  const bf16_t* xa = x + (int64_t)rb * kBM * K;
+  const bf16_t* wb = w + ((int64_t)e * N + (int64_t)cn * BN) * K;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h2 = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // lane's source offset / wave-uniform LDS destination per glds instruction
+  int src_off[BI];
+  int dst_base[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int idx0 = wid * 64 + 256 * i;
+    const int idx = idx0 + lane, row = idx >> 3, chp = idx & 7;
+    src_off[i] = row * K + (chp ^ ((row >> 1) & 7)) * 8;
+    dst_base[i] = idx0 * 8;
+  }
+  auto issue = [&](int stage, int k0) {
+    bf16_t* sa = smem + stage * STAGE;
+    bf16_t* sb = sa + kBM * kBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(xa + src_off[i] + k0, sa + dst_base[i]);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      glds16(wb + src_off[i] + k0, sb + dst_base[i]);
+  };
+
+  f32x16 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = K / kBK;
+  issue(0, 0);
+  if (nk > 1) issue(1, kBK);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nk) {
+      if constexpr (BN == 256) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* a_lds = smem + st * STAGE;
+    const bf16_t* b_lds = a_lds + kBM * kBK;
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      s16x8 af[2], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + r;
+        af[i] = reinterpret_cast<const s16x8*>(a_lds + row * kBK)[swz64(row, 2 * ks + h2)];
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + r;
+        bfr[j] = reinterpret_cast<const s16x8*>(b_lds + row * kBK)[swz64(row, 2 * ks + h2)];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(af[i]), as_bf16x8(bfr[j]),
+                                                              acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                 // stage st fully consumed by every wave
+    if (kt + 2 < nk) issue(st, (kt + 2) * kBK);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = rb * kBM + wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h2;
+        const int col = cn * BN + wn * (BN / 2) + j * 32 + r;
+        out[(int64_t)row * N + col] = f2bf(acc[i][j][q]);
+      }
+}
+
+
 // ------------------------------------------------------------------ combine
 __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ y,
                                                           const int32_t* __restrict__ inv_pos,
@@ -265,8 +387,19 @@ void launch_moe_grouped_gemm(const bf16_t* x, const bf16_t* w, bf16_t* out,
                              int max_blocks, int N, int K, int E, hipStream_t s) {
   if (max_blocks == 0) return;
   (void)E;
-  moe_grouped_gemm_kernel<<<max_blocks * (N / kBN), 256, 0, s>>>(x, w, out, expert_of_block,
-                                                                  num_blocks, N, K);
+  static const int impl = [] {
+    const char* v = getenv("RFQ_MOE_GEMM");
+    return v ? atoi(v) : 1;
+  }();
+  if (impl == 2 && N % 256 == 0)
+    moe_grouped_gemm_glds_kernel<256><<<max_blocks * (N / 256), 256, 0, s>>>(
+        x, w, out, expert_of_block, num_blocks, N, K);
+  else if (impl >= 1)
+    moe_grouped_gemm_glds_kernel<128><<<max_blocks * (N / kBN), 256, 0, s>>>(
+        x, w, out, expert_of_block, num_blocks, N, K);
+  else
+    moe_grouped_gemm_kernel<<<max_blocks * (N / kBN), 256, 0, s>>>(x, w, out, expert_of_block,
+                                                                    num_blocks, N, K);
 }
 
 void launch_moe_combine(const bf16_t* y, const int32_t* inv_pos, const float* w, int T, int k,
