@@ -34,7 +34,7 @@ from ..utils.trace import trace_range
 from .grammar import get_grammar
 from .. import runtime
 from .kv_cache import KVCache
-from .runner import EXT_MAX, TOKEN_MULTS, ModelRunner
+from .runner import EXT_MAX, MAX_GRAPH_TOKENS, TOKEN_MULTS, ModelRunner
 from .sequence import SamplingParams, Sequence, Status
 from .tokenizer import flavor_for_vocab, get_tokenizer
 
@@ -84,8 +84,18 @@ class LLMEngine:
             self._tune_gemms()
         if capture and self.device.type == "cuda" and self.cfg.use_graphs:
             buckets = [b for b in self.cfg.graph_buckets if b <= self.cfg.max_num_seqs]
+            limit = MAX_GRAPH_TOKENS
+            if self.model_cfg.is_moe:
+                # MoE: graphs only where the per-expert skinny kernels run; larger
+                # steps go eager so they can use one hipBLASLt GEMM per expert
+                import os
+
+                from ..models.moe import SKINNY_MAX_TOKENS
+
+                limit = int(os.environ.get("RFQ_MOE_GRAPH_TOKENS", SKINNY_MAX_TOKENS))
+                buckets = [b for b in buckets if b <= limit]
             if buckets:
-                self.capture_s = self.runner.capture_graphs(buckets)
+                self.capture_s = self.runner.capture_graphs(buckets, limit)
                 self.core.set_graph_keys(sorted(self.runner.graphs))
         self.num_steps = 0
         self.step_times: list[float] = []

@@ -242,13 +242,13 @@ class ModelRunner:
         return out
 
     # ----------------------------------------------------------------- graphs
-    def capture_graphs(self, buckets) -> float:
+    def capture_graphs(self, buckets, max_tokens: int = MAX_GRAPH_TOKENS) -> float:
         """Capture forward+sample graphs for (NB, TB) buckets, largest first."""
         if not self.is_cuda or not self.cfg.use_graphs:
             return 0.0
         t0 = time.perf_counter()
         keys = [(nb, nb * m) for nb in sorted(buckets) for m in TOKEN_MULTS
-                if nb * m <= max(MAX_GRAPH_TOKENS, nb)]
+                if nb * m <= max(max_tokens, nb if max_tokens >= MAX_GRAPH_TOKENS else 0)]
         maxb = self.max_blocks
         pool = torch.cuda.graph_pool_handle()
         for nb, tb in sorted(keys, key=lambda k: (-k[1], -k[0])):

@@ -94,6 +94,8 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         assert act.shape[1] == F
         ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
         return out
+    if not torch.cuda.is_current_stream_capturing():
+        return _moe_per_expert(x, w13, w2, topk, bufs, logits, out)
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
     nb = cap // BLOCK_M
     ops.moe_topk(logits, topk, True, w, ids)
@@ -105,5 +107,36 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks)
     ops.silu_mul(h13, act)
     ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks)
+    ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
+    return out
+
+
+def _moe_per_expert(x, w13, w2, topk, bufs, logits, out):
+    """Large eager steps: expert segments padded to 16 rows, one hipBLASLt GEMM per
+    routed expert.  Reading the 9 segment offsets costs one host sync per layer,
+    which only eager (non-graph) steps can afford; it buys ~1.0 PF/s GEMMs instead
+    of the grouped kernel's ~0.65 (tools/bench_moe.py) and 1/8 of its row padding."""
+    T = x.shape[0]
+    E = w13.shape[0]
+    n = T * topk
+    w, ids = bufs.weights[:T], bufs.ids[:T]
+    ops.moe_topk(logits, topk, True, w, ids)
+    cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
+    sorted_ids = bufs.sorted_ids[:cap]
+    ops.moe_align(ids, E, BLOCK_S, sorted_ids, bufs.inv_pos[:n],
+                  bufs.expert_of_block[:cap // BLOCK_S], bufs.expert_offsets, bufs.num_blocks)
+    xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
+    ops.moe_gather(x, sorted_ids, topk, xs)
+    off = bufs.expert_offsets[:E + 1].tolist()
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        if b > a:
+            torch.matmul(xs[a:b], w13[e].t(), out=h13[a:b])
+    total = off[E]
+    ops.silu_mul(h13[:total], act[:total])
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        if b > a:
+            torch.matmul(act[a:b], w2[e].t(), out=y[a:b])
     ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
     return out
