@@ -1,4 +1,6 @@
 // pybind11 bindings of the host runtime: replisense_rfq_amd._runtime
+#include <cstring>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -6,6 +8,7 @@
 #include "block_manager.h"
 #include "engine_core.h"
 #include "grammar.h"
+#include "shm_ring.h"
 
 namespace py = pybind11;
 using namespace rfqrt;
@@ -228,4 +231,28 @@ PYBIND11_MODULE(_runtime, m) {
       .def_property_readonly("prefix_hits", [](EngineCore& e) { return e.bm().hits; })
       .def_property_readonly("prefix_queries", [](EngineCore& e) { return e.bm().queries; })
       .def_property_readonly("evictions", [](EngineCore& e) { return e.bm().evictions; });
+
+  py::class_<ShmRing>(m, "ShmRing")
+      .def(py::init<const std::string&, int64_t, int, bool, int>(), py::arg("name"),
+           py::arg("capacity"), py::arg("n_readers"), py::arg("create"), py::arg("reader_id") = -1)
+      .def("publish", [](ShmRing& r, py::array_t<int32_t, py::array::c_style> msg, double timeout) {
+        const void* p = msg.data();
+        const int64_t n = (int64_t)msg.size() * 4;
+        py::gil_scoped_release nogil;
+        return r.publish(p, n, timeout);
+      })
+      .def("receive", [](ShmRing& r, double timeout) -> py::object {
+        std::vector<uint8_t> buf;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = r.receive(buf, timeout);
+        }
+        if (!ok) return py::none();
+        py::array_t<int32_t> out((py::ssize_t)(buf.size() / 4));
+        std::memcpy(out.mutable_data(), buf.data(), buf.size());
+        return out;
+      })
+      .def_property_readonly("capacity", &ShmRing::capacity)
+      .def_property_readonly("name", &ShmRing::name);
 }

@@ -78,6 +78,9 @@ class ModelRunner:
         self._stage = None                   # its numpy view
         self._header = np.zeros(HEADER, np.int32)
         self.decode_tiles = int(getattr(cfg, "decode_tiles", 1))
+        self.ring = None
+        if tp.enabled:
+            self._setup_control_plane()
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
                       "pack_s": 0.0}
 
@@ -163,7 +166,42 @@ class ModelRunner:
             self._broadcast(header, payload)
         return self._run(header, payload)
 
+    def _setup_control_plane(self, capacity: int = 64 << 20) -> None:
+        """TP step metadata over a host shared-memory channel (csrc/runtime/shm_ring.cpp)
+        when every rank of the group is on this node; RCCL broadcast otherwise
+        (``RFQ_TP_CONTROL=rccl``)."""
+        import os
+        import socket
+        import uuid
+
+        from .. import runtime
+
+        mode = os.environ.get("RFQ_TP_CONTROL", "shm")
+        host = socket.gethostname()
+        same = all(h == host for h in self._gather_hosts(host))
+        if mode != "shm" or not same:
+            return
+        rt = runtime.load()
+        if self.tp.rank == 0:
+            name = f"rfq_tp_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            self.ring = rt.ShmRing(name, capacity, self.tp.world - 1, True, -1)
+            self.tp.broadcast_obj(name)
+        else:
+            name = self.tp.broadcast_obj(None)
+            self.ring = rt.ShmRing(name, capacity, self.tp.world - 1, False, self.tp.rank - 1)
+        self.tp.barrier()
+
+    def _gather_hosts(self, host: str) -> list:
+        out = [None] * self.tp.world
+        torch.distributed.all_gather_object(out, host, group=self.tp.group)
+        return out
+
     def _broadcast(self, header, payload):
+        if self.ring is not None:
+            msg = np.concatenate([header.astype(np.int32), payload.astype(np.int32, copy=False)])
+            if not self.ring.publish(msg, 120.0):
+                raise RuntimeError("TP control plane: a worker stopped acknowledging steps")
+            return
         dev = self.device if self.is_cuda else "cpu"
         h = torch.from_numpy(header.copy()).to(dev)
         torch.distributed.broadcast(h, src=0, group=self.tp.group)
@@ -173,6 +211,15 @@ class ModelRunner:
 
     def worker_step(self) -> bool:
         """TP ranks > 0: receive one step from rank 0 and run it.  False = stop."""
+        if self.ring is not None:
+            msg = None
+            while msg is None:                   # idle server: keep waiting for rank 0
+                msg = self.ring.receive(1.0)
+            header = msg[:HEADER]
+            if header[H_STOP]:
+                return False
+            self._run(header, msg[HEADER:HEADER + int(header[H_PAYLOAD])])
+            return True
         dev = self.device if self.is_cuda else "cpu"
         h = torch.empty(HEADER, dtype=torch.int32, device=dev)
         torch.distributed.broadcast(h, src=0, group=self.tp.group)

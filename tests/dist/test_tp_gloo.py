@@ -58,9 +58,9 @@ def _forward_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _engine_worker(rank, world, port, q):
+def _engine_worker(rank, world, port, q, control="shm"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world))
+                      WORLD_SIZE=str(world), RFQ_TP_CONTROL=control)
     from replisense_rfq_amd.engine.engine import LLMEngine
     from replisense_rfq_amd.parallel.tp import init_distributed
     from replisense_rfq_amd.service.prompt import build_messages
@@ -69,6 +69,7 @@ def _engine_worker(rank, world, port, q):
 
     tp = init_distributed("gloo")
     eng = LLMEngine(EngineConfig(model="tiny-llama-tp", device="cpu", max_num_seqs=4), tp=tp)
+    assert (eng.runner.ring is not None) == (control == "shm")
     if tp.rank == 0:
         prompts = [eng.tokenizer.chat_ids(build_messages(synth.make_rfq(i).text)) for i in range(2)]
         seqs = eng.generate(prompts)
@@ -89,11 +90,15 @@ def test_tp2_forward_matches_tp1():
 
 
 @pytest.mark.timeout(600)
-def test_tp2_engine_valid_json():
+@pytest.mark.parametrize("control", ["shm", "rccl"])
+def test_tp2_engine_valid_json(control):
+    """TP=2 engine; step metadata over the shared-memory control plane or the
+    collective broadcast."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    mp.start_processes(_engine_worker, args=(2, port, q), nprocs=2, start_method="spawn")
+    mp.start_processes(_engine_worker, args=(2, port, q, control), nprocs=2,
+                       start_method="spawn")
     from replisense_rfq_amd.service.schema import RFQResponse
 
     for text in q.get(timeout=10):
