@@ -18,7 +18,9 @@ def server_config(host: str = "0.0.0.0", port: int | None = None) -> dict:
     reload = (os.getenv("ENVIRONMENT", "development") == "development"
               and os.getenv("RFQ_BACKEND", "") == "mock")
     return {"host": host, "port": port or int(os.getenv("PORT", "8000")), "reload": reload,
-            "log_level": os.getenv("LOG_LEVEL", "info").lower(), "access_log": True}
+            "log_level": os.getenv("LOG_LEVEL", "info").lower(), "access_log": True,
+            "timeout_keep_alive": int(os.getenv("RFQ_KEEP_ALIVE_S", "75")),
+            "backlog": 4096}
 
 
 def main(argv=None) -> None:

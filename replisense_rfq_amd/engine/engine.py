@@ -267,6 +267,12 @@ class AsyncEngine:
     """
 
     def __init__(self, engine: LLMEngine):
+        import os
+        import sys
+
+        # The HTTP event loop and this engine thread share the GIL; a short switch
+        # interval keeps the engine from waiting up to 5 ms for it between GPU steps.
+        sys.setswitchinterval(float(os.environ.get("RFQ_GIL_SWITCH_MS", "0.5")) / 1e3)
         self.engine = engine
         self._inbox: queue.Queue = queue.Queue()
         self._stop = threading.Event()

@@ -220,7 +220,10 @@ class RouterBackend:
 
 
 def maybe_router(cfg):
-    """A DPRouter when RFQ_DP > 1 (replicas of cfg.tp devices each), else None."""
-    if cfg.dp <= 1:
+    """A DPRouter when RFQ_DP > 1 (replicas of cfg.tp devices each) or when the
+    single engine should live in its own process (RFQ_ENGINE_PROCESS=1: the API
+    process then only parses HTTP, tokenises and validates), else None."""
+    own_process = os.environ.get("RFQ_ENGINE_PROCESS", "0").lower() in ("1", "true", "on")
+    if cfg.dp <= 1 and not own_process:
         return None
-    return DPRouter(cfg, cfg.dp, max(1, cfg.tp))
+    return DPRouter(cfg, max(1, cfg.dp), max(1, cfg.tp))

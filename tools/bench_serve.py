@@ -62,6 +62,7 @@ async def _throughput(url: str, docs: list[str], clients: int) -> tuple[float, i
     for d in docs:
         queue.put_nowait(d)
     ok = bad = 0
+    retries = [0]
     limits = httpx.Limits(max_connections=clients, max_keepalive_connections=clients)
 
     async def worker(c):
@@ -71,8 +72,14 @@ async def _throughput(url: str, docs: list[str], clients: int) -> tuple[float, i
                 d = queue.get_nowait()
             except asyncio.QueueEmpty:
                 return
-            r = await c.post(url + "/parse-text/", json={"text": d})
-            data = r.json().get("data", {}) if r.status_code == 200 else {}
+            r = None
+            for _ in range(3):                       # transport hiccups are retried, not
+                try:                                 # counted as extraction failures
+                    r = await c.post(url + "/parse-text/", json={"text": d})
+                    break
+                except httpx.TransportError:
+                    retries[0] += 1
+            data = r.json().get("data", {}) if r is not None and r.status_code == 200 else {}
             if data.get("success") and "validation warnings" not in data.get("message", ""):
                 ok += 1
             else:
@@ -82,6 +89,7 @@ async def _throughput(url: str, docs: list[str], clients: int) -> tuple[float, i
         t0 = time.perf_counter()
         await asyncio.gather(*(worker(c) for _ in range(clients)))
         dt = time.perf_counter() - t0
+    _throughput.retries = retries[0]
     return dt, ok, bad
 
 
@@ -120,7 +128,7 @@ def main():
         print(json.dumps({
             "metric": "http_rfq_docs_per_sec", "value": round(a.requests / dt, 3),
             "unit": "docs/s", "model": a.model, "clients": a.clients, "requests": a.requests,
-            "valid": ok, "invalid": bad,
+            "valid": ok, "invalid": bad, "transport_retries": getattr(_throughput, "retries", 0),
             "p50_parse_text_http_s": round(statistics.median(lat), 4),
             "p90_parse_text_http_s": round(q[8], 4),
             "baseline_p50_s": 0.883, "server_startup_s": round(startup, 1),
