@@ -90,8 +90,10 @@ void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cf
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm: w must be contiguous [N, K]");
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  const bool gated = cfg & 16;          // x = [M, 2K] gate|up, B operand silu(gate)*up
+  const int M = x.size(0), K = gated ? x.size(1) / 2 : x.size(1), N = w.size(0);
   const int nt = (cfg & 1) ? 2 : 1;  // bits 2-3 select the load variant
+  TORCH_CHECK(!gated || x.size(1) == 2 * K, "skinny_gemm: gated x must be [M, 2K]");
   TORCH_CHECK(M >= 1 && M <= 64, "skinny_gemm: M must be in [1, 64]");
   TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N % (16 * nt) == 0,
               "skinny_gemm: K % 128 and N % tile required");

@@ -33,7 +33,28 @@ __device__ __forceinline__ s16x8 ldw(const bf16_t* p) {
 // CMAP: k-permutation.  false: lane-group g owns 32 contiguous k (4 x 16 B, one per
 // MFMA j); true: MFMA j reads k [j*32, j*32+32) and group g the 8-element slice g
 // of it, so the 4 groups of one row read 64 contiguous bytes per load instruction.
-template <int MT, int NT, int NW, int U, bool CMAP, bool NTL>
+// GX: X is a [M, 2K] gate|up activation and the B operand is silu(gate) * up,
+// computed while loading (rounded like silu_mul: bf16(silu(g)) * u -> bf16), so the
+// down projection consumes the SwiGLU input without the separate act.hip pass.
+template <bool GX>
+__device__ __forceinline__ s16x8 ldx8(const bf16_t* p, int K) {
+  if constexpr (!GX) {
+    return *reinterpret_cast<const s16x8*>(p);
+  } else {
+    const s16x8 g = *reinterpret_cast<const s16x8*>(p);
+    const s16x8 u = *reinterpret_cast<const s16x8*>(p + K);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float gf = bf2f_s(g[i]);
+      const float sg = bf2f(f2bf(gf / (1.f + __expf(-gf))));
+      o[i] = sg * bf2f_s(u[i]);
+    }
+    return pack8(o);
+  }
+}
+
+template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
     bf16_t* __restrict__ Y, int64_t ldy, int M) {
@@ -79,8 +100,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
       for (int t = 0; t < MT; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          x[u][t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + (ks + u) * 128 + j * JS)
-                             : zero;
+          x[u][t][j] = xv[t] ? ldx8<GX>(xp[t] + (ks + u) * 128 + j * JS, K) : zero;
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -103,7 +123,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     for (int t = 0; t < MT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        x[t][j] = xv[t] ? *reinterpret_cast<const s16x8*>(xp[t] + ks * 128 + j * JS) : zero;
+        x[t][j] = xv[t] ? ldx8<GX>(xp[t] + ks * 128 + j * JS, K) : zero;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -142,6 +162,11 @@ template <int MT, int NT, int NW, int U>
 static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
                        int64_t ldy, int M, int variant, hipStream_t s) {
   dim3 grid(N / (16 * NT));
+  if (variant >= 4) {   // gated X (silu(gate) * up), contiguous-k, plain loads
+    hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, true, false, true>), grid, dim3(NW * 64),
+                       0, s, X, ldx, W, K, Y, ldy, M);
+    return;
+  }
 #define SK_LAUNCH(cm, nt)                                                                   \
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, cm, nt>), grid, dim3(NW * 64), 0, s, \
                      X, ldx, W, K, Y, ldy, M)
@@ -155,11 +180,12 @@ static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int
 }
 
 // cfg bits: [1:0] tile (0: NT=1 NW=4, 1: NT=2 NW=4, 2: NT=1 NW=8, 3: NT=2 NW=8),
-// [3:2] variant (bit2 contiguous k-map, bit3 plain loads instead of non-temporal).
+// [3:2] variant (bit2 contiguous k-map, bit3 plain loads instead of non-temporal),
+// bit 4: gated X (x is [M, 2K] gate|up; B operand = silu(gate) * up).
 void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
                         int64_t ldy, int M, int cfg, hipStream_t s) {
   const int MT = (M + 15) / 16;
-  const int v = (cfg >> 2) & 3;
+  const int v = (cfg & 16) ? 4 : ((cfg >> 2) & 3);
 #define SK_CASE(mt, u1, u2)                                                              \
   case mt:                                                                               \
     switch (cfg & 3) {                                                                   \

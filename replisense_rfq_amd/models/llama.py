@@ -141,8 +141,7 @@ class DecoderLM:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs)
             else:
                 gu = ops.linear(x, lw["gate_up"])
-                a = ops.silu_mul(gu)
-                mo = ops.linear(a, lw["down"])
+                mo = ops.silu_linear(gu, lw["down"])
             self.tp.all_reduce_(mo)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
             ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)

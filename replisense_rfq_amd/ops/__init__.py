@@ -14,7 +14,7 @@ from . import reference as ref
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
-    "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan", "set_linear_plan",
+    "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan", "set_linear_plan", "silu_linear", "set_silu_plan",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -61,6 +61,33 @@ def linear_plan(M: int, N: int, K: int) -> int:
                     return c if (c < 0 or c & 1 == 0 or N % 32 == 0) else -1
                 break
     return _default_plan(M, N, K)
+
+
+_SILU_PLAN: dict[tuple[int, int, int], int] = {}
+
+
+def set_silu_plan(plan: dict) -> None:
+    _SILU_PLAN.clear()
+    _SILU_PLAN.update(plan)
+
+
+def silu_linear(gu, w, out=None):
+    """out = (silu(gate) * up) @ w^T for gu = [M, 2F] gate|up.  Small M: one skinny
+    kernel computes SwiGLU while loading its operand (gemm_skinny.hip, gated X) when
+    the start-up plan found it faster; otherwise act.hip silu_mul + linear."""
+    M, F2 = gu.shape
+    F, N = F2 // 2, w.shape[0]
+    if _gpu(gu) and _TUNED_MS and M <= SKINNY_MAX_M and gu.stride(1) == 1:
+        for m in _TUNED_MS:
+            if m >= M:
+                cfg = _SILU_PLAN.get((m, N, F), -1)
+                if cfg >= 0:
+                    if out is None:
+                        out = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
+                    _native.ops().skinny_gemm(gu, w, out, cfg)
+                    return out
+                break
+    return linear(silu_mul(gu), w, out=out)
 
 
 def linear(x, w, out=None, plan: int | None = None):

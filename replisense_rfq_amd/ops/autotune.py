@@ -13,7 +13,7 @@ import logging
 
 import torch
 
-from . import _native, set_linear_plan
+from . import _native, set_linear_plan, set_silu_plan, silu_mul
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -61,6 +61,34 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
     return plan, report
 
 
+def tune_silu_down(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: float = 0.97):
+    """down projection with its SwiGLU input: silu_mul + best plain GEMM vs the gated
+    skinny kernel (one pass)."""
+    from . import linear
+
+    ops = _native.ops()
+    N, F = ws[0].shape
+    plan, report = {}, []
+    if F % 128 or N % 16:
+        return plan, report
+    for M in ms:
+        if M > 64:
+            continue
+        gu = torch.randn(M, 2 * F, device=ws[0].device, dtype=ws[0].dtype)
+        out = torch.empty(M, N, device=gu.device, dtype=gu.dtype)
+        t_ref = _time(lambda w: linear(silu_mul(gu), w, out=out), ws, reps)
+        best, t_best = -1, t_ref * margin
+        for c in (16, 17, 18, 19):
+            if c & 1 and N % 32:
+                continue
+            t = _time(lambda w, c=c: ops.skinny_gemm(gu, w, out, c), ws, reps)
+            if t < t_best:
+                best, t_best = c, t
+        plan[(M, N, F)] = best
+        report.append(("silu+down", M, N, F, round(t_ref, 1), best, round(min(t_best, t_ref), 1)))
+    return plan, report
+
+
 def tune_model(model, ms: list[int], lm_ms: list[int]) -> list:
     """Tune every projection of a DecoderLM and install the plan."""
     w = model.w
@@ -73,6 +101,10 @@ def tune_model(model, ms: list[int], lm_ms: list[int]) -> list:
     msg["lm_head"] = lm_ms
     plan, report = tune_linear(groups, msg)
     set_linear_plan(plan, sorted(set(ms) | set(lm_ms)))
+    if "down" in groups:                       # after the plain plan: the reference path uses it
+        splan, sreport = tune_silu_down(groups["down"], ms)
+        set_silu_plan(splan)
+        report += sreport
     for r in report:
         log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
                  r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6])

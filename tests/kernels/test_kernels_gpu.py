@@ -234,3 +234,18 @@ def test_skinny_gemm_strided_rows(gpu):
     ops.linear(x, w, out=out)
     _close(out, x.float() @ w.float().t(), 1e-2, 1e-2, "linear strided")
     assert torch.all(obuf[:, 1024:] == 0)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33])
+@pytest.mark.parametrize("cfg", [16, 17, 18, 19])
+def test_skinny_gemm_gated_swiglu(gpu, M, cfg):
+    """Gated-X skinny GEMM == silu_mul (act.hip semantics) followed by the GEMM."""
+    torch.manual_seed(M + cfg)
+    F, N = 1024, 512
+    gu = torch.randn(M, 2 * F, device=gpu, dtype=BF)
+    w = (torch.randn(N, F, device=gpu) * 0.03).to(BF)
+    out = torch.empty(M, N, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm(gu, w, out, cfg)
+    act = torch.empty(M, F, dtype=BF)
+    ref.silu_mul(gu.cpu(), act)
+    _close(out, act.float() @ w.float().cpu().t(), 2e-2, 1e-2, f"gated skinny M={M} cfg={cfg}")
