@@ -130,14 +130,14 @@ __device__ __forceinline__ int swz64(int row, int ch) { return ch ^ ((row >> 1) 
 __global__ __launch_bounds__(256) void moe_grouped_gemm_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
     const int32_t* __restrict__ expert_of_block, const int32_t* __restrict__ num_blocks, int N,
-    int K) {
+    int K, int E) {
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[kBM * kBK];
   __shared__ __attribute__((aligned(16))) bf16_t b_lds[kBN * kBK];
   const int ntn = N / kBN;
   const int rb = blockIdx.x / ntn, cn = blockIdx.x % ntn;
   if (rb >= *num_blocks) return;
   const int e = expert_of_block[rb];
-  if (e < 0) return;
+  if (e < 0 || e >= E) return;      // padding block, or a remote expert's segment (EP)
   const bf16_t* xa = x + (int64_t)rb * kBM * K;
   const bf16_t* wb = w + ((int64_t)e * N + (int64_t)cn * kBN) * K;
 
@@ -236,7 +236,7 @@ template <int BN>
 __global__ __launch_bounds__(256) void moe_grouped_gemm_glds_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
     const int32_t* __restrict__ expert_of_block, const int32_t* __restrict__ num_blocks, int N,
-    int K) {
+    int K, int E) {
   constexpr int NJ = BN / 64;                       // 32-col MFMA tiles per wave
   constexpr int BI = BN / 32;                       // B glds instructions per thread per stage
   constexpr int STAGE = (kBM + BN) * kBK;           // elements per stage
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void moe_grouped_gemm_glds_kernel(
   const int rb = blockIdx.x / ntn, cn = blockIdx.x % ntn;
   if (rb >= *num_blocks) return;
   const int e = expert_of_block[rb];
-  if (e < 0) return;
+  if (e < 0 || e >= E) return;      // padding block, or a remote expert's segment (EP)
   const bf16_t* xa = x + (int64_t)rb * kBM * K;
   const bf16_t* wb = w + ((int64_t)e * N + (int64_t)cn * BN) * K;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -347,6 +347,7 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < k; ++j) {
       const float wj = wts[t * k + j];
+      if (wj == 0.f) continue;        // pair routed to another rank's expert (EP)
       const int p = inv_pos[t * k + j];
       float v[8];
       unpack8(reinterpret_cast<const s16x8*>(y + (int64_t)p * d)[c], v);
@@ -386,20 +387,19 @@ void launch_moe_grouped_gemm(const bf16_t* x, const bf16_t* w, bf16_t* out,
                              const int32_t* expert_of_block, const int32_t* num_blocks,
                              int max_blocks, int N, int K, int E, hipStream_t s) {
   if (max_blocks == 0) return;
-  (void)E;
   static const int impl = [] {
     const char* v = getenv("RFQ_MOE_GEMM");
     return v ? atoi(v) : 1;
   }();
   if (impl == 2 && N % 256 == 0)
     moe_grouped_gemm_glds_kernel<256><<<max_blocks * (N / 256), 256, 0, s>>>(
-        x, w, out, expert_of_block, num_blocks, N, K);
+        x, w, out, expert_of_block, num_blocks, N, K, E);
   else if (impl >= 1)
     moe_grouped_gemm_glds_kernel<128><<<max_blocks * (N / kBN), 256, 0, s>>>(
-        x, w, out, expert_of_block, num_blocks, N, K);
+        x, w, out, expert_of_block, num_blocks, N, K, E);
   else
     moe_grouped_gemm_kernel<<<max_blocks * (N / kBN), 256, 0, s>>>(x, w, out, expert_of_block,
-                                                                    num_blocks, N, K);
+                                                                    num_blocks, N, K, E);
 }
 
 void launch_moe_combine(const bf16_t* y, const int32_t* inv_pos, const float* w, int T, int k,

@@ -67,7 +67,8 @@ class LLMEngine:
         self.model_cfg = get_config(self.cfg.model)
         self.tokenizer = get_tokenizer(flavor_for_vocab(self.model_cfg.vocab_size))
         t0 = time.perf_counter()
-        self.model = model or DecoderLM(self.model_cfg, self.device, tp, seed=self.cfg.seed)
+        self.model = model or DecoderLM(self.model_cfg, self.device, tp, seed=self.cfg.seed,
+                                        moe_ep=self.cfg.moe_parallel == "ep")
         self.init_weights_s = time.perf_counter() - t0
         self.kv = KVCache(self.model_cfg, self.model.hkv, self._num_blocks(), self.device,
                           prefix_cache=self.cfg.prefix_cache)

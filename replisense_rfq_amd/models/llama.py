@@ -66,15 +66,19 @@ class ForwardMeta:
 
 class DecoderLM:
     def __init__(self, cfg: ModelConfig, device, tp: TPContext = SINGLE, seed: int = 0,
-                 weights: dict | None = None, dtype=torch.bfloat16):
+                 weights: dict | None = None, dtype=torch.bfloat16, moe_ep: bool = False):
         self.cfg = cfg
         self.tp = tp
         self.device = torch.device(device)
         self.dtype = dtype
         self.hq = cfg.n_heads // tp.world
         self.hkv = cfg.n_kv_heads // tp.world
-        self.ffn_local = cfg.ffn // tp.world
-        self.w = weights if weights is not None else init_weights(cfg, tp, self.device, dtype, seed)
+        # MoE expert parallelism over the TP group: whole experts per rank
+        self.moe_ep = bool(moe_ep and cfg.is_moe and tp.world > 1)
+        self.ffn_local = cfg.ffn if self.moe_ep else cfg.ffn // tp.world
+        self.expert_offset = tp.rank * (cfg.n_experts // tp.world) if self.moe_ep else 0
+        self.w = weights if weights is not None else init_weights(cfg, tp, self.device, dtype, seed,
+                                                                  moe_ep=self.moe_ep)
         self.vocab_start = self.w["vocab_start"]
         self.vocab_local = self.w["lm_head"].shape[0]
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
@@ -138,7 +142,8 @@ class DecoderLM:
             self.tp.all_reduce_(o)
             ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
             if cfg.is_moe:
-                mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs)
+                mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
+                             expert_offset=self.expert_offset)
             else:
                 gu = ops.linear(x, lw["gate_up"])
                 mo = ops.silu_linear(gu, lw["down"])

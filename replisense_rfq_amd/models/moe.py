@@ -64,23 +64,34 @@ class MoEBuffers:
 
 
 def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
-            topk: int, bufs: MoEBuffers | None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """x [T, d] -> [T, d].  w13 [E, 2F, d] (gate|up), w2 [E, d, F], router_w [E, d]."""
+            topk: int, bufs: MoEBuffers | None, out: torch.Tensor | None = None,
+            expert_offset: int = 0) -> torch.Tensor:
+    """x [T, d] -> [T, d].  w13 [E, 2F, d] (gate|up), w2 [E, d, F], router_w [E_all, d].
+
+    Expert parallelism: when this rank holds experts [expert_offset, expert_offset +
+    E) of E_all, pairs routed elsewhere are sent to a dummy expert segment that no
+    kernel computes and get combine weight 0; the TP all-reduce after the MLP sums
+    the ranks' partial outputs (each expert runs on exactly one rank)."""
     T = x.shape[0]
     logits = x @ router_w.t()
     if not x.is_cuda:
-        return ref.moe_forward(x, w13, w2, logits, topk)
+        return ref.moe_forward(x, w13, w2, logits, topk, expert_offset)
     E = w13.shape[0]
+    ep = E != router_w.shape[0]
     assert bufs is not None and T <= bufs.max_tokens
     out = torch.empty_like(x) if out is None else out
     # buffers are sliced to this step's token count but keep their capacity-based
     # padding so the grouped GEMM grid is fixed for a given bucket
     n = T * topk
     w, ids = bufs.weights[:T], bufs.ids[:T]
+    if ep:
+        E = E + 1                  # + the dummy segment for remote experts
     if T <= SKINNY_MAX_TOKENS:
         # decode / short-extend steps: stream only the routed experts' weights,
         # gather rows on the fly, SwiGLU fused into the w13 pass
         ops.moe_topk(logits, topk, True, w, ids)
+        if ep:
+            _localize(ids, w, expert_offset, E - 1)
         cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
         sorted_ids = bufs.sorted_ids[:cap]
         ops.moe_align(ids, E, BLOCK_S, sorted_ids, bufs.inv_pos[:n],
@@ -95,10 +106,12 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
         return out
     if not torch.cuda.is_current_stream_capturing():
-        return _moe_per_expert(x, w13, w2, topk, bufs, logits, out)
+        return _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset, E)
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
     nb = cap // BLOCK_M
     ops.moe_topk(logits, topk, True, w, ids)
+    if ep:
+        _localize(ids, w, expert_offset, E - 1)
     sorted_ids, eob = bufs.sorted_ids[:cap], bufs.expert_of_block[:nb]
     ops.moe_align(ids, E, BLOCK_M, sorted_ids, bufs.inv_pos[:n], eob, bufs.expert_offsets,
                   bufs.num_blocks)
@@ -111,16 +124,27 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     return out
 
 
-def _moe_per_expert(x, w13, w2, topk, bufs, logits, out):
+def _localize(ids: torch.Tensor, w: torch.Tensor, e0: int, e_local: int) -> None:
+    """Global expert ids -> this rank's local ids; remote pairs -> dummy id e_local
+    with weight 0 (graph-capturable tensor ops)."""
+    loc = ids - e0
+    mine = (loc >= 0) & (loc < e_local)
+    ids.copy_(torch.where(mine, loc, torch.full_like(loc, e_local)))
+    w.mul_(mine.to(w.dtype))
+
+
+def _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset=0, E_align=None):
     """Large eager steps: expert segments padded to 16 rows, one hipBLASLt GEMM per
     routed expert.  Reading the 9 segment offsets costs one host sync per layer,
     which only eager (non-graph) steps can afford; it buys ~1.0 PF/s GEMMs instead
     of the grouped kernel's ~0.65 (tools/bench_moe.py) and 1/8 of its row padding."""
     T = x.shape[0]
-    E = w13.shape[0]
+    E = E_align or w13.shape[0]
     n = T * topk
     w, ids = bufs.weights[:T], bufs.ids[:T]
     ops.moe_topk(logits, topk, True, w, ids)
+    if E != w13.shape[0]:
+        _localize(ids, w, expert_offset, w13.shape[0])
     cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
     sorted_ids = bufs.sorted_ids[:cap]
     ops.moe_align(ids, E, BLOCK_S, sorted_ids, bufs.inv_pos[:n],
@@ -128,13 +152,13 @@ def _moe_per_expert(x, w13, w2, topk, bufs, logits, out):
     xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
     ops.moe_gather(x, sorted_ids, topk, xs)
     off = bufs.expert_offsets[:E + 1].tolist()
-    for e in range(E):
+    for e in range(w13.shape[0]):
         a, b = off[e], off[e + 1]
         if b > a:
             torch.matmul(xs[a:b], w13[e].t(), out=h13[a:b])
-    total = off[E]
+    total = off[w13.shape[0]]
     ops.silu_mul(h13[:total], act[:total])
-    for e in range(E):
+    for e in range(w13.shape[0]):
         a, b = off[e], off[e + 1]
         if b > a:
             torch.matmul(act[a:b], w2[e].t(), out=y[a:b])

@@ -43,11 +43,16 @@ class LayerWeights(dict):
     __getattr__ = dict.__getitem__
 
 
-def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, seed: int = 0):
+def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, seed: int = 0,
+                 moe_ep: bool = False):
+    """moe_ep: experts are split across the TP group (each rank holds E/TP whole
+    experts) instead of every expert's FFN being column/row split."""
     d, D = cfg.hidden, cfg.head_dim
     R = tp.world
     if cfg.n_heads % R or cfg.n_kv_heads % R or cfg.ffn % R or cfg.vocab_size % R:
         raise ValueError(f"{cfg.name} is not divisible by TP={R}")
+    if moe_ep and cfg.n_experts % R:
+        raise ValueError(f"{cfg.n_experts} experts are not divisible by EP={R}")
     hq, hkv, F = cfg.n_heads // R, cfg.n_kv_heads // R, cfg.ffn // R
     std = cfg.init_std
     r = tp.rank
@@ -63,8 +68,13 @@ def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, 
         if cfg.is_moe:
             E = cfg.n_experts
             lw["router"] = _randn((E, d), std, (seed, li, "router"), device, dtype)
-            lw["w13"] = _randn((E, 2 * F, d), std, (seed, li, "w13", r), device, dtype)
-            lw["w2"] = _randn((E, d, F), std, (seed, li, "w2", r), device, dtype)
+            if moe_ep:
+                El, Ff = E // R, cfg.ffn
+                lw["w13"] = _randn((El, 2 * Ff, d), std, (seed, li, "w13e", r), device, dtype)
+                lw["w2"] = _randn((El, d, Ff), std, (seed, li, "w2e", r), device, dtype)
+            else:
+                lw["w13"] = _randn((E, 2 * F, d), std, (seed, li, "w13", r), device, dtype)
+                lw["w2"] = _randn((E, d, F), std, (seed, li, "w2", r), device, dtype)
         else:
             lw["gate_up"] = _randn((2 * F, d), std, (seed, li, "gate_up", r), device, dtype)
             lw["down"] = _randn((d, F), std, (seed, li, "down", r), device, dtype)
@@ -139,9 +149,10 @@ def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=t
     )
 
 
-def shard_weights(full: dict, cfg: ModelConfig, tp: TPContext) -> dict:
+def shard_weights(full: dict, cfg: ModelConfig, tp: TPContext, moe_ep: bool = False) -> dict:
     """Slice full (TP=1) weights into this rank's Megatron shard (same layout as
-    init_weights), e.g. to check TP numerics against the single-device model."""
+    init_weights), e.g. to check TP numerics against the single-device model.
+    moe_ep: whole experts per rank instead of FFN-split experts."""
     D, R, r = cfg.head_dim, tp.world, tp.rank
     hq, hkv, F = cfg.n_heads // R, cfg.n_kv_heads // R, cfg.ffn // R
     Hq, Hkv = cfg.n_heads, cfg.n_kv_heads
@@ -153,7 +164,12 @@ def shard_weights(full: dict, cfg: ModelConfig, tp: TPContext) -> dict:
         out = LayerWeights(attn_norm=lw["attn_norm"], mlp_norm=lw["mlp_norm"],
                            qkv=torch.cat([q, k, v]).contiguous(),
                            o=lw["o"][:, r * hq * D:(r + 1) * hq * D].contiguous())
-        if cfg.is_moe:
+        if cfg.is_moe and moe_ep:
+            El = cfg.n_experts // R
+            out["router"] = lw["router"]
+            out["w13"] = lw["w13"][r * El:(r + 1) * El].contiguous()
+            out["w2"] = lw["w2"][r * El:(r + 1) * El].contiguous()
+        elif cfg.is_moe:
             Ff = cfg.ffn
             out["router"] = lw["router"]
             out["w13"] = torch.cat([lw["w13"][:, r * F:(r + 1) * F],

@@ -161,13 +161,15 @@ def moe_topk(router_logits, topk: int, renorm: bool):
     return w, ids.int()
 
 
-def moe_forward(x, w13, w2, router_logits, topk: int):
-    """Mixtral sparse MLP oracle: x [T,d], w13 [E, 2F, d], w2 [E, d, F]."""
+def moe_forward(x, w13, w2, router_logits, topk: int, expert_offset: int = 0):
+    """Mixtral sparse MLP oracle: x [T,d], w13 [E, 2F, d], w2 [E, d, F].  With expert
+    parallelism w13/w2 hold experts [expert_offset, expert_offset + E) only and the
+    result is this rank's partial sum."""
     w, ids = moe_topk(router_logits, topk, True)
     out = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
     F = w2.shape[2]
     for e in range(w13.shape[0]):
-        tok, slot = torch.nonzero(ids == e, as_tuple=True)
+        tok, slot = torch.nonzero(ids == e + expert_offset, as_tuple=True)
         if tok.numel() == 0:
             continue
         h = x[tok].float() @ w13[e].float().t()

@@ -43,6 +43,7 @@ class EngineConfig:
     max_tokens: int = 1200               # rfq_agent.py:67
     request_timeout_s: float = 30.0      # rfq_agent.py:69
     step_timeout_s: float = 120.0        # watchdog
+    moe_parallel: str = "tp"             # tp: FFN-split experts | ep: whole experts per rank
     decode_tiles: int = 2                # column tiles per decode attention work item
     tune_gemm: bool = True               # per-shape skinny-vs-hipBLASLt plan at start-up
     custom_allreduce: bool = False
@@ -66,6 +67,7 @@ class EngineConfig:
             custom_allreduce=_env("RFQ_CUSTOM_AR", cls.custom_allreduce, bool),
             tune_gemm=_env("RFQ_TUNE_GEMM", cls.tune_gemm, bool),
             decode_tiles=_env("RFQ_DECODE_TILES", cls.decode_tiles, int),
+            moe_parallel=_env("RFQ_MOE_PARALLEL", cls.moe_parallel),
             trace=_env("RFQ_TRACE", cls.trace, bool),
         )
         gb = os.environ.get("RFQ_GRAPH_BUCKETS")

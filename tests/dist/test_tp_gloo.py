@@ -80,6 +80,59 @@ def _engine_worker(rank, world, port, q, control="shm"):
     dist.destroy_process_group()
 
 
+def _moe_forward_worker(rank, world, port, q, ep):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from replisense_rfq_amd.models.config import get_config
+    from replisense_rfq_amd.models.llama import DecoderLM, ForwardMeta
+    from replisense_rfq_amd.models.weights import init_weights, shard_weights
+    from replisense_rfq_amd.parallel.tp import SINGLE, TPContext
+
+    base = get_config("tiny-mixtral")
+    cfg = base.__class__(**{**base.to_dict(), "n_heads": 8, "n_kv_heads": 2, "name": "tiny-mx-tp"})
+    full = init_weights(cfg, SINGLE, "cpu", seed=5)
+    tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
+    m = DecoderLM(cfg, "cpu", tp=tp, weights=shard_weights(full, cfg, tp, moe_ep=ep), moe_ep=ep)
+    T, nb = 24, 2
+    shape = (cfg.n_layers, nb, m.hkv, 32, 128)
+    m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16),
+                      torch.zeros(shape, dtype=torch.bfloat16))
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(0, 5000, (T,), generator=g, dtype=torch.int32)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32)  # noqa: E731
+    meta = ForwardMeta(input_ids=ids, positions=torch.arange(T, dtype=torch.int32),
+                       slot_mapping=torch.arange(T, dtype=torch.int32), num_decode=0,
+                       num_prefill_tokens=T, pf_block_tables=i32([[0]]), pf_q_start=i32([0]),
+                       pf_q_len=i32([T]), pf_kv_len=i32([T]), work_seq=i32([0]),
+                       work_qblk=i32([0]), logits_idx=torch.tensor([T - 1]))
+    part = m.forward(meta).float()
+    parts = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(parts, part)
+    if rank == 0:
+        ref = DecoderLM(cfg, "cpu", weights=full)
+        shape1 = (cfg.n_layers, nb, ref.hkv, 32, 128)
+        ref.attach_kv_cache(torch.zeros(shape1, dtype=torch.bfloat16),
+                            torch.zeros(shape1, dtype=torch.bfloat16))
+        exp = ref.forward(meta).float()
+        got = torch.cat(parts, -1)
+        q.put(float((got - exp).norm() / exp.norm()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("ep", [False, True])
+def test_tp2_mixtral_forward_matches_tp1(ep):
+    """Mixtral MoE under TP=2: FFN-split experts (ep=False) or whole experts per
+    rank (expert parallelism, ep=True) both reproduce the single-device logits."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    mp.start_processes(_moe_forward_worker, args=(2, port, q, ep), nprocs=2,
+                       start_method="spawn")
+    assert q.get(timeout=10) < 0.02
+
+
 @pytest.mark.timeout(600)
 def test_tp2_forward_matches_tp1():
     ctx = mp.get_context("spawn")

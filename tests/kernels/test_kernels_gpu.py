@@ -249,3 +249,28 @@ def test_skinny_gemm_gated_swiglu(gpu, M, cfg):
     act = torch.empty(M, F, dtype=BF)
     ref.silu_mul(gu.cpu(), act)
     _close(out, act.float() @ w.float().cpu().t(), 2e-2, 1e-2, f"gated skinny M={M} cfg={cfg}")
+
+
+@pytest.mark.parametrize("T", [3, 40, 100, 200])
+@pytest.mark.parametrize("grouped", [False, True])
+def test_moe_expert_parallel_partial(gpu, T, grouped, monkeypatch):
+    """Expert parallelism: a rank holding experts [2, 6) of 8 computes exactly the
+    partial sum of its experts (remote pairs -> dummy segment, weight 0) on every
+    path: skinny (T <= 64), per-expert hipBLASLt (eager) and the grouped kernel
+    (the graph-capture path, forced here)."""
+    from replisense_rfq_amd.models import moe as M
+
+    if grouped:
+        monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    torch.manual_seed(40 + T)
+    d, F, E, k, e0, el = 512, 384, 8, 2, 2, 4
+    x = (torch.randn(T, d, device=gpu) * 0.5).to(BF)
+    router = (torch.randn(E, d, device=gpu) * 0.05).to(BF)
+    w13 = (torch.randn(E, 2 * F, d, device=gpu) / math.sqrt(d)).to(BF)
+    w2 = (torch.randn(E, d, F, device=gpu) / math.sqrt(F)).to(BF)
+    bufs = M.MoEBuffers.allocate(T, k, E, d, F, gpu)
+    out = M.moe_mlp(x, router, w13[e0:e0 + el].contiguous(), w2[e0:e0 + el].contiguous(), k, bufs,
+                    expert_offset=e0)
+    logits = (x @ router.t()).cpu()
+    exp = ref.moe_forward(x.cpu(), w13[e0:e0 + el].cpu(), w2[e0:e0 + el].cpu(), logits, k, e0)
+    _close(out, exp, 3e-2, 2e-2, f"moe EP T={T} grouped={grouped}")
