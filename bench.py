@@ -110,6 +110,7 @@ class Replica:
 
     def latency(self, runs: int) -> list[float]:
         out = []
+        self.lat_detail = []
         eng = self.engine
         for i in range(runs):
             d = synth.make_rfq(10_000_000 + self.dp_rank * 1000 + i)
@@ -118,8 +119,28 @@ class Replica:
             s, = eng.generate([ids], eng.default_params(min_items=estimate_line_items(d.text)))
             parse_and_validate_response(eng.decode_text(s), "direct_text_input")
             out.append(time.perf_counter() - t0)
+            sp = s.span()
+            self.lat_detail.append((s.num_generated, s.num_sampled, sp.get("ttft_ms") or 0.0,
+                                    out[-1]))
         eng.runner.tp.enabled and eng.shutdown()      # release the TP workers' loop
         return out
+
+
+def _single_stream(detail):
+    """Single-request decode rates (Groq 350 tok/s per stream): output
+    tokens/s after the first token, and the sampled (non-jump-forward) step rate."""
+    if not detail:
+        return None
+    rates, steps, ttft = [], [], []
+    for gen, sampled, ttft_ms, total in detail:
+        dec = max(total - ttft_ms / 1e3, 1e-6)
+        rates.append(gen / dec)
+        steps.append(sampled / dec)
+        ttft.append(ttft_ms)
+    return {"completion_tok_s_p50": round(statistics.median(rates), 1),
+            "sampled_steps_per_s_p50": round(statistics.median(steps), 1),
+            "ttft_ms_p50": round(statistics.median(ttft), 1),
+            "baseline_decode_tok_s": 350.0}
 
 
 def sync():
@@ -209,6 +230,7 @@ def main():
                        "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
                        "mode": args.mode, "max_num_seqs": args.max_num_seqs},
             "p50_parse_text_latency_s": round(p50, 4) if p50 is not None else None,
+            "single_stream": _single_stream(getattr(rep, "lat_detail", [])),
             "latency_vs_baseline_p50": round(BASELINE_P50_S / p50, 2) if p50 else None,
             "baseline": "vs_baseline = docs/s / (1 / 0.883 s), the reference's single-stream "
                         "Groq llama3-70b p50 server time (BASELINE.md)",
