@@ -12,4 +12,6 @@ timeout -k 10 ${PROF_TIMEOUT:-900} rocprofv3 --kernel-trace --stats --output-for
 rc=$?
 tail -2 "$OUT/bench.log"
 python3 tools/prof_summary.py "$OUT" || true
+# the raw per-dispatch trace can exceed gpurun's 64 MiB copy-back limit
+[ "${KEEP_TRACE:-0}" = "1" ] || find "$OUT" -name '*kernel_trace.csv' -delete
 exit $rc
