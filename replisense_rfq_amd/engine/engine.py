@@ -65,15 +65,23 @@ class LLMEngine:
         if tp.enabled and self.cfg.custom_allreduce and self.device.type == "cuda":
             tp.enable_custom_allreduce()
         self.model_cfg = get_config(self.cfg.model)
-        self.tokenizer = get_tokenizer(flavor_for_vocab(self.model_cfg.vocab_size))
+        self.tokenizer = get_tokenizer(flavor_for_vocab(self.model_cfg.vocab_size),
+                                       self._tokenizer_path())
         t0 = time.perf_counter()
+        weights = None
+        if model is None and self.cfg.weights_path:
+            from ..models.weights import load_safetensors
+
+            weights = load_safetensors(self.cfg.weights_path, self.model_cfg, tp, self.device,
+                                       moe_ep=self.cfg.moe_parallel == "ep")
         self.model = model or DecoderLM(self.model_cfg, self.device, tp, seed=self.cfg.seed,
-                                        moe_ep=self.cfg.moe_parallel == "ep")
+                                        weights=weights, moe_ep=self.cfg.moe_parallel == "ep")
         self.init_weights_s = time.perf_counter() - t0
         self.kv = KVCache(self.model_cfg, self.model.hkv, self._num_blocks(), self.device,
                           prefix_cache=self.cfg.prefix_cache)
         self.model.attach_kv_cache(self.kv.k, self.kv.v)
-        self.grammar = get_grammar(self.tokenizer.flavor) if self.cfg.grammar else None
+        self.grammar = get_grammar(self.tokenizer.flavor, self.tokenizer) if self.cfg.grammar \
+            else None
         self.runner = ModelRunner(self.model, self.kv, self.cfg,
                                   self.grammar.mask_table() if self.grammar else None, tp)
         self.core = self._make_core()
@@ -104,6 +112,17 @@ class LLMEngine:
         self.faults = FaultInjector()
 
     # ------------------------------------------------------------------ setup
+    def _tokenizer_path(self) -> str | None:
+        import os
+
+        if self.cfg.tokenizer_path:
+            return self.cfg.tokenizer_path
+        if self.cfg.weights_path and os.path.isdir(self.cfg.weights_path):
+            cand = os.path.join(self.cfg.weights_path, "tokenizer.json")
+            if os.path.exists(cand):
+                return cand
+        return None
+
     def _make_core(self):
         """Native scheduler / packer / post-processor (csrc/runtime/engine_core.cpp)."""
         c = self.cfg

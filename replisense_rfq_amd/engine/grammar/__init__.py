@@ -124,7 +124,7 @@ class RFQGrammar:
 
 
 @functools.lru_cache(maxsize=4)
-def get_grammar(flavor: str = "llama3") -> RFQGrammar:
+def get_grammar(flavor: str = "llama3", tokenizer=None) -> RFQGrammar:
     from ..tokenizer import get_tokenizer
 
-    return RFQGrammar(get_tokenizer(flavor))
+    return RFQGrammar(tokenizer if tokenizer is not None else get_tokenizer(flavor))

@@ -34,10 +34,14 @@ _U2B = {u: b for b, u in _bytes_to_unicode().items()}
 
 
 class Tokenizer:
-    def __init__(self, flavor: str = "llama3"):
-        path = _DIR / f"{flavor}_synth.json.gz"
-        with gzip.open(path, "rb") as f:
-            self._tok = _HFTok.from_str(f.read().decode())
+    def __init__(self, flavor: str = "llama3", path: str | None = None):
+        """path: a real checkpoint's ``tokenizer.json`` (HF tokenizers format);
+        default: the shipped synthetic vocabulary of the flavor."""
+        if path:
+            self._tok = _HFTok.from_file(str(path))
+        else:
+            with gzip.open(_DIR / f"{flavor}_synth.json.gz", "rb") as f:
+                self._tok = _HFTok.from_str(f.read().decode())
         self.flavor = flavor
         self.vocab_size = self._tok.get_vocab_size()
         if flavor == "llama3":
@@ -108,8 +112,8 @@ class Tokenizer:
 
 
 @functools.lru_cache(maxsize=4)
-def get_tokenizer(flavor: str = "llama3") -> Tokenizer:
-    return Tokenizer(flavor)
+def get_tokenizer(flavor: str = "llama3", path: str | None = None) -> Tokenizer:
+    return Tokenizer(flavor, path)
 
 
 def flavor_for_vocab(vocab_size: int) -> str:

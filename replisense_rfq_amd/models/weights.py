@@ -89,8 +89,10 @@ def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, 
     )
 
 
-def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16):
-    """Load HF-style Llama/Mixtral safetensors shards into this rank's layout."""
+def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16,
+                     moe_ep: bool = False):
+    """Load HF-style Llama/Mixtral safetensors shards into this rank's layout
+    (Megatron TP split, or whole experts per rank with moe_ep)."""
     import glob
     import os
 
@@ -124,7 +126,16 @@ def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=t
             qkv=torch.cat([q, k, v]),
             o=rows(tensors[p + "self_attn.o_proj.weight"], cfg.n_heads * D),
         )
-        if cfg.is_moe:
+        if cfg.is_moe and moe_ep and tp.world > 1:
+            ex = p + "block_sparse_moe."
+            El = cfg.n_experts // tp.world
+            mine = range(tp.rank * El, (tp.rank + 1) * El)
+            lw["router"] = tensors[ex + "gate.weight"]
+            lw["w13"] = torch.stack([torch.cat([tensors[f"{ex}experts.{e}.w1.weight"],
+                                                tensors[f"{ex}experts.{e}.w3.weight"]])
+                                     for e in mine])
+            lw["w2"] = torch.stack([tensors[f"{ex}experts.{e}.w2.weight"] for e in mine])
+        elif cfg.is_moe:
             ex = p + "block_sparse_moe."
             lw["router"] = tensors[ex + "gate.weight"]
             lw["w13"] = torch.stack([torch.cat([cols(tensors[f"{ex}experts.{e}.w1.weight"], F),
@@ -184,3 +195,31 @@ def shard_weights(full: dict, cfg: ModelConfig, tp: TPContext, moe_ep: bool = Fa
     v0, v1 = tp.shard(cfg.vocab_size)
     return dict(embed=full["embed"], final_norm=full["final_norm"],
                 lm_head=full["lm_head"][v0:v1].contiguous(), layers=layers, vocab_start=v0)
+
+
+def export_hf(full: dict, cfg: ModelConfig) -> dict[str, torch.Tensor]:
+    """Inverse of load_safetensors for TP=1 weights: HF tensor names -> tensors
+    (used to write test checkpoints and to round-trip the loader)."""
+    D, F, Hq, Hkv = cfg.head_dim, cfg.ffn, cfg.n_heads, cfg.n_kv_heads
+    out = {"model.embed_tokens.weight": full["embed"], "model.norm.weight": full["final_norm"],
+           "lm_head.weight": full["lm_head"]}
+    for li, lw in enumerate(full["layers"]):
+        p = f"model.layers.{li}."
+        out[p + "input_layernorm.weight"] = lw["attn_norm"]
+        out[p + "post_attention_layernorm.weight"] = lw["mlp_norm"]
+        out[p + "self_attn.q_proj.weight"] = lw["qkv"][: Hq * D]
+        out[p + "self_attn.k_proj.weight"] = lw["qkv"][Hq * D:(Hq + Hkv) * D]
+        out[p + "self_attn.v_proj.weight"] = lw["qkv"][(Hq + Hkv) * D:]
+        out[p + "self_attn.o_proj.weight"] = lw["o"]
+        if cfg.is_moe:
+            ex = p + "block_sparse_moe."
+            out[ex + "gate.weight"] = lw["router"]
+            for e in range(cfg.n_experts):
+                out[f"{ex}experts.{e}.w1.weight"] = lw["w13"][e, :F]
+                out[f"{ex}experts.{e}.w3.weight"] = lw["w13"][e, F:]
+                out[f"{ex}experts.{e}.w2.weight"] = lw["w2"][e]
+        else:
+            out[p + "mlp.gate_proj.weight"] = lw["gate_up"][:F]
+            out[p + "mlp.up_proj.weight"] = lw["gate_up"][F:]
+            out[p + "mlp.down_proj.weight"] = lw["down"]
+    return {k: v.contiguous() for k, v in out.items()}

@@ -23,6 +23,8 @@ def _env(name, default, cast=str):
 @dataclass
 class EngineConfig:
     model: str = "llama3-8b"
+    weights_path: str = ""               # HF-layout safetensors dir/file; "" = seeded random init
+    tokenizer_path: str = ""             # tokenizer.json; default: <weights_path>/tokenizer.json
     tp: int = 1
     dp: int = 1
     device: str = "auto"                 # auto -> cuda if available else cpu
@@ -53,6 +55,8 @@ class EngineConfig:
     def from_env(cls, **overrides) -> "EngineConfig":
         c = cls(
             model=_env("RFQ_MODEL", cls.model),
+            weights_path=_env("RFQ_WEIGHTS", cls.weights_path),
+            tokenizer_path=_env("RFQ_TOKENIZER", cls.tokenizer_path),
             tp=_env("RFQ_TP", cls.tp, int),
             dp=_env("RFQ_DP", cls.dp, int),
             device=_env("RFQ_DEVICE", cls.device),
