@@ -89,72 +89,94 @@ def init_weights(cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16, 
     )
 
 
+class _LazyCheckpoint:
+    """Tensor name -> file index over a set of safetensors files; reads only the
+    requested slice of each tensor (memory-mapped), so a TP rank of a 141 GB
+    Llama-3-70B checkpoint touches ~1/8 of it and never holds the whole file."""
+
+    def __init__(self, files):
+        from safetensors import safe_open
+
+        self._handles = [safe_open(f, framework="pt", device="cpu") for f in files]
+        self._where = {}
+        for h in self._handles:
+            for k in h.keys():
+                self._where[k] = h
+
+    def __contains__(self, name):
+        return name in self._where
+
+    def full(self, name):
+        return self._where[name].get_tensor(name)
+
+    def rows(self, name, a, b):          # W[a:b]
+        return self._where[name].get_slice(name)[a:b]
+
+    def cols(self, name, a, b):          # W[:, a:b]
+        return self._where[name].get_slice(name)[:, a:b]
+
+
 def load_safetensors(path: str, cfg: ModelConfig, tp: TPContext, device, dtype=torch.bfloat16,
                      moe_ep: bool = False):
     """Load HF-style Llama/Mixtral safetensors shards into this rank's layout
-    (Megatron TP split, or whole experts per rank with moe_ep)."""
+    (Megatron TP split, or whole experts per rank with moe_ep), reading only this
+    rank's slices; each layer is moved to the device as it is assembled."""
     import glob
     import os
 
-    from safetensors import safe_open
-
     files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
-    tensors = {}
-    for f in files:
-        with safe_open(f, framework="pt", device="cpu") as fh:
-            for k in fh.keys():
-                tensors[k] = fh.get_tensor(k)
+    ck = _LazyCheckpoint(files)
 
-    def cols(t, n):           # column-parallel rows of W
+    def cols(name, n):        # column-parallel: this rank's rows of W
         a, b = tp.shard(n)
-        return t[a:b]
+        return ck.rows(name, a, b)
 
-    def rows(t, n):           # row-parallel columns of W
+    def rows(name, n):        # row-parallel: this rank's columns of W
         a, b = tp.shard(n)
-        return t[:, a:b]
+        return ck.cols(name, a, b)
 
     D, F = cfg.head_dim, cfg.ffn
     layers = []
     for li in range(cfg.n_layers):
         p = f"model.layers.{li}."
-        q = cols(tensors[p + "self_attn.q_proj.weight"], cfg.n_heads * D)
-        k = cols(tensors[p + "self_attn.k_proj.weight"], cfg.n_kv_heads * D)
-        v = cols(tensors[p + "self_attn.v_proj.weight"], cfg.n_kv_heads * D)
+        q = cols(p + "self_attn.q_proj.weight", cfg.n_heads * D)
+        k = cols(p + "self_attn.k_proj.weight", cfg.n_kv_heads * D)
+        v = cols(p + "self_attn.v_proj.weight", cfg.n_kv_heads * D)
         lw = LayerWeights(
-            attn_norm=tensors[p + "input_layernorm.weight"],
-            mlp_norm=tensors[p + "post_attention_layernorm.weight"],
+            attn_norm=ck.full(p + "input_layernorm.weight"),
+            mlp_norm=ck.full(p + "post_attention_layernorm.weight"),
             qkv=torch.cat([q, k, v]),
-            o=rows(tensors[p + "self_attn.o_proj.weight"], cfg.n_heads * D),
+            o=rows(p + "self_attn.o_proj.weight", cfg.n_heads * D),
         )
         if cfg.is_moe and moe_ep and tp.world > 1:
             ex = p + "block_sparse_moe."
             El = cfg.n_experts // tp.world
             mine = range(tp.rank * El, (tp.rank + 1) * El)
-            lw["router"] = tensors[ex + "gate.weight"]
-            lw["w13"] = torch.stack([torch.cat([tensors[f"{ex}experts.{e}.w1.weight"],
-                                                tensors[f"{ex}experts.{e}.w3.weight"]])
+            lw["router"] = ck.full(ex + "gate.weight")
+            lw["w13"] = torch.stack([torch.cat([ck.full(f"{ex}experts.{e}.w1.weight"),
+                                                ck.full(f"{ex}experts.{e}.w3.weight")])
                                      for e in mine])
-            lw["w2"] = torch.stack([tensors[f"{ex}experts.{e}.w2.weight"] for e in mine])
+            lw["w2"] = torch.stack([ck.full(f"{ex}experts.{e}.w2.weight") for e in mine])
         elif cfg.is_moe:
             ex = p + "block_sparse_moe."
-            lw["router"] = tensors[ex + "gate.weight"]
-            lw["w13"] = torch.stack([torch.cat([cols(tensors[f"{ex}experts.{e}.w1.weight"], F),
-                                                cols(tensors[f"{ex}experts.{e}.w3.weight"], F)])
+            lw["router"] = ck.full(ex + "gate.weight")
+            lw["w13"] = torch.stack([torch.cat([cols(f"{ex}experts.{e}.w1.weight", F),
+                                                cols(f"{ex}experts.{e}.w3.weight", F)])
                                      for e in range(cfg.n_experts)])
-            lw["w2"] = torch.stack([rows(tensors[f"{ex}experts.{e}.w2.weight"], F)
+            lw["w2"] = torch.stack([rows(f"{ex}experts.{e}.w2.weight", F)
                                     for e in range(cfg.n_experts)])
         else:
-            lw["gate_up"] = torch.cat([cols(tensors[p + "mlp.gate_proj.weight"], F),
-                                       cols(tensors[p + "mlp.up_proj.weight"], F)])
-            lw["down"] = rows(tensors[p + "mlp.down_proj.weight"], F)
+            lw["gate_up"] = torch.cat([cols(p + "mlp.gate_proj.weight", F),
+                                       cols(p + "mlp.up_proj.weight", F)])
+            lw["down"] = rows(p + "mlp.down_proj.weight", F)
         layers.append(LayerWeights({k: t.to(device=device, dtype=dtype).contiguous()
                                     for k, t in lw.items()}))
     v0, v1 = tp.shard(cfg.vocab_size)
-    head = tensors.get("lm_head.weight", tensors["model.embed_tokens.weight"])
+    head_name = "lm_head.weight" if "lm_head.weight" in ck else "model.embed_tokens.weight"
     return dict(
-        embed=tensors["model.embed_tokens.weight"].to(device=device, dtype=dtype),
-        final_norm=tensors["model.norm.weight"].to(device=device, dtype=dtype),
-        lm_head=head[v0:v1].to(device=device, dtype=dtype).contiguous(),
+        embed=ck.full("model.embed_tokens.weight").to(device=device, dtype=dtype),
+        final_norm=ck.full("model.norm.weight").to(device=device, dtype=dtype),
+        lm_head=ck.rows(head_name, v0, v1).to(device=device, dtype=dtype).contiguous(),
         layers=layers,
         vocab_start=v0,
     )
