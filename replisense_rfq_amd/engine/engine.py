@@ -18,13 +18,16 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import queue
+import sys
 import threading
 import time
 
 import numpy as np
 import torch
 
+from .. import runtime
 from ..models.config import get_config
 from ..models.llama import DecoderLM
 from ..parallel.tp import SINGLE, TPContext
@@ -32,7 +35,6 @@ from ..utils.config import EngineConfig
 from ..utils.faults import FaultInjector
 from ..utils.trace import trace_range
 from .grammar import get_grammar
-from .. import runtime
 from .kv_cache import KVCache
 from .runner import EXT_MAX, MAX_GRAPH_TOKENS, TOKEN_MULTS, ModelRunner
 from .sequence import SamplingParams, Sequence, Status
@@ -46,8 +48,6 @@ FINISH_REASONS = {1: "stop", 2: "length", 3: "grammar_error", 4: "abort", 5: "en
 def resolve_device(spec: str, tp: TPContext) -> torch.device:
     if spec == "auto":
         if torch.cuda.is_available():
-            import os
-
             local = int(os.environ.get("LOCAL_RANK", tp.rank))
             return torch.device("cuda", local % max(1, torch.cuda.device_count()))
         return torch.device("cpu")
@@ -97,8 +97,6 @@ class LLMEngine:
             if self.model_cfg.is_moe:
                 # MoE: graphs only where the per-expert skinny kernels run; larger
                 # steps go eager so they can use one hipBLASLt GEMM per expert
-                import os
-
                 from ..models.moe import SKINNY_MAX_TOKENS
 
                 limit = int(os.environ.get("RFQ_MOE_GRAPH_TOKENS", SKINNY_MAX_TOKENS))
@@ -113,8 +111,6 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ setup
     def _tokenizer_path(self) -> str | None:
-        import os
-
         if self.cfg.tokenizer_path:
             return self.cfg.tokenizer_path
         if self.cfg.weights_path and os.path.isdir(self.cfg.weights_path):
@@ -287,8 +283,6 @@ class AsyncEngine:
     """
 
     def __init__(self, engine: LLMEngine):
-        import os
-        import sys
 
         # The HTTP event loop and this engine thread share the GIL; a short switch
         # interval keeps the engine from waiting up to 5 ms for it between GPU steps.

@@ -6,6 +6,8 @@ if it cannot be.  CPU tensors use :mod:`.reference` (tests / CPU engine).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native
@@ -14,12 +16,13 @@ from . import reference as ref
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
-    "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan", "set_linear_plan", "silu_linear", "set_silu_plan",
+    "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
+    "set_linear_plan", "silu_linear", "set_silu_plan",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
 # (csrc/kernels/gemm_skinny.hip) instead of hipBLASLt; 0 disables it.
-SKINNY_MAX_M = int(__import__("os").environ.get("RFQ_SKINNY_MAX_M", "64"))
+SKINNY_MAX_M = int(os.environ.get("RFQ_SKINNY_MAX_M", "64"))
 
 
 def native_available() -> bool:
