@@ -77,6 +77,18 @@ std::vector<int32_t> EngineCore::abort_all(FinishReason why, double now) {
   return out;
 }
 
+bool EngineCore::abort(int32_t id, FinishReason why, double now) {
+  if (id < 0 || id >= (int32_t)seqs_.size() || !seqs_[id].live) return false;
+  if (seqs_[id].status == S_FINISHED) return false;
+  auto w = std::find(waiting_.begin(), waiting_.end(), id);
+  if (w != waiting_.end()) waiting_.erase(w);
+  auto r = std::find(running_.begin(), running_.end(), id);
+  if (r != running_.end()) running_.erase(r);
+  std::vector<int32_t> sink;
+  finish(id, why, now, sink);
+  return true;
+}
+
 // ---------------------------------------------------------------- KV blocks
 int32_t EngineCore::blocks_needed(const Seq& s, int32_t upto) const {
   const int32_t need = (upto + cfg_.block_size - 1) / cfg_.block_size;

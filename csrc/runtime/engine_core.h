@@ -32,7 +32,8 @@ namespace rfqrt {
 
 enum SeqStatus : int8_t { S_WAITING = 0, S_RUNNING = 1, S_FINISHED = 2 };
 enum FinishReason : int8_t {
-  F_NONE = 0, F_STOP = 1, F_LENGTH = 2, F_GRAMMAR_ERROR = 3, F_ABORT = 4, F_ENGINE_ERROR = 5
+  F_NONE = 0, F_STOP = 1, F_LENGTH = 2, F_GRAMMAR_ERROR = 3, F_ABORT = 4, F_ENGINE_ERROR = 5,
+  F_TIMEOUT = 6
 };
 
 struct SeqParams {
@@ -99,6 +100,9 @@ class EngineCore {
   int32_t add(const int32_t* prompt, int32_t n, const SeqParams& p, double t_arrival);
   void release(int32_t id);              // forget a finished sequence's record
   std::vector<int32_t> abort_all(FinishReason why, double now);
+  // Retire one queued/running sequence between steps (releases its blocks).
+  // Returns false if it already finished.
+  bool abort(int32_t id, FinishReason why, double now);
 
   // --- one step
   // Schedules the next step and packs it.  Returns the payload length (int32

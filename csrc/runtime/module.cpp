@@ -193,6 +193,9 @@ PYBIND11_MODULE(_runtime, m) {
         return e.abort_all((FinishReason)reason, now);
       })
       .def("drain_finished", &EngineCore::drain_finished)
+      .def("abort", [](EngineCore& e, int32_t id, int reason, double now) {
+        return e.abort(id, (FinishReason)reason, now);
+      })
       .def("release", &EngineCore::release)
       .def("set_graph_keys", &EngineCore::set_graph_keys)
       .def("payload_bound", &EngineCore::payload_bound)

@@ -42,7 +42,8 @@ from .tokenizer import flavor_for_vocab, get_tokenizer
 
 log = logging.getLogger("replisense_rfq_amd.engine")
 
-FINISH_REASONS = {1: "stop", 2: "length", 3: "grammar_error", 4: "abort", 5: "engine_error"}
+FINISH_REASONS = {1: "stop", 2: "length", 3: "grammar_error", 4: "abort", 5: "engine_error",
+                  6: "timeout"}
 
 
 def resolve_device(spec: str, tp: TPContext) -> torch.device:
@@ -225,6 +226,18 @@ class LLMEngine:
     def has_work(self) -> bool:
         return self.core.has_work
 
+    def abort_request(self, seq: Sequence, reason: str = "abort") -> bool:
+        """Retire one request between steps (deadline expired, client gone); its KV
+        blocks return to the pool immediately."""
+        code = {v: k for k, v in FINISH_REASONS.items()}.get(reason, 4)
+        cid = getattr(seq, "core_id", None)
+        if cid is None or cid not in self._live or self._live[cid] is not seq:
+            return False
+        if not self.core.abort(cid, code, time.perf_counter()):
+            return False
+        self._finalize(cid)
+        return True
+
     def abort_all(self, reason: str) -> list[Sequence]:
         """Finish every queued/running sequence (releasing its KV blocks)."""
         code = {v: k for k, v in FINISH_REASONS.items()}.get(reason, 4)
@@ -274,6 +287,14 @@ class LLMEngine:
         return st
 
 
+class _Request:
+    """Handle shared by the HTTP side and the engine thread (set once admitted)."""
+    __slots__ = ("seq",)
+
+    def __init__(self):
+        self.seq = None
+
+
 class AsyncEngine:
     """Thread-hosted engine loop with an asyncio front door.
 
@@ -320,8 +341,13 @@ class AsyncEngine:
         while not self._stop.is_set():
             try:
                 while True:
-                    prompt, params, cb = self._inbox.get_nowait()
-                    eng.add_request(prompt, params, cb)
+                    msg = self._inbox.get_nowait()
+                    if msg[0] == "add":
+                        _, prompt, params, cb, req = msg
+                        req.seq = eng.add_request(prompt, params, cb)
+                    else:                       # ("abort", req): deadline expired
+                        if msg[1].seq is not None:
+                            eng.abort_request(msg[1].seq, "timeout")
             except queue.Empty:
                 pass
             if eng.has_work():
@@ -346,11 +372,17 @@ class AsyncEngine:
         def done(seq):
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(seq))
 
-        self._inbox.put((prompt_ids, params, done))
+        req = _Request()
+        self._inbox.put(("add", prompt_ids, params, done, req))
         self._wake.set()
-        if timeout:
-            return await asyncio.wait_for(fut, timeout)
-        return await fut
+        if not timeout:
+            return await fut
+        try:
+            return await asyncio.wait_for(asyncio.shield(fut), timeout)
+        except asyncio.TimeoutError:
+            self._inbox.put(("abort", req))      # stop computing it; free its KV
+            self._wake.set()
+            raise
 
     def shutdown(self):
         self._stop.set()

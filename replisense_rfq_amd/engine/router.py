@@ -44,9 +44,15 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
                 msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
                 if msg is None:
                     return
+                if msg[0] == "abort":               # the client's deadline expired
+                    for sid, (r, s) in list(pending.items()):
+                        if r == msg[1]:
+                            eng.abort_request(s, "timeout")
+                            pending.pop(sid, None)
+                    continue
                 rid, prompt, p = msg
                 seq = eng.add_request(prompt, SamplingParams(**p))
-                pending[seq.req_id] = rid
+                pending[seq.req_id] = (rid, seq)
         except queue.Empty:
             pass
         if not eng.has_work():
@@ -57,7 +63,7 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
             log.exception("replica %d step failed", idx)
             finished = eng.abort_all("engine_error")
         for s in finished:
-            rid = pending.pop(s.req_id, None)
+            rid, _ = pending.pop(s.req_id, (None, None))
             if rid is not None:
                 outq.put(("done", rid, {"text": eng.decode_text(s), "finish": s.finish_reason,
                                         "span": s.span()}))
@@ -168,7 +174,17 @@ class DPRouter:
             self.where[rid] = r
             self.futures[rid] = (loop, fut, cost)
         self.inqs[r].put((rid, prompt, params))
-        return await (asyncio.wait_for(fut, timeout) if timeout else fut)
+        if not timeout:
+            return await fut
+        try:
+            return await asyncio.wait_for(asyncio.shield(fut), timeout)
+        except asyncio.TimeoutError:
+            with self._lock:
+                _, _, cost = self.futures.pop(rid, (None, None, 0))
+                if self.where.pop(rid, None) is not None:
+                    self.load[r] -= cost
+            self.inqs[r].put(("abort", rid))
+            raise
 
     def backend(self):
         return RouterBackend(self)

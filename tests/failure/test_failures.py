@@ -98,3 +98,26 @@ def test_router_replica_crash_is_restarted(monkeypatch):
         assert router.healthy
     finally:
         router.shutdown()
+
+
+def test_request_deadline_aborts_and_frees_kv():
+    """A request whose deadline expires is retired inside the engine (finish reason
+    'timeout', KV released) instead of running to completion in the background."""
+    eng = LLMEngine(_cfg())
+    free0 = eng.kv.stats()["free"]
+    eng.faults = FaultInjector("step_sleep:1:300,step_sleep:2:300,step_sleep:3:300")
+    aeng = AsyncEngine(eng)
+
+    async def run():
+        return await aeng.generate(_prompt(eng, 11), timeout=0.5)
+
+    with pytest.raises(asyncio.TimeoutError):
+        asyncio.run(run())
+    import time
+
+    t0 = time.time()
+    while eng.has_work() and time.time() - t0 < 30:
+        time.sleep(0.05)
+    assert not eng.has_work()
+    assert eng.kv.stats()["free"] == free0
+    aeng.shutdown()
