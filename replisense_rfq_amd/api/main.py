@@ -132,6 +132,17 @@ app.add_middleware(CORSMiddleware, allow_origins=os.getenv("ALLOWED_ORIGINS", "*
                    allow_credentials=True, allow_methods=["GET", "POST"], allow_headers=["*"])
 
 
+# Prometheus exposition (additive: GET /metrics/prometheus).  A private registry
+# keeps repeated app imports (tests) from colliding in the global one.
+from prometheus_client import CollectorRegistry, Counter, Histogram  # noqa: E402
+from prometheus_client import generate_latest, CONTENT_TYPE_LATEST  # noqa: E402
+
+PROM = CollectorRegistry()
+_REQS = Counter("rfq_http_requests_total", "HTTP requests", ["path", "status"], registry=PROM)
+_LAT = Histogram("rfq_http_request_seconds", "HTTP request latency", ["path"], registry=PROM,
+                 buckets=(0.05, 0.1, 0.2, 0.3, 0.5, 0.75, 1.0, 1.5, 2.5, 5, 10, 30))
+
+
 @app.middleware("http")
 async def log_requests(request: Request, call_next):
     start = time.time()
@@ -143,6 +154,9 @@ async def log_requests(request: Request, call_next):
         logger.info("%s %s - Status: %s - Duration: %.2fs", request.method, request.url.path,
                     response.status_code, dt)
         response.headers["X-Process-Time"] = str(dt)
+        path = request.url.path if request.url.path in _KNOWN_PATHS else "other"
+        _REQS.labels(path, str(response.status_code)).inc()
+        _LAT.labels(path).observe(dt)
         return response
     except Exception as e:
         logger.error("%s %s - Error: %s - Duration: %.2fs", request.method, request.url.path,
@@ -355,6 +369,28 @@ async def metrics():
     if router is not None:
         data["router"] = router.stats()
     return StandardResponse.success(data=data, message="Metrics")
+
+
+@app.get("/metrics/prometheus")
+async def metrics_prometheus():
+    """Prometheus text format: HTTP counters/latency + engine gauges."""
+    from fastapi.responses import Response
+
+    lines = [generate_latest(PROM).decode()]
+    eng = _engine_handles.get("engine")
+    stats = eng.stats() if eng is not None else {}
+    router = _engine_handles.get("router")
+    if router is not None:
+        stats.update({f"router_{k}": v for k, v in router.stats().items()})
+    for k, v in sorted(stats.items()):
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            name = "rfq_engine_" + "".join(c if c.isalnum() else "_" for c in k)
+            lines.append(f"# TYPE {name} gauge\n{name} {float(v)}\n")
+    return Response("".join(lines), media_type=CONTENT_TYPE_LATEST)
+
+
+_KNOWN_PATHS = {"/", "/health", "/upload/", "/parse-text/", "/supported-formats/", "/metrics",
+                "/metrics/prometheus"}
 
 
 # --------------------------------------------------------- exception handlers

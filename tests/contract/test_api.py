@@ -198,3 +198,11 @@ def test_process_time_header_and_http_exception_envelope():
     body = r.json()
     assert set(body) == {"success", "error", "details", "timestamp"}
     assert body["details"] == "POST /parse-text/"
+
+
+def test_prometheus_metrics():
+    client.get("/")
+    r = client.get("/metrics/prometheus")
+    assert r.status_code == 200 and r.headers["content-type"].startswith("text/plain")
+    assert 'rfq_http_requests_total{path="/",status="200"}' in r.text
+    assert "rfq_http_request_seconds_bucket" in r.text
