@@ -109,7 +109,8 @@ async def lifespan(app: FastAPI):
     global parser, field_generator
     logger.info("Starting RFQ Processing API...")
     try:
-        parser = FileParser(max_file_size_mb=MAX_FILE_SIZE_MB)
+        parser = FileParser(max_file_size_mb=MAX_FILE_SIZE_MB,
+                            processes=int(os.getenv("RFQ_PARSER_PROCS", "0")))
         field_generator = build_generator()
         logger.info("Services initialized successfully")
     except Exception as e:
@@ -117,6 +118,8 @@ async def lifespan(app: FastAPI):
         raise
     yield
     logger.info("Shutting down RFQ Processing API...")
+    if parser is not None:
+        parser.close()
     if "async_engine" in _engine_handles:
         _engine_handles["async_engine"].shutdown()
     if "router" in _engine_handles:

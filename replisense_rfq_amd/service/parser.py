@@ -42,12 +42,27 @@ class FileParsingError(Exception):
     """Domain error mapped to HTTP 422 by the API."""
 
 
+def _parse_in_process(kind: str, path: str, max_excel_rows: int) -> str:
+    """Process-pool entry: the document readers are pure Python, so parallel parses
+    need processes, not threads (the GIL serialises them)."""
+    p = FileParser.__new__(FileParser)
+    p.max_excel_rows = max_excel_rows
+    fn = {"pdf": p._parse_pdf_sync, "excel": p._parse_excel_sync, "docx": p._parse_docx_sync,
+          "csv": p._parse_csv_sync}[kind]
+    return fn(Path(path))
+
+
 class FileParser:
     def __init__(self, max_file_size_mb: int = 10, max_excel_rows: int = 1000,
-                 workers: int = 4):
+                 workers: int = 4, processes: int = 0):
+        """workers: the reference's 4-thread pool (file_parser.py:33).  processes > 0:
+        PDF/Excel/DOCX/CSV parsing runs in that many spawned processes instead, so
+        concurrent uploads parse in parallel next to the engine."""
         self.max_file_size = max_file_size_mb * 1024 * 1024
         self.max_excel_rows = max_excel_rows
         self.thread_pool = ThreadPoolExecutor(max_workers=workers)
+        self.processes = processes
+        self._proc_pool = None
         self.supported_extensions = set(SUPPORTED_EXTENSIONS)
         log.info("FileParser initialized with max_file_size=%sMB, max_excel_rows=%s",
                  max_file_size_mb, max_excel_rows)
@@ -66,13 +81,13 @@ class FileParser:
             if ext == ".txt":
                 text = await self._parse_txt_async(file_path)
             elif ext == ".pdf":
-                text = await self._in_pool(self._parse_pdf_sync, file_path)
+                text = await self._in_pool(self._parse_pdf_sync, file_path, "pdf")
             elif ext in (".xlsx", ".xls"):
-                text = await self._in_pool(self._parse_excel_sync, file_path)
+                text = await self._in_pool(self._parse_excel_sync, file_path, "excel")
             elif ext == ".docx":
-                text = await self._in_pool(self._parse_docx_sync, file_path)
+                text = await self._in_pool(self._parse_docx_sync, file_path, "docx")
             elif ext == ".csv":
-                text = await self._in_pool(self._parse_csv_sync, file_path)
+                text = await self._in_pool(self._parse_csv_sync, file_path, "csv")
             elif ext == ".json":
                 text = await self._parse_json_async(file_path)
             else:
@@ -94,8 +109,19 @@ class FileParser:
     def parse_file(self, file_path: str) -> dict[str, Any]:
         return asyncio.run(self.parse_file_async(file_path))
 
-    async def _in_pool(self, fn, *args):
-        return await asyncio.get_running_loop().run_in_executor(self.thread_pool, fn, *args)
+    async def _in_pool(self, fn, path, kind: str):
+        loop = asyncio.get_running_loop()
+        if self.processes > 0:
+            if self._proc_pool is None:
+                import multiprocessing as mp
+                from concurrent.futures import ProcessPoolExecutor
+
+                # spawn, never fork: the serving process may own a GPU context
+                self._proc_pool = ProcessPoolExecutor(self.processes,
+                                                      mp_context=mp.get_context("spawn"))
+            return await loop.run_in_executor(self._proc_pool, _parse_in_process, kind,
+                                              str(path), self.max_excel_rows)
+        return await loop.run_in_executor(self.thread_pool, fn, path)
 
     # -------------------------------------------------------------- validation
     async def _validate_file_async(self, file_path: Path) -> None:
@@ -216,9 +242,16 @@ class FileParser:
         except Exception as e:
             raise FileParsingError(f"Failed to extract PDF metadata: {str(e)}")
 
+    def close(self) -> None:
+        if self._proc_pool is not None:
+            self._proc_pool.shutdown(wait=False, cancel_futures=True)
+            self._proc_pool = None
+
     def __del__(self):
         if hasattr(self, "thread_pool"):
             self.thread_pool.shutdown(wait=False)
+        if getattr(self, "_proc_pool", None) is not None:
+            self._proc_pool.shutdown(wait=False)
 
 
 async def parse_file_async(file_path: str, max_file_size_mb: int = 10) -> dict[str, Any]:

@@ -287,7 +287,12 @@ def rfq_attachment(doc, fmt: str, path=None) -> bytes:
     if fmt == "docx":
         return write_docx(doc.text.splitlines(), [[[str(c) for c in r] for r in rows]], path)
     if fmt == "csv":
-        data = "\n".join(",".join(str(c) for c in r) for r in rows).encode()
+        import csv
+        import io
+
+        buf = io.StringIO()
+        csv.writer(buf, lineterminator="\n").writerows(rows)
+        data = buf.getvalue().encode()
     elif fmt == "json":
         data = json.dumps({"rfq": doc.text, "items": rows[1:]}).encode()
     else:

@@ -106,3 +106,28 @@ def test_reference_uploads_parse(reference_root):
     for name in sorted(os.listdir(up)):
         res = run(FileParser().parse_file_async(os.path.join(up, name)))
         assert len(res["raw_text"]) > 10
+
+
+def test_process_pool_parsing_matches_threads(tmp_path):
+    """processes > 0 parses in spawned workers with byte-identical output."""
+    import asyncio
+
+    from replisense_rfq_amd.service.parser import FileParser
+    from replisense_rfq_amd.utils import docgen, synth
+
+    files = []
+    for i, ext in enumerate(["pdf", "docx", "xlsx", "xls", "csv"]):
+        path = tmp_path / f"doc{i}.{ext}"
+        docgen.rfq_attachment(synth.make_rfq(70 + i), ext, path)
+        files.append(path)
+
+    async def parse_all(p):
+        return await asyncio.gather(*(p.parse_file_async(str(f)) for f in files))
+
+    a = asyncio.run(parse_all(FileParser()))
+    pp = FileParser(processes=2)
+    try:
+        b = asyncio.run(parse_all(pp))
+    finally:
+        pp.close()
+    assert [x["raw_text"] for x in a] == [x["raw_text"] for x in b]
