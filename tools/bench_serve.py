@@ -55,7 +55,7 @@ async def _latency(url: str, docs: list[str]) -> list[float]:
     return out
 
 
-async def _throughput(url: str, docs: list[str], clients: int) -> tuple[float, int, int]:
+async def _throughput(url: str, docs: list, clients: int) -> tuple[float, int, int]:
     import httpx
 
     queue: asyncio.Queue = asyncio.Queue()
@@ -75,7 +75,10 @@ async def _throughput(url: str, docs: list[str], clients: int) -> tuple[float, i
             r = None
             for _ in range(3):                       # transport hiccups are retried, not
                 try:                                 # counted as extraction failures
-                    r = await c.post(url + "/parse-text/", json={"text": d})
+                    if isinstance(d, tuple):         # (filename, bytes): POST /upload/
+                        r = await c.post(url + "/upload/", files={"file": d})
+                    else:
+                        r = await c.post(url + "/parse-text/", json={"text": d})
                     break
                 except httpx.TransportError:
                     retries[0] += 1
@@ -102,12 +105,17 @@ def main():
     ap.add_argument("--latency-requests", type=int, default=10)
     ap.add_argument("--max-batch", type=int, default=1024)
     ap.add_argument("--startup-timeout", type=float, default=600.0)
+    ap.add_argument("--mode", choices=("text", "upload"), default="text",
+                    help="upload: PDF/XLSX/DOCX attachments through POST /upload/ "
+                         "(parsing on the server, RFQ_PARSER_PROCS workers)")
+    ap.add_argument("--parser-procs", type=int, default=8)
     a = ap.parse_args()
 
     from replisense_rfq_amd.utils import synth
 
     url = f"http://127.0.0.1:{a.port}"
     env = dict(os.environ, RFQ_BACKEND="engine", RFQ_MODEL=a.model, ENVIRONMENT="production",
+               RFQ_PARSER_PROCS=str(a.parser_procs),
                RFQ_MAX_BATCH=str(a.max_batch), LOG_LEVEL="warning", PYTHONUNBUFFERED="1")
     log = open(os.path.join(ROOT, "gpurun_out", "bench_serve_server.log")
                if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else os.devnull, "w")
@@ -122,11 +130,22 @@ def main():
         asyncio.run(_latency(url, warm))
         lat = asyncio.run(_latency(url, [synth.make_rfq(800_000 + i).text
                                          for i in range(a.latency_requests)]))
-        docs = [synth.make_rfq(700_000 + i).text for i in range(a.requests)]
+        if a.mode == "upload":
+            from replisense_rfq_amd.utils import docgen
+
+            fmts = ("pdf", "xlsx", "docx")
+            docs = []
+            for i in range(a.requests):
+                f = fmts[i % 3]
+                docs.append((f"rfq_{i}.{f}",
+                             docgen.rfq_attachment(synth.make_rfq(700_000 + i), f)))
+        else:
+            docs = [synth.make_rfq(700_000 + i).text for i in range(a.requests)]
         dt, ok, bad = asyncio.run(_throughput(url, docs, a.clients))
         q = statistics.quantiles(lat, n=10) if len(lat) >= 2 else [lat[0]] * 9
         print(json.dumps({
-            "metric": "http_rfq_docs_per_sec", "value": round(a.requests / dt, 3),
+            "metric": "http_rfq_docs_per_sec", "mode": a.mode,
+            "value": round(a.requests / dt, 3),
             "unit": "docs/s", "model": a.model, "clients": a.clients, "requests": a.requests,
             "valid": ok, "invalid": bad, "transport_retries": getattr(_throughput, "retries", 0),
             "p50_parse_text_http_s": round(statistics.median(lat), 4),
