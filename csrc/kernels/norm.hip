@@ -17,12 +17,15 @@ __global__ __launch_bounds__(256) void rms_norm_kernel(
   const int row = blockIdx.x;
   const int nchunk = d >> 3;
   const s16x8* xr = reinterpret_cast<const s16x8*>(x + row * x_stride);
+  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
   float v[NCH][8];
+  s16x8 wv[NCH];
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = threadIdx.x + k * blockDim.x;
     if (c < nchunk) {
+      wv[k] = wr[c];                  // weight fetched with x: one memory round trip
       unpack8(xr[c], v[k]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) ss += v[k][i] * v[k][i];
@@ -30,14 +33,13 @@ __global__ __launch_bounds__(256) void rms_norm_kernel(
   }
   ss = block_sum(ss, scratch);
   const float r = rsqrtf(ss / (float)d + eps);
-  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
   s16x8* orow = reinterpret_cast<s16x8*>(out + row * out_stride);
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = threadIdx.x + k * blockDim.x;
     if (c < nchunk) {
       float wf[8], o[8];
-      unpack8(wr[c], wf);
+      unpack8(wv[k], wf);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = v[k][i] * r * wf[i];
       orow[c] = pack8(o);
@@ -55,12 +57,15 @@ __global__ __launch_bounds__(256) void fused_add_rms_norm_kernel(
   const int nchunk = d >> 3;
   const s16x8* xr = reinterpret_cast<const s16x8*>(x + row * x_stride);
   s16x8* rr = reinterpret_cast<s16x8*>(residual + row * res_stride);
+  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
   float v[NCH][8];
+  s16x8 wv[NCH];
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = threadIdx.x + k * blockDim.x;
     if (c < nchunk) {
+      wv[k] = wr[c];                  // weight fetched with x: one memory round trip
       float a[8], b[8];
       unpack8(xr[c], a);
       unpack8(rr[c], b);
@@ -75,14 +80,13 @@ __global__ __launch_bounds__(256) void fused_add_rms_norm_kernel(
   }
   ss = block_sum(ss, scratch);
   const float r = rsqrtf(ss / (float)d + eps);
-  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
   s16x8* orow = reinterpret_cast<s16x8*>(out + row * out_stride);
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = threadIdx.x + k * blockDim.x;
     if (c < nchunk) {
       float wf[8], o[8];
-      unpack8(wr[c], wf);
+      unpack8(wv[k], wf);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = v[k][i] * r * wf[i];
       orow[c] = pack8(o);
