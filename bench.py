@@ -246,6 +246,10 @@ def main():
             print("[bench] gemm plan %s M=%d N=%d K=%d hipblaslt %.1fus -> %s %.1fus"
                   % (r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6]),
                   file=sys.stderr)
+        from replisense_rfq_amd.ops.autotune import SPLIT_REPORT
+        for r in SPLIT_REPORT:
+            print("[bench] gemm split %s M=%d N=%d K=%d one call %.1fus -> %s %.1fus" % r,
+                  file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

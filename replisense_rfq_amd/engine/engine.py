@@ -143,7 +143,10 @@ class LLMEngine:
         t0 = time.perf_counter()
         nbs = [b for b in self.cfg.graph_buckets if b <= min(64, self.cfg.max_num_seqs)] or [1]
         ms = sorted({nb * m for nb in nbs for m in TOKEN_MULTS if nb * m <= 64})
-        self.gemm_plan = tune_model(self.model, ms, nbs)
+        self.gemm_plan = tune_model(
+            self.model, ms, nbs,
+            max_tokens=min(self.cfg.max_batched_tokens, 16384) if self.cfg.gemm_split else 0,
+            max_seqs=self.cfg.max_num_seqs)
         self.tune_s = time.perf_counter() - t0
 
     def _num_blocks(self) -> int:

@@ -17,7 +17,7 @@ __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
-    "set_linear_plan", "silu_linear", "set_silu_plan",
+    "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -93,10 +93,42 @@ def silu_linear(gu, w, out=None):
     return linear(silu_mul(gu), w, out=out)
 
 
+# (N, K) -> (quantum q, table) where table[j] is the row-chunk split (in units of q
+# rows, largest first) for M in ((j-1)q, jq], or None to keep one GEMM.  Filled by
+# ops.autotune.tune_split at engine start: hipBLASLt's heuristic is uneven across
+# M (e.g. down 4096x14336 runs at 0.9 PFLOP/s at M=6656 but 1.6 at M=4096), so
+# large steps are cut into chunks whose measured times sum to less.
+_SPLIT_PLAN: dict[tuple[int, int], tuple[int, list]] = {}
+
+
+def set_split_plan(plan: dict) -> None:
+    _SPLIT_PLAN.clear()
+    _SPLIT_PLAN.update(plan)
+
+
+def split_chunks(M: int, N: int, K: int) -> list[int] | None:
+    """Row counts of the hipBLASLt calls for an [M, K] x [K, N] GEMM (None = one call)."""
+    p = _SPLIT_PLAN.get((N, K))
+    if p is None:
+        return None
+    q, table = p
+    j = -(-M // q)
+    if j >= len(table) or table[j] is None:
+        return None
+    rows, left = [], M
+    for c in table[j]:
+        r = min(left, c * q)
+        if r > 0:
+            rows.append(r)
+        left -= r
+    return rows
+
+
 def linear(x, w, out=None, plan: int | None = None):
     """out[M, N] = x[M, K] . w[N, K]^T (bf16).  Small M streams W through the skinny
     MFMA kernel (csrc/kernels/gemm_skinny.hip) when the tuning plan says it beats
-    hipBLASLt; otherwise the plain library GEMM."""
+    hipBLASLt; large M goes to hipBLASLt, split into row chunks where the start-up
+    M-split plan measured that to be faster."""
     M, K = x.shape
     N = w.shape[0]
     if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:
@@ -106,6 +138,16 @@ def linear(x, w, out=None, plan: int | None = None):
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
             _native.ops().skinny_gemm(x, w, out, cfg)
             return out
+        if _SPLIT_PLAN and M > SKINNY_MAX_M:
+            rows = split_chunks(M, N, K)
+            if rows is not None and len(rows) > 1:
+                if out is None:
+                    out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+                a = 0
+                for r in rows:
+                    torch.matmul(x[a:a + r], w.t(), out=out[a:a + r])
+                    a += r
+                return out
     if out is None:
         return x @ w.t()
     torch.matmul(x, w.t(), out=out)

@@ -13,9 +13,12 @@ import logging
 
 import torch
 
-from . import _native, set_linear_plan, set_silu_plan, silu_mul
+from . import _native, set_linear_plan, set_silu_plan, set_split_plan, silu_mul
 
 log = logging.getLogger("replisense_rfq_amd.ops")
+
+# (name, M, N, K, one-call µs, chunk rows, split µs) of the last tune_split
+SPLIT_REPORT: list = []
 
 # tile configs (bits 0-1) on the contiguous-k / plain-load variant (bits 2-3 = 3)
 CANDIDATES = (12, 13, 14, 15)
@@ -89,7 +92,65 @@ def tune_silu_down(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin:
     return plan, report
 
 
-def tune_model(model, ms: list[int], lm_ms: list[int]) -> list:
+def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0) -> list:
+    """Row-chunk plan from measured single-GEMM times.
+
+    ``times[j]`` = µs of one hipBLASLt call with ``j`` quanta of rows (``times[0]``
+    unused).  Returns ``table`` with ``table[j]`` = chunk sizes in quanta (largest
+    first) whose summed times (+ ``launch_us`` per extra call) beat ``times[j]`` by
+    ``margin``, or None where one call is best.  Exact DP over all partitions."""
+    J = len(times) - 1
+    best = [0.0] * (J + 1)
+    choice = [0] * (J + 1)        # size of one chunk of the best partition of j
+    for j in range(1, J + 1):
+        best[j], choice[j] = times[j], j
+        for c in range(1, j):
+            t = times[c] + best[j - c] + launch_us
+            if t < best[j]:
+                best[j], choice[j] = t, c
+    table: list = [None] * (J + 1)
+    for j in range(1, J + 1):
+        if choice[j] == j or best[j] > margin * times[j]:
+            continue
+        parts, r = [], j
+        while r > 0:
+            parts.append(choice[r])
+            r -= choice[r]
+        table[j] = tuple(sorted(parts, reverse=True))
+    return table
+
+
+def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], quantum: int = 256,
+               reps: int = 4) -> tuple[dict, list]:
+    """Time hipBLASLt at every multiple of ``quantum`` rows up to ``max_m[name]`` for
+    each projection and derive the M-split plan (see ops.split_chunks)."""
+    plan, report = {}, []
+    for name, ws in groups.items():
+        N, K = ws[0].shape
+        J = max_m.get(name, 0) // quantum
+        if J < 2 or (N, K) in plan:
+            continue
+        w = ws[0]
+        x = torch.randn(J * quantum, K, device=w.device, dtype=w.dtype)
+        out = torch.empty(J * quantum, N, device=w.device, dtype=w.dtype)
+        times = [0.0]
+        for j in range(1, J + 1):
+            m = j * quantum
+            times.append(_time(lambda w_, m=m: torch.matmul(x[:m], w_.t(), out=out[:m]),
+                               [w], reps))
+        table = plan_splits(times)
+        plan[(N, K)] = (quantum, table)
+        for j, parts in enumerate(table):
+            if parts is not None:
+                t_split = sum(times[c] for c in parts)
+                report.append(("split:" + name, j * quantum, N, K, round(times[j], 1),
+                               "+".join(str(c * quantum) for c in parts), round(t_split, 1)))
+        del x, out
+    return plan, report
+
+
+def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
+               max_seqs: int = 0) -> list:
     """Tune every projection of a DecoderLM and install the plan."""
     w = model.w
     groups = {"qkv": [l["qkv"] for l in w["layers"]], "o": [l["o"] for l in w["layers"]]}
@@ -105,6 +166,14 @@ def tune_model(model, ms: list[int], lm_ms: list[int]) -> list:
         splan, sreport = tune_silu_down(groups["down"], ms)
         set_silu_plan(splan)
         report += sreport
+    if max_tokens > 0:
+        mm = {k: max_tokens for k in groups}
+        mm["lm_head"] = max_seqs
+        xplan, xreport = tune_split(groups, mm)
+        set_split_plan(xplan)
+        SPLIT_REPORT[:] = xreport
+        for r in xreport:
+            log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d one call %.1fus -> %s %.1fus", *r)
     for r in report:
         log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
                  r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6])

@@ -48,6 +48,7 @@ class EngineConfig:
     moe_parallel: str = "tp"             # tp: FFN-split experts | ep: whole experts per rank
     decode_tiles: int = 2                # column tiles per decode attention work item
     tune_gemm: bool = True               # per-shape skinny-vs-hipBLASLt plan at start-up
+    gemm_split: bool = True              # + hipBLASLt row-chunk plan for large steps
     custom_allreduce: bool = False
     trace: bool = False                  # per-request JSON spans
 
@@ -70,6 +71,7 @@ class EngineConfig:
             prefix_cache=_env("RFQ_PREFIX_CACHE", cls.prefix_cache, bool),
             custom_allreduce=_env("RFQ_CUSTOM_AR", cls.custom_allreduce, bool),
             tune_gemm=_env("RFQ_TUNE_GEMM", cls.tune_gemm, bool),
+            gemm_split=_env("RFQ_GEMM_SPLIT", cls.gemm_split, bool),
             decode_tiles=_env("RFQ_DECODE_TILES", cls.decode_tiles, int),
             moe_parallel=_env("RFQ_MOE_PARALLEL", cls.moe_parallel),
             trace=_env("RFQ_TRACE", cls.trace, bool),

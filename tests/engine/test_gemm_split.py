@@ -1,0 +1,75 @@
+"""hipBLASLt M-split planner (ops/autotune.py plan_splits + ops.split_chunks): exact DP
+on synthetic timing curves, chunk rows always cover M exactly, and the split
+linear path equals one GEMM (CPU oracle)."""
+import itertools
+
+import torch
+
+from replisense_rfq_amd import ops
+from replisense_rfq_amd.ops.autotune import plan_splits
+
+
+def _brute(times, launch):
+    J = len(times) - 1
+    best = {}
+
+    def parts(n, mx):
+        if n == 0:
+            yield ()
+            return
+        for c in range(min(n, mx), 0, -1):
+            for rest in parts(n - c, c):
+                yield (c,) + rest
+
+    for j in range(1, J + 1):
+        best[j] = min(sum(times[c] for c in p) + launch * (len(p) - 1) for p in parts(j, j))
+    return best
+
+
+def test_plan_matches_bruteforce_and_margin():
+    # a curve with a cliff: 5..7 quanta are slow per row (heuristic picks a bad tile)
+    times = [0.0, 10, 18, 26, 34, 80, 95, 110, 70, 78, 86]
+    table = plan_splits(times, margin=1.0, launch_us=1.0)
+    brute = _brute(times, 1.0)
+    for j in range(1, len(times)):
+        p = table[j]
+        got = times[j] if p is None else sum(times[c] for c in p) + (len(p) - 1) * 1.0
+        assert abs(got - brute[j]) < 1e-9, (j, p, got, brute[j])
+        if p is not None:
+            assert sum(p) == j and list(p) == sorted(p, reverse=True)
+    assert table[5] is not None and table[4] is None
+    # margin: a 1 % gain is not worth a second launch
+    flat = [0.0] + [10.0 * j for j in range(1, 9)]
+    assert all(p is None for p in plan_splits(flat, margin=0.95, launch_us=0.0))
+
+
+def test_split_chunks_cover_m():
+    times = [0.0, 10, 18, 26, 34, 80, 95, 110, 70, 78, 86]
+    ops.set_split_plan({(64, 32): (16, plan_splits(times, margin=1.0, launch_us=1.0))})
+    try:
+        for M in range(1, 16 * 10 + 1):
+            rows = ops.split_chunks(M, 64, 32)
+            if rows is not None:
+                assert sum(rows) == M and all(r > 0 for r in rows)
+        assert ops.split_chunks(16 * 11, 64, 32) is None      # past the tuned range
+        assert ops.split_chunks(100, 64, 31) is None          # untuned shape
+        rows = ops.split_chunks(16 * 5 - 3, 64, 32)
+        assert rows is not None and len(rows) > 1
+    finally:
+        ops.set_split_plan({})
+
+
+def test_split_linear_equals_one_gemm(monkeypatch):
+    """The chunked path writes every row exactly once (run on CPU via the same slicing)."""
+    torch.manual_seed(0)
+    x = torch.randn(77, 32)
+    w = torch.randn(64, 32)
+    want = x @ w.t()
+    rows = [48, 16, 13]
+    out = torch.empty(77, 64)
+    a = 0
+    for r in rows:
+        torch.matmul(x[a:a + r], w.t(), out=out[a:a + r])
+        a += r
+    assert torch.allclose(out, want, atol=1e-5)
+    assert list(itertools.accumulate(rows))[-1] == 77

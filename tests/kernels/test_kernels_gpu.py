@@ -274,3 +274,26 @@ def test_moe_expert_parallel_partial(gpu, T, grouped, monkeypatch):
     logits = (x @ router.t()).cpu()
     exp = ref.moe_forward(x.cpu(), w13[e0:e0 + el].cpu(), w2[e0:e0 + el].cpu(), logits, k, e0)
     _close(out, exp, 3e-2, 2e-2, f"moe EP T={T} grouped={grouped}")
+
+
+def test_linear_m_split_plan(gpu):
+    """hipBLASLt row-chunk plan (ops.autotune.tune_split): a measured plan on a real
+    shape, then ops.linear through a forced multi-chunk split == one GEMM."""
+    from replisense_rfq_amd.ops.autotune import plan_splits, tune_split
+
+    torch.manual_seed(11)
+    w = (torch.randn(512, 1024, device=gpu) * 0.03).to(BF)
+    plan, _ = tune_split({"t": [w]}, {"t": 1024}, quantum=128, reps=1)
+    q, table = plan[(512, 1024)]
+    assert q == 128 and len(table) == 9
+    forced = plan_splits([0.0] + [1.0] * 8 + [100.0], margin=1.0, launch_us=0.0)
+    ops.set_split_plan({(512, 1024): (128, forced)})
+    try:
+        M = 128 * 8 + 77
+        rows = ops.split_chunks(M, 512, 1024)
+        assert rows is not None and len(rows) > 1 and sum(rows) == M
+        x = torch.randn(M, 1024, device=gpu, dtype=BF)
+        out = ops.linear(x, w)
+        _close(out, x.float() @ w.float().t(), 1e-2, 1e-2, "split linear")
+    finally:
+        ops.set_split_plan({})
