@@ -87,6 +87,18 @@ __device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
       (__attribute__((address_space(3))) s16x4*)(lds_ptr));
 }
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// 16-byte global -> LDS DMA (global_load_lds_dwordx4): no VGPR round trip.  The LDS
+// destination is lane-linear: wave-uniform base + lane * 16 B, so any swizzle of
+// the LDS image is applied to the per-lane *source* address.  Completion is
+// tracked by vmcnt like any other vector load.
+__device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
+#endif
+}
+
 // Counter-based RNG (splitmix/murmur style finaliser) — deterministic per
 // (seed, row, column), identical on every TP rank for the same global column.
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint32_t a, uint32_t b) {

@@ -220,14 +220,7 @@ __global__ __launch_bounds__(256) void moe_grouped_gemm_kernel(
 // so the XOR swizzle is applied to the *source* address: the lane that fills
 // slot (row, c') fetches global chunk c' ^ ((row >> 1) & 7) — the involution the
 // ds_read side already uses.  All LDS lives in one __shared__ array.
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-// 16-byte global -> LDS DMA (lane-linear destination: wave-uniform base + lane*16)
-__device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* l) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)l, 16, 0, 0);
-#endif
-}
+// (glds16: common.h)
 
 // BN = 128: 4 waves as 2x2 quadrants of 64x64 (4 MFMAs per 4 ds_read_b128).
 // BN = 256: 4 waves as 2x2 of 64x128 (8 MFMAs per 6 reads) — LDS read traffic per

@@ -66,9 +66,11 @@ def main():
     for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (1024, 1000, 416, 1)]:
         a = run(B, C, P, True, q=q)
         b = run(B, C, P, False, q=q)
+        c = run(B, C - P, 0, False, q=q)      # the suffix alone: cascade attention's floor
         print(json.dumps({"B": B, "ctx": C, "shared_prefix": P, "q": q,
                           "shared_us": round(a[0], 1), "shared_logical_TBps": round(a[1], 2),
-                          "distinct_us": round(b[0], 1), "distinct_TBps": round(b[1], 2)}),
+                          "distinct_us": round(b[0], 1), "distinct_TBps": round(b[1], 2),
+                          "suffix_only_us": round(c[0], 1)}),
               flush=True)
 
 
