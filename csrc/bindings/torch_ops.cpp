@@ -43,6 +43,7 @@ void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, i
 int64_t car_signal_bytes();
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
+void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 uint32_t car_read_error(const void*);
 void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
                        int, bf16_t*, int64_t, int, int, int, bool, bool, hipStream_t);
@@ -311,8 +312,9 @@ int64_t car_error(int64_t ptr) {
   return (int64_t)rfq::car_read_error(reinterpret_cast<const void*>(ptr));
 }
 
+// algo: 0 = auto (two-shot above 512 KiB on > 2 ranks), 1 = one-shot, 2 = two-shot
 void car_allreduce(const Tensor& inp, const Tensor& out, c10::IntArrayRef bases, int64_t rank,
-                   int64_t capacity_bytes) {
+                   int64_t capacity_bytes, int64_t algo) {
   CHECK_DEV(inp); CHECK_BF16(inp); CHECK_BF16(out);
   TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.numel() == out.numel(),
               "car_allreduce: contiguous tensors of equal size required");
@@ -322,7 +324,11 @@ void car_allreduce(const Tensor& inp, const Tensor& out, c10::IntArrayRef bases,
   TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "car_allreduce: world");
   char* b[8];
   for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
-  rfq::launch_car_oneshot(b, (int)rank, world, bp(inp), bpm(out), inp.numel(), cur_stream());
+  const bool two = algo == 2 || (algo == 0 && world > 2 && inp.numel() * 2 > (512 << 10));
+  if (two)
+    rfq::launch_car_twoshot(b, (int)rank, world, bp(inp), bpm(out), inp.numel(), cur_stream());
+  else
+    rfq::launch_car_oneshot(b, (int)rank, world, bp(inp), bpm(out), inp.numel(), cur_stream());
 }
 
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
@@ -382,7 +388,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
-  m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes) -> ()");
+  m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
+        "int algo=0) -> ()");
   // host-side setup of the custom all-reduce regions (no tensor dispatch)
   m.def("car_alloc(int data_bytes) -> int", &car_alloc_op);
   m.def("car_free(int ptr) -> ()", &car_free_op);

@@ -1,5 +1,5 @@
-// One-shot all-reduce over xGMI peer memory for tensor-parallel decode steps
-// (SURVEY.md §2.2 custom_allreduce, §2.5 C1/C2, §5.8).
+// One-shot (decode-size) and two-shot (prefill-size) all-reduce over xGMI peer
+// memory for tensor-parallel steps (SURVEY.md §2.2 custom_allreduce, §2.5 C1/C2, §5.8).
 //
 // A decode step of Llama-3-70B at TP=8 issues 160 all-reduces of a few KB to
 // ~1 MB.  At that size the cost is latency, not bandwidth: every rank simply
@@ -35,6 +35,7 @@ constexpr int kCarThreads = 512;
 
 struct CarSignal {
   uint32_t start[kCarMaxBlocks][kCarMaxRanks];
+  uint32_t mid[kCarMaxBlocks][kCarMaxRanks];     // two-shot: reduced slices published
   uint32_t end[kCarMaxBlocks][kCarMaxRanks];
   uint32_t counter[kCarMaxBlocks];
   uint32_t error;
@@ -111,6 +112,93 @@ __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
   }
 }
 
+// Two-shot all-reduce for prefill-size messages: a one-shot
+// call makes every rank read world x n bytes over xGMI, which stops paying once the
+// message is bandwidth-bound.  Here the message is cut into `world` slices and
+// every rank moves only ~2n bytes, striped over all of its links at once:
+//   1. stage sub-range b of every slice into the own region; flags start[b];
+//   2. reduce-scatter: rank r sums sub-range b of slice r over every peer's staged
+//      copy and writes the sum back into slice r of its own staging (safe: in this
+//      step peer q reads only slice q of this rank's staging); flags mid[b];
+//   3. all-gather: out[slice p, sub-range b] = peer p's reduced sub-range b;
+//      flags end[b] so no rank overwrites its staging while a peer still reads.
+// Block b of every rank owns the same sub-range of every slice, so the per-block
+// flag protocol of the one-shot kernel carries over unchanged.
+__global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
+    CarPeers peers, int rank, int world, const bf16_t* __restrict__ in,
+    bf16_t* __restrict__ out, int64_t n8) {
+  CarSignal* self = reinterpret_cast<CarSignal*>(peers.base[rank]);
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int tid = threadIdx.x;
+  const int64_t slice = (n8 + world - 1) / world;   // 16-byte chunks per slice
+  const int64_t per = (slice + nb - 1) / nb;        // ... per block within a slice
+  const int64_t o0 = b * per, o1 = min(slice, o0 + per);
+  __shared__ uint32_t cnt_s;
+  __shared__ int fail_s;
+  if (tid == 0) {
+    cnt_s = self->counter[b] + 1;
+    fail_s = 0;
+  }
+  s16x8* own = reinterpret_cast<s16x8*>(peers.base[rank] + kCarDataOffset);
+  const s16x8* src = reinterpret_cast<const s16x8*>(in);
+  // 1. stage sub-range b of every slice
+  for (int sl = 0; sl < world; ++sl) {
+    const int64_t base = sl * slice;
+    for (int64_t i = o0 + tid; i < o1; i += kCarThreads)
+      if (base + i < n8) own[base + i] = src[base + i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  const uint32_t c = cnt_s;
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->start[b][rank], c);
+    if (!car_wait(&self->start[b][tid], c)) fail_s = 1;
+  }
+  __syncthreads();
+  // 2. reduce-scatter: own slice, summed over every rank's staged copy
+  {
+    const int64_t base = rank * slice;
+    for (int64_t i = o0 + tid; i < o1; i += kCarThreads) {
+      if (base + i >= n8) break;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < world; ++p) {
+        const s16x8 v = reinterpret_cast<const s16x8*>(peers.base[p] + kCarDataOffset)[base + i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f_s(v[j]);
+      }
+      own[base + i] = pack8(acc);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->mid[b][rank], c);
+    if (!car_wait(&self->mid[b][tid], c)) fail_s = 1;
+  }
+  __syncthreads();
+  // 3. all-gather the reduced slices
+  s16x8* dst = reinterpret_cast<s16x8*>(out);
+  for (int p = 0; p < world; ++p) {
+    const s16x8* rem = reinterpret_cast<const s16x8*>(peers.base[p] + kCarDataOffset);
+    const int64_t base = p * slice;
+    for (int64_t i = o0 + tid; i < o1; i += kCarThreads)
+      if (base + i < n8) dst[base + i] = rem[base + i];
+  }
+  __syncthreads();
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->end[b][rank], c);
+    if (!car_wait(&self->end[b][tid], c)) fail_s = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    self->counter[b] = c;
+    if (fail_s) atomicAdd(&self->error, 1u);
+  }
+}
+
 // ------------------------------------------------------------------ host side
 int64_t car_signal_bytes() { return kCarDataOffset; }
 
@@ -129,6 +217,17 @@ void launch_car_oneshot(char* const* bases, int rank, int world, const bf16_t* i
   int nb = (int)((n8 + kCarThreads * 2 - 1) / (kCarThreads * 2));
   nb = nb < 1 ? 1 : (nb > kCarMaxBlocks ? kCarMaxBlocks : nb);
   car_oneshot_kernel<<<nb, kCarThreads, 0, s>>>(peers, rank, world, in, out, n8);
+}
+
+void launch_car_twoshot(char* const* bases, int rank, int world, const bf16_t* in, bf16_t* out,
+                        int64_t numel, hipStream_t s) {
+  CarPeers peers{};
+  for (int p = 0; p < world; ++p) peers.base[p] = bases[p];
+  const int64_t n8 = numel / 8;
+  const int64_t slice = (n8 + world - 1) / world;
+  int nb = (int)((slice + kCarThreads * 2 - 1) / (kCarThreads * 2));
+  nb = nb < 1 ? 1 : (nb > kCarMaxBlocks ? kCarMaxBlocks : nb);
+  car_twoshot_kernel<<<nb, kCarThreads, 0, s>>>(peers, rank, world, in, out, n8);
 }
 
 uint32_t car_read_error(const void* base) {

@@ -1,4 +1,6 @@
-"""One-shot xGMI all-reduce (csrc/comm/custom_ar.hip) for small TP messages.
+"""Custom xGMI all-reduce (csrc/comm/custom_ar.hip) for TP messages up to the
+staging capacity: one-shot for decode-size messages, two-shot (reduce-scatter +
+all-gather, ~2n bytes per rank over all links) above 512 KiB on more than 2 ranks.
 
 Setup: every rank of the TP group allocates one uncached region (signal flags +
 staging buffer), exports it with hipIpcGetMemHandle, all-gathers the handles
@@ -45,8 +47,10 @@ class CustomAllReduce:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()
                 and t.numel() % 8 == 0 and t.numel() * 2 <= self.capacity)
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        torch.ops.rfq_amd.car_allreduce(t, t, self.bases, self.rank, self.capacity)
+    def all_reduce_(self, t: torch.Tensor, algo: int = 0) -> torch.Tensor:
+        """In-place sum over the group; algo 0 = size-based choice, 1 = one-shot,
+        2 = two-shot."""
+        torch.ops.rfq_amd.car_allreduce(t, t, self.bases, self.rank, self.capacity, algo)
         self.calls += 1
         return t
 

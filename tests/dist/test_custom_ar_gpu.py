@@ -1,4 +1,4 @@
-"""Custom one-shot all-reduce (csrc/comm/custom_ar.hip) across processes.
+"""Custom one-shot / two-shot all-reduce (csrc/comm/custom_ar.hip) across processes.
 
 The development box has one MI355X, so the ranks are separate processes on the
 same GPU: the region exchange (hipIpcGetMemHandle / hipIpcOpenMemHandle), the
@@ -37,14 +37,17 @@ def _worker(rank, world, port, q):
         _native.require()
         car = CustomAllReduce(rank, world, None, capacity_bytes=4 << 20)
         errs = []
-        for n in (8, 4096, 8192 * 3, 65536 * 8, 8192 * 128):
-            g = torch.Generator(device="cuda").manual_seed(n)
-            parts = [torch.randn(n, generator=g, device="cuda").to(torch.bfloat16)
-                     for _ in range(world)]
-            x = parts[rank].clone()
-            car.all_reduce_(x)
-            exp = torch.stack([p.float() for p in parts]).sum(0)
-            errs.append(float((x.float() - exp).abs().max()))
+        # one-shot, two-shot (incl. sizes that do not split evenly into world slices
+        # and blocks) and the size-based choice
+        for algo in (1, 2, 0):
+            for n in (8, 4096, 8192 * 3 + 24, 65536 * 8, 8192 * 128, 8 * 100_003):
+                g = torch.Generator(device="cuda").manual_seed(n + algo)
+                parts = [torch.randn(n, generator=g, device="cuda").to(torch.bfloat16)
+                         for _ in range(world)]
+                x = parts[rank].clone()
+                car.all_reduce_(x, algo)
+                exp = torch.stack([p.float() for p in parts]).sum(0)
+                errs.append(float((x.float() - exp).abs().max()))
         # graph capture + replays: counters advance inside the graph
         x = torch.empty(8192 * 4, device="cuda", dtype=torch.bfloat16)
         s = torch.cuda.Stream()
@@ -56,6 +59,9 @@ def _worker(rank, world, port, q):
         with torch.cuda.graph(graph):
             x.fill_(float(rank + 1))
             car.all_reduce_(x)
+            x.mul_(1.0)
+            car.all_reduce_(x, 2)          # two-shot inside the same graph
+            x.div_(float(world))
         want = float(sum(range(1, world + 1)))
         for _ in range(3):
             dist.barrier()
