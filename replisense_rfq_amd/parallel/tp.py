@@ -25,7 +25,7 @@ class TPContext:
     rank: int = 0
     world: int = 1
     group: object = None
-    car: object = None            # CustomAllReduce for small messages (RFQ_CUSTOM_AR=1)
+    car: object = None            # CustomAllReduce (RFQ_CUSTOM_AR, on by default)
 
     @property
     def enabled(self) -> bool:
@@ -46,12 +46,31 @@ class TPContext:
         return t
 
     def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
-        """Switch small all-reduces to the xGMI one-shot kernel (GPU groups only)."""
+        """Switch all-reduces up to ``capacity_bytes`` to the xGMI one-/two-shot kernels
+        (GPU groups only).  A start-up self-test runs both algorithms against the known
+        sum; unless every rank passes with no flag timeouts the group stays on RCCL."""
         if self.world <= 1 or not torch.cuda.is_available() or self.car is not None:
             return self.car is not None
         from .custom_ar import CustomAllReduce
 
-        self.car = CustomAllReduce(self.rank, self.world, self.group, capacity_bytes)
+        car = CustomAllReduce(self.rank, self.world, self.group, capacity_bytes)
+        ok = True
+        try:
+            want = float(sum(range(1, self.world + 1)))
+            for algo, n in ((1, 4096), (2, 1 << 19)):
+                x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
+                car.all_reduce_(x, algo)
+                ok &= bool((x.float() == want).all().item())
+            ok &= car.errors() == 0
+        except RuntimeError:
+            ok = False
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 0:
+            car.close()
+            return False
+        self.car = car
         return True
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:

@@ -49,7 +49,7 @@ class EngineConfig:
     decode_tiles: int = 2                # column tiles per decode attention work item
     tune_gemm: bool = True               # per-shape skinny-vs-hipBLASLt plan at start-up
     gemm_split: bool = True              # + hipBLASLt row-chunk plan for large steps
-    custom_allreduce: bool = False
+    custom_allreduce: bool = True        # TP>1 on GPU: xGMI one-/two-shot kernels (self-tested)
     trace: bool = False                  # per-request JSON spans
 
     @classmethod

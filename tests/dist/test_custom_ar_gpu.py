@@ -69,8 +69,19 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             errs.append(float((x.float() - want).abs().max()))
         dist.barrier()
-        q.put((rank, errs, car.errors()))
+        nerr = car.errors()
         car.close()
+        # the engine's entry point: self-test, then route eligible all-reduces
+        from replisense_rfq_amd.parallel.tp import TPContext
+
+        tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
+        assert tp.enable_custom_allreduce(capacity_bytes=2 << 20), "self-test failed"
+        y = torch.full((8192,), float(rank + 1), device="cuda", dtype=torch.bfloat16)
+        tp.all_reduce_(y)
+        errs.append(float((y.float() - want).abs().max()))
+        nerr += tp.car.errors()
+        tp.car.close()
+        q.put((rank, errs, nerr))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e), -1))
