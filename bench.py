@@ -29,8 +29,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import queue
 import statistics
 import sys
+import threading
 import time
 
 import torch
@@ -40,6 +42,7 @@ from replisense_rfq_amd.engine.engine import LLMEngine
 from replisense_rfq_amd.parallel.tp import init_distributed, split_groups
 from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
 from replisense_rfq_amd.service.hints import estimate_line_items
+from replisense_rfq_amd.service.prompt import register_prompt_prefix
 from replisense_rfq_amd.utils import synth
 from replisense_rfq_amd.utils.config import EngineConfig
 
@@ -75,6 +78,7 @@ class Replica:
     def __init__(self, engine: LLMEngine, dp_rank: int, seed: int):
         self.engine = engine
         self.tok = engine.tokenizer
+        register_prompt_prefix(self.tok)         # what the service's EngineBackend does
         self.dp_rank = dp_rank
         self.seed = seed
         self.wave = 0
@@ -86,20 +90,59 @@ class Replica:
         return [synth.make_rfq(base + i) for i in range(n)]
 
     def run_wave(self, n: int, waves: int = 1) -> int:
+        """Push n * waves documents through the service path.  As in the HTTP server
+        (requests are tokenised by the API front-end while the engine steps), a
+        producer thread builds and tokenises the prompts and the engine admits each
+        one as soon as it is ready, so prompt preparation overlaps GPU execution."""
+        t0 = time.perf_counter()
         docs = [d for _ in range(waves) for d in self.docs(n)]
         n = len(docs)
-        msgs = [build_messages(d.text) for d in docs]
-        prompts = [self.tok.chat_ids(m) for m in msgs]
         eng = self.engine
-        params = [eng.default_params(seed=(self.wave * 100_003 + i) & 0xFFFFFF,
-                                     min_items=estimate_line_items(d.text))
-                  for i, d in enumerate(docs)]
-        seqs = eng.generate(prompts, params)
+        wave = self.wave
+        ready: queue.SimpleQueue = queue.SimpleQueue()
+        prep = {}
+
+        def produce():
+            ts = time.perf_counter()
+            for i, d in enumerate(docs):
+                ids = self.tok.chat_ids(build_messages(d.text))
+                ready.put((ids, eng.default_params(seed=(wave * 100_003 + i) & 0xFFFFFF,
+                                                   min_items=estimate_line_items(d.text))))
+            prep["s"] = time.perf_counter() - ts
+            ready.put(None)
+
+        old_switch = sys.getswitchinterval()
+        sys.setswitchinterval(2e-4)        # the step loop re-takes the GIL promptly
+        th = threading.Thread(target=produce, name="bench-tokenize", daemon=True)
+        th.start()
+        seqs, producing = [], True
+        try:
+            while True:
+                while producing:
+                    try:
+                        item = ready.get() if not eng.has_work() else ready.get_nowait()
+                    except queue.Empty:
+                        break
+                    if item is None:
+                        producing = False
+                    else:
+                        seqs.append(eng.add_request(*item))
+                if eng.has_work():
+                    eng.step()
+                elif not producing:
+                    break
+        finally:
+            sys.setswitchinterval(old_switch)
+            th.join()
+        t1 = t0 + prep.get("s", 0.0)
+        t2 = time.perf_counter()
         ok = 0
         for s in seqs:
             out = parse_and_validate_response(eng.decode_text(s), "direct_text_input")
             ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
         eng.runner.tp.enabled and eng.shutdown()
+        self.phases = {"prep_s_overlapped": round(t1 - t0, 2), "engine_s": round(t2 - t0, 2),
+                       "post_s": round(time.perf_counter() - t2, 2)}
         self.last = dict(
             prompt_tokens=sum(s.prompt_len for s in seqs) / n,
             completion_tokens=sum(s.num_generated for s in seqs) / n,
@@ -237,6 +280,7 @@ def main():
             "per_doc": {k: round(v, 2) for k, v in rep.last.items()},
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
                        "gemm_tune_s": round(engine.tune_s, 1),
+                       "wave_phases": getattr(rep, "phases", None),
                        "engine_steps": steps_before, "graph_steps": st.get("graph_steps"),
                        "kv_blocks": st.get("blocks"), "preempted": st.get("preempted"),
                        "host_s": {k: round(st.get(k, 0), 2) for k in

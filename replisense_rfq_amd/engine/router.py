@@ -213,6 +213,9 @@ class RouterBackend:
         from ..models.config import get_config
 
         self.tokenizer = get_tokenizer(flavor_for_vocab(get_config(router.cfg.model).vocab_size))
+        from ..service.prompt import register_prompt_prefix
+
+        register_prompt_prefix(self.tokenizer)
 
     @property
     def healthy(self) -> bool:

@@ -44,6 +44,8 @@ class Tokenizer:
                 self._tok = _HFTok.from_str(f.read().decode())
         self.flavor = flavor
         self.vocab_size = self._tok.get_vocab_size()
+        self._content_prefixes: list[str] = []
+        self._raw_prefixes: dict[str, tuple[list[int], int]] = {}
         if flavor == "llama3":
             self.bos_id = self._tok.token_to_id("<|begin_of_text|>")
             self.eot_id = self._tok.token_to_id("<|eot_id|>")
@@ -57,7 +59,44 @@ class Tokenizer:
 
     # -------------------------------------------------------------- encode/decode
     def encode(self, text: str) -> list[int]:
+        for raw, (ids, last_start) in self._raw_prefixes.items():
+            if text.startswith(raw) and self._splits_at(text, last_start, len(raw)):
+                return ids + self._tok.encode(text[len(raw):], add_special_tokens=False).ids
         return self._tok.encode(text, add_special_tokens=False).ids
+
+    def register_prefix(self, prefix: str) -> None:
+        """Declare a long string that many messages start with (the RFQ extraction
+        template is ~84 % of every user message).  chat_ids() then encodes it once:
+        BPE never merges across pre-tokenizer splits, so when the text's pre-token
+        boundaries include the end of the prefix, encode(prefix + rest) ==
+        encode(prefix) + encode(rest) exactly; the boundary is checked per text."""
+        if prefix and prefix not in self._content_prefixes:
+            self._content_prefixes.append(prefix)
+
+    def _splits_at(self, text: str, start: int, pos: int) -> bool:
+        """True if the pre-tokenizer puts a boundary at ``pos`` in ``text`` (``start`` =
+        beginning of the pre-token that ends at ``pos`` in the cached prefix)."""
+        pre = self._tok.pre_tokenizer
+        if pre is None:
+            return True
+        window = text[start:pos + 64]
+        return any(end == pos - start for _, (_, end) in pre.pre_tokenize_str(window))
+
+    def _cache_raw_prefix(self, raw: str) -> None:
+        if raw in self._raw_prefixes or len(self._raw_prefixes) >= 64:
+            return
+        pre = self._tok.pre_tokenizer
+        last_start = pre.pre_tokenize_str(raw)[-1][1][0] if pre is not None else 0
+        self._raw_prefixes[raw] = (self._tok.encode(raw, add_special_tokens=False).ids,
+                                   last_start)
+
+    def _encode_segment(self, seg: str, content_at: int = 0) -> list[int]:
+        """encode(seg) where a registered content prefix may start at ``content_at``."""
+        for p in self._content_prefixes:
+            if seg.startswith(p, content_at):
+                self._cache_raw_prefix(seg[:content_at + len(p)])
+                break
+        return self.encode(seg)
 
     def encode_batch(self, texts: list[str]) -> list[list[int]]:
         return [e.ids for e in self._tok.encode_batch(texts, add_special_tokens=False)]
@@ -85,7 +124,7 @@ class Tokenizer:
             ids = [self.bos_id]
             for m in messages:
                 ids += [self._hdr_start] + self.encode(m["role"]) + [self._hdr_end]
-                ids += self.encode("\n\n" + m["content"].strip()) + [self.eot_id]
+                ids += self._encode_segment("\n\n" + m["content"].strip(), 2) + [self.eot_id]
             if add_generation_prompt:
                 ids += [self._hdr_start] + self.encode("assistant") + [self._hdr_end]
                 ids += self.encode("\n\n")
@@ -97,7 +136,8 @@ class Tokenizer:
             if m["role"] == "user":
                 body = (sys_txt + "\n\n" + m["content"]) if sys_txt else m["content"]
                 sys_txt = ""
-                ids += self.encode(f"[INST] {body} [/INST]")
+                ids += self._encode_segment(f"[INST] {body} [/INST]",
+                                            len(body) - len(m["content"]) + 7)
             elif m["role"] == "assistant":
                 ids += self.encode(m["content"]) + [self.eot_id]
         return ids

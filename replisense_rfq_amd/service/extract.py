@@ -32,7 +32,7 @@ from typing import Any, Protocol
 
 from pydantic import ValidationError
 
-from .prompt import SYSTEM_MESSAGE, build_user_message, truncate
+from .prompt import SYSTEM_MESSAGE, build_user_message, register_prompt_prefix, truncate
 from .schema import RFQResponse
 
 log = logging.getLogger("replisense_rfq_amd.service.extract")
@@ -260,6 +260,7 @@ class EngineBackend:
     def __init__(self, engine, async_engine=None, timeout_s: float | None = None):
         self.engine = engine
         self.tokenizer = engine.tokenizer
+        register_prompt_prefix(self.tokenizer)
         self.async_engine = async_engine
         self.timeout_s = timeout_s if timeout_s is not None else engine.cfg.request_timeout_s
         self.spans: list[dict] = []
