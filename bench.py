@@ -57,14 +57,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--docs-per-step", type=int, default=2048)
-    ap.add_argument("--max-num-seqs", type=int, default=2048)
-    ap.add_argument("--latency-runs", type=int, default=5)
+    ap.add_argument("--docs-per-step", type=int, default=3072)
+    ap.add_argument("--max-num-seqs", type=int, default=3072)
+    ap.add_argument("--latency-runs", type=int, default=15)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump-forward", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--prefill-chunk", type=int, default=16384)
-    ap.add_argument("--kv-fraction", type=float, default=0.7,
+    ap.add_argument("--kv-fraction", type=float, default=0.85,
                     help="fraction of free HBM for the paged KV pool (288 GB per MI355X)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--mode", choices=("stream", "wave"), default="stream",

@@ -17,6 +17,9 @@ void launch_fused_add_rms_norm(const bf16_t*, int64_t, bf16_t*, int64_t, const b
                                int64_t, int, int, float, hipStream_t);
 void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
                         hipStream_t);
+void launch_skinny_gemm_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
+                             int, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
+                             unsigned*, hipStream_t);
 void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
@@ -102,6 +105,40 @@ void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cf
   TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "skinny_gemm: alignment");
   rfq::launch_skinny_gemm(bp(x), x.stride(0), bp(w), N, K, bpm(out), out.stride(0), M, (int)cfg,
                           cur_stream());
+}
+
+// y = x . w^T (skinny, M <= 16), then residual <- y + residual and
+// out <- rmsnorm(residual) * norm_w in the grid's last workgroup (= skinny_gemm followed
+// by fused_add_rms_norm(y, residual, norm_w, eps, out)).  counter: int32 [>= 1], zero,
+// owned by the stream (the kernel leaves it at zero).
+void skinny_gemm_norm(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& residual,
+                      const Tensor& norm_w, double eps, const Tensor& out, const Tensor& counter,
+                      int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_BF16(residual);
+  CHECK_BF16(norm_w); CHECK_BF16(out); CHECK_I32(counter);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(y); CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm_norm: w must be contiguous [N, K]");
+  const bool gated = cfg & 16;
+  const int M = x.size(0), K = gated ? x.size(1) / 2 : x.size(1), N = w.size(0);
+  const int nt = (cfg & 1) ? 2 : 1;
+  const int threads = (cfg & 2) ? 512 : 256;
+  TORCH_CHECK(!gated || x.size(1) == 2 * K, "skinny_gemm_norm: gated x must be [M, 2K]");
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm_norm: M must be in [1, 16]");
+  TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N % (16 * nt) == 0 && N % 8 == 0 &&
+                  N / 8 <= 4 * threads,
+              "skinny_gemm_norm: K % 128, N % tile and N <= 32 * threads required");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N && residual.size(0) == M &&
+                  residual.size(1) == N && out.size(0) == M && out.size(1) == N &&
+                  norm_w.numel() == N,
+              "skinny_gemm_norm: shapes");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 8 == 0 && residual.stride(0) % 8 == 0 &&
+                  out.stride(0) % 8 == 0,
+              "skinny_gemm_norm: alignment");
+  TORCH_CHECK(counter.is_cuda() && counter.numel() >= 1, "skinny_gemm_norm: counter");
+  rfq::launch_skinny_gemm_norm(bp(x), x.stride(0), bp(w), N, K, bpm(y), y.stride(0), M, (int)cfg,
+                               bpm(residual), residual.stride(0), bp(norm_w), bpm(out),
+                               out.stride(0), (float)eps,
+                               reinterpret_cast<unsigned*>(counter.data_ptr()), cur_stream());
 }
 
 void silu_mul(const Tensor& gate_up, const Tensor& out) {
@@ -388,6 +425,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("fused_add_rms_norm(Tensor x, Tensor(a!) residual, Tensor w, float eps, Tensor(b!) out) -> ()");
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("skinny_gemm_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
+        "float eps, Tensor(c!) out, Tensor(d!) counter, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
   // host-side setup of the custom all-reduce regions (no tensor dispatch)
@@ -427,6 +466,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("fused_add_rms_norm", &fused_add_rms_norm);
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
+  m.impl("skinny_gemm_norm", &skinny_gemm_norm);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);

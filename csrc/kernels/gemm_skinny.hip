@@ -54,10 +54,83 @@ __device__ __forceinline__ s16x8 ldx8(const bf16_t* p, int K) {
   }
 }
 
-template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false>
+typedef __attribute__((address_space(1))) unsigned long long gu64;   // global, for sc1 access
+
+// Optional epilogue of the o / down projections on the latency path (TP = 1):
+// residual <- bf16(Y + residual); out <- rmsnorm(residual) * w, i.e. the next
+// fused_add_rms_norm, run by the workgroup that finishes last.  Every workgroup
+// publishes its Y tile write-through (8-byte sc1 stores, vmcnt(0) in every wave,
+// barrier, then a relaxed agent-scope ticket on *counter: no release fence); the one
+// drawing gridDim.x - 1 reads Y back with sc1 loads (no acquire), normalises the M
+// rows and resets the counter for the next launch on the stream
+// (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2, §6 Guideline 16 R1).
+// No workgroup waits on another, so there is no spin and no co-residency assumption.
+struct NormEpi {
+  bf16_t* residual;
+  int64_t res_stride;
+  const bf16_t* w;
+  bf16_t* out;
+  int64_t out_stride;
+  float eps;
+  unsigned* counter;
+};
+
+constexpr int kNormMaxChunks = 4;       // hidden <= 8 * threads * 4 (8192 at 256 threads)
+
+template <int NTH>
+__device__ __forceinline__ void last_block_add_norm(const bf16_t* Y, int64_t ldy, int N, int M,
+                                                    const NormEpi& ep, float* scratch) {
+  const int nchunk = N >> 3;
+  const s16x8* wr = reinterpret_cast<const s16x8*>(ep.w);
+  for (int m = 0; m < M; ++m) {
+    const s16x8* yr = reinterpret_cast<const s16x8*>(Y + (int64_t)m * ldy);
+    s16x8* rr = reinterpret_cast<s16x8*>(ep.residual + (int64_t)m * ep.res_stride);
+    s16x8* orow = reinterpret_cast<s16x8*>(ep.out + (int64_t)m * ep.out_stride);
+    float v[kNormMaxChunks][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < kNormMaxChunks; ++k) {
+      const int c = threadIdx.x + k * NTH;
+      if (c < nchunk) {
+        float a[8], b[8];
+        const gu64* yq = (const gu64*)(yr + c);
+        const unsigned long long y0 = __hip_atomic_load(yq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long y1 = __hip_atomic_load(yq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a[i] = bf2f((bf16_t)(y0 >> (16 * i)));
+          a[4 + i] = bf2f((bf16_t)(y1 >> (16 * i)));
+        }
+        unpack8(rr[c], b);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] += b[i];
+        const s16x8 packed = pack8(a);
+        rr[c] = packed;
+        unpack8(packed, v[k]);           // normalise the rounded residual (= fused_add_rms_norm)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ss += v[k][i] * v[k][i];
+      }
+    }
+    ss = block_sum(ss, scratch);
+    const float r = rsqrtf(ss / (float)N + ep.eps);
+#pragma unroll
+    for (int k = 0; k < kNormMaxChunks; ++k) {
+      const int c = threadIdx.x + k * NTH;
+      if (c < nchunk) {
+        float wf[8], o[8];
+        unpack8(wr[c], wf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[k][i] * r * wf[i];
+        orow[c] = pack8(o);
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
-    bf16_t* __restrict__ Y, int64_t ldy, int M) {
+    bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep) {
   __shared__ f32x4 red[NW][NT * MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -153,23 +226,61 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
       uint2 v;
       v.x = pack_bf16x2(s[0], s[1]);
       v.y = pack_bf16x2(s[2], s[3]);
-      *reinterpret_cast<uint2*>(Y + (int64_t)m * ldy + n0 + a * 16 + g * 4) = v;
+      bf16_t* yp = Y + (int64_t)m * ldy + n0 + a * 16 + g * 4;
+      if constexpr (NORM)   // write-through (sc1) so the last workgroup reads it without a release
+        __hip_atomic_store((gu64*)yp,
+                           (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *reinterpret_cast<uint2*>(yp) = v;
     }
+  }
+
+  if constexpr (NORM) {
+    // publish this tile and take a ticket; the last workgroup runs the add + RMSNorm
+    __shared__ float nscratch[17];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev =
+          __hip_atomic_fetch_add(ep.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nscratch[16] = (prev == gridDim.x - 1) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (nscratch[16] == 0.f) return;
+    // every load of the handed-off Y is an sc1 load (last_block_add_norm), so a
+    // wavefront-scope fence (compiler ordering only) replaces the agent acquire
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x == 0)
+      __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_block_add_norm<NW * 64>(Y, ldy, gridDim.x * 16 * NT, M, ep, nscratch);
   }
 }
 
 template <int MT, int NT, int NW, int U>
 static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
-                       int64_t ldy, int M, int variant, hipStream_t s) {
+                       int64_t ldy, int M, int variant, bool norm, const NormEpi& ep,
+                       hipStream_t s) {
   dim3 grid(N / (16 * NT));
+  if constexpr (MT == 1) {  // fused add + RMSNorm epilogue (M <= 16): contiguous-k, plain loads
+    if (norm) {
+      if (variant >= 4)
+        hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, true, true>), grid,
+                           dim3(NW * 64), 0, s, X, ldx, W, K, Y, ldy, M, ep);
+      else
+        hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, false, true>), grid,
+                           dim3(NW * 64), 0, s, X, ldx, W, K, Y, ldy, M, ep);
+      return;
+    }
+  }
   if (variant >= 4) {   // gated X (silu(gate) * up), contiguous-k, plain loads
     hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, true, false, true>), grid, dim3(NW * 64),
-                       0, s, X, ldx, W, K, Y, ldy, M);
+                       0, s, X, ldx, W, K, Y, ldy, M, ep);
     return;
   }
 #define SK_LAUNCH(cm, nt)                                                                   \
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, cm, nt>), grid, dim3(NW * 64), 0, s, \
-                     X, ldx, W, K, Y, ldy, M)
+                     X, ldx, W, K, Y, ldy, M, ep)
   switch (variant) {
     case 0: SK_LAUNCH(false, true); break;
     case 1: SK_LAUNCH(true, true); break;
@@ -182,18 +293,19 @@ static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int
 // cfg bits: [1:0] tile (0: NT=1 NW=4, 1: NT=2 NW=4, 2: NT=1 NW=8, 3: NT=2 NW=8),
 // [3:2] variant (bit2 contiguous k-map, bit3 plain loads instead of non-temporal),
 // bit 4: gated X (x is [M, 2K] gate|up; B operand = silu(gate) * up).
-void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
-                        int64_t ldy, int M, int cfg, hipStream_t s) {
+static void skinny_dispatch(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                            bf16_t* Y, int64_t ldy, int M, int cfg, bool norm, const NormEpi& ep,
+                            hipStream_t s) {
   const int MT = (M + 15) / 16;
   const int v = (cfg & 16) ? 4 : ((cfg >> 2) & 3);
-#define SK_CASE(mt, u1, u2)                                                              \
-  case mt:                                                                               \
-    switch (cfg & 3) {                                                                   \
-      case 0: launch_cfg<mt, 1, 4, u1>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
-      case 1: launch_cfg<mt, 2, 4, u2>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
-      case 2: launch_cfg<mt, 1, 8, u1>(X, ldx, W, N, K, Y, ldy, M, v, s); break;         \
-      default: launch_cfg<mt, 2, 8, u2>(X, ldx, W, N, K, Y, ldy, M, v, s); break;        \
-    }                                                                                    \
+#define SK_CASE(mt, u1, u2)                                                                    \
+  case mt:                                                                                     \
+    switch (cfg & 3) {                                                                         \
+      case 0: launch_cfg<mt, 1, 4, u1>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
+      case 1: launch_cfg<mt, 2, 4, u2>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
+      case 2: launch_cfg<mt, 1, 8, u1>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
+      default: launch_cfg<mt, 2, 8, u2>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;    \
+    }                                                                                          \
     break;
   switch (MT) {
     SK_CASE(1, 4, 2)
@@ -202,6 +314,21 @@ void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, in
     default: SK_CASE(4, 2, 1)
   }
 #undef SK_CASE
+}
+
+void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                        int64_t ldy, int M, int cfg, hipStream_t s) {
+  skinny_dispatch(X, ldx, W, N, K, Y, ldy, M, cfg, false, NormEpi{}, s);
+}
+
+// Y = X W^T, then residual <- Y + residual, out <- rmsnorm(residual) * norm_w (M <= 16,
+// N <= 8192; counter: one zero-initialised uint32 per stream, left at zero).
+void launch_skinny_gemm_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                             bf16_t* Y, int64_t ldy, int M, int cfg, bf16_t* residual,
+                             int64_t res_stride, const bf16_t* norm_w, bf16_t* out,
+                             int64_t out_stride, float eps, unsigned* counter, hipStream_t s) {
+  const NormEpi ep{residual, res_stride, norm_w, out, out_stride, eps, counter};
+  skinny_dispatch(X, ldx, W, N, K, Y, ldy, M, cfg, true, ep, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -138,17 +138,25 @@ class DecoderLM:
                 ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                                  m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
                                  self.scale)
-            o = ops.linear(attn, lw["o"])
-            self.tp.all_reduce_(o)
-            ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
+            # TP = 1 latency path: the o / down skinny GEMM runs the residual-add
+            # RMSNorm in its last workgroup when the start-up plan measured it faster
+            fuse = not self.tp.enabled and T <= ops.NORM_FUSE_MAX_M
+            if not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
+                                                 x)):
+                o = ops.linear(attn, lw["o"])
+                self.tp.all_reduce_(o)
+                ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
+            nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
             if cfg.is_moe:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
                              expert_offset=self.expert_offset)
             else:
                 gu = ops.linear(x, lw["gate_up"])
+                if fuse and ops.linear_add_norm(gu, lw["down"], residual, nxt, eps, x,
+                                                gated=True):
+                    continue
                 mo = ops.silu_linear(gu, lw["down"])
             self.tp.all_reduce_(mo)
-            nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
             ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])

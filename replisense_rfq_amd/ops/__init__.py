@@ -18,6 +18,7 @@ __all__ = [
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
+    "set_norm_plan", "norm_plan", "norm_counter", "linear_add_norm",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -91,6 +92,57 @@ def silu_linear(gu, w, out=None):
                     return out
                 break
     return linear(silu_mul(gu), w, out=out)
+
+
+# (M, N, K, gated) -> skinny cfg whose kernel also runs the following residual-add +
+# RMSNorm in its last workgroup (gemm_skinny.hip NormEpi), or absent = unfused.
+# Filled by ops.autotune.tune_norm for TP = 1 engines; M <= 16 only.
+_NORM_PLAN: dict[tuple[int, int, int, bool], int] = {}
+_NORM_COUNTERS: dict = {}
+NORM_FUSE_MAX_M = 16
+
+
+def set_norm_plan(plan: dict) -> None:
+    _NORM_PLAN.clear()
+    _NORM_PLAN.update(plan)
+
+
+def norm_counter(device) -> torch.Tensor:
+    """The zero-initialised ticket counter of the fused-norm GEMM (one per device; the
+    kernels of a stream run in order and each leaves it at zero).  Allocated before
+    any graph capture (ops.autotune) so captured graphs bake in a stable pointer."""
+    d = torch.device(device)
+    c = _NORM_COUNTERS.get(d)
+    if c is None:
+        c = _NORM_COUNTERS[d] = torch.zeros(64, dtype=torch.int32, device=d)
+    return c
+
+
+def norm_plan(M: int, N: int, K: int, gated: bool) -> int:
+    if not _NORM_PLAN or M > NORM_FUSE_MAX_M:
+        return -1
+    for m in _TUNED_MS:
+        if m >= M:
+            return _NORM_PLAN.get((m, N, K, gated), -1)
+    return -1
+
+
+def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bool:
+    """Try the fused path for ``y = x w^T`` (``gated``: x = gate|up, y = down(SwiGLU(x)))
+    followed by ``fused_add_rms_norm(y, residual, norm_w, eps, out)``.  Returns False
+    (nothing done) when the start-up plan has no fused kernel for this shape."""
+    if not _gpu(x) or x.stride(1) != 1:
+        return False
+    M = x.shape[0]
+    K = x.shape[1] // 2 if gated else x.shape[1]
+    N = w.shape[0]
+    cfg = norm_plan(M, N, K, gated)
+    if cfg < 0:
+        return False
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    _native.ops().skinny_gemm_norm(x, w, y, residual, norm_w, eps, out,
+                                   norm_counter(x.device), cfg)
+    return True
 
 
 # (N, K) -> (quantum q, table) where table[j] is the row-chunk split (in units of q

@@ -251,6 +251,36 @@ def test_skinny_gemm_gated_swiglu(gpu, M, cfg):
     _close(out, act.float() @ w.float().cpu().t(), 2e-2, 1e-2, f"gated skinny M={M} cfg={cfg}")
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("gated,cfg", [(False, 12), (False, 13), (False, 14), (False, 15),
+                                       (True, 16), (True, 19)])
+def test_skinny_gemm_fused_add_norm(gpu, M, gated, cfg):
+    """skinny GEMM + last-workgroup residual-add RMSNorm == skinny GEMM followed by
+    fused_add_rms_norm; three launches in a row (the ticket counter must reset)."""
+    torch.manual_seed(M * 31 + cfg)
+    N, K = 4096, 1024
+    x = torch.randn(M, 2 * K if gated else K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.03).to(BF)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
+    counter = torch.zeros(4, dtype=torch.int32, device=gpu)
+    res = torch.randn(M, N, device=gpu, dtype=BF)
+    res_ref = res.clone()
+    for it in range(3):
+        y = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+        out = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+        torch.ops.rfq_amd.skinny_gemm_norm(x, w, y, res, nw, 1e-5, out, counter, cfg)
+        y_ref = torch.empty(M, N, device=gpu, dtype=BF)
+        torch.ops.rfq_amd.skinny_gemm(x, w, y_ref, cfg)
+        assert torch.equal(y, y_ref), f"GEMM part differs (iteration {it})"
+        res_cpu, out_ref = res_ref.cpu(), torch.empty(M, N, dtype=BF)
+        ref.fused_add_rms_norm(y_ref.cpu(), res_cpu, nw.cpu(), 1e-5, out_ref)
+        res_ref = res_cpu.to(gpu)
+        assert torch.equal(res, res_ref), f"residual differs (iteration {it})"
+        _close(out, out_ref, 3e-2, 1e-2, f"fused norm M={M} cfg={cfg} it={it}")
+    torch.cuda.synchronize()
+    assert int(counter[0]) == 0, "ticket counter not reset"
+
+
 @pytest.mark.parametrize("T", [3, 40, 100, 200])
 @pytest.mark.parametrize("grouped", [False, True])
 def test_moe_expert_parallel_partial(gpu, T, grouped, monkeypatch):
