@@ -29,7 +29,7 @@ class EngineConfig:
     dp: int = 1
     device: str = "auto"                 # auto -> cuda if available else cpu
     seed: int = 0
-    kv_fraction: float = 0.45            # of free HBM for the paged KV pool
+    kv_fraction: float = 0.85            # of free HBM for the paged KV pool (bench.py default)
     max_kv_blocks: int = 0               # 0 = from kv_fraction
     block_size: int = 32                 # tokens per KV page (kernel tile)
     max_num_seqs: int = 256

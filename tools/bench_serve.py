@@ -55,45 +55,77 @@ async def _latency(url: str, docs: list[str]) -> list[float]:
     return out
 
 
-async def _throughput(url: str, docs: list, clients: int) -> tuple[float, int, int]:
-    import httpx
+async def _throughput_aio(url: str, docs: list, clients: int) -> tuple[int, int, int]:
+    """One client process: ``clients`` concurrent keep-alive connections (aiohttp)."""
+    import aiohttp
 
     queue: asyncio.Queue = asyncio.Queue()
     for d in docs:
         queue.put_nowait(d)
-    ok = bad = 0
-    retries = [0]
-    limits = httpx.Limits(max_connections=clients, max_keepalive_connections=clients)
+    ok = bad = retries = 0
 
-    async def worker(c):
-        nonlocal ok, bad
+    async def worker(sess):
+        nonlocal ok, bad, retries
         while True:
             try:
                 d = queue.get_nowait()
             except asyncio.QueueEmpty:
                 return
-            r = None
+            status, body = None, {}
             for _ in range(3):                       # transport hiccups are retried, not
                 try:                                 # counted as extraction failures
                     if isinstance(d, tuple):         # (filename, bytes): POST /upload/
-                        r = await c.post(url + "/upload/", files={"file": d})
+                        form = aiohttp.FormData()
+                        form.add_field("file", d[1], filename=d[0])
+                        async with sess.post(url + "/upload/", data=form) as r:
+                            status, body = r.status, await r.json()
                     else:
-                        r = await c.post(url + "/parse-text/", json={"text": d})
+                        async with sess.post(url + "/parse-text/", json={"text": d}) as r:
+                            status, body = r.status, await r.json()
                     break
-                except httpx.TransportError:
-                    retries[0] += 1
-            data = r.json().get("data", {}) if r is not None and r.status_code == 200 else {}
+                except (aiohttp.ClientError, asyncio.TimeoutError):
+                    retries += 1
+            data = body.get("data", {}) if status == 200 else {}
             if data.get("success") and "validation warnings" not in data.get("message", ""):
                 ok += 1
             else:
                 bad += 1
 
-    async with httpx.AsyncClient(timeout=600.0, limits=limits) as c:
-        t0 = time.perf_counter()
-        await asyncio.gather(*(worker(c) for _ in range(clients)))
-        dt = time.perf_counter() - t0
-    _throughput.retries = retries[0]
-    return dt, ok, bad
+    conn = aiohttp.TCPConnector(limit=clients, limit_per_host=clients)
+    async with aiohttp.ClientSession(connector=conn,
+                                     timeout=aiohttp.ClientTimeout(total=600)) as sess:
+        await asyncio.gather(*(worker(sess) for _ in range(clients)))
+    return ok, bad, retries
+
+
+def _client_proc(url, docs, clients, start_evt, out_q):
+    start_evt.wait()
+    out_q.put(asyncio.run(_throughput_aio(url, docs, clients)))
+
+
+def _throughput(url: str, docs: list, clients: int, procs: int = 4) -> tuple[float, int, int]:
+    """Closed-loop load from ``procs`` client processes (``clients`` connections in
+    total): one Python HTTP client process saturates its own CPU long before the
+    server does (httpx: ~23 ms of client CPU per request at 512 connections)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
+    procs = max(1, min(procs, clients))
+    start_evt, out_q = ctx.Event(), ctx.Queue()
+    ps = [ctx.Process(target=_client_proc,
+                      args=(url, docs[i::procs], clients // procs + (i < clients % procs),
+                            start_evt, out_q), daemon=True) for i in range(procs)]
+    for p in ps:
+        p.start()
+    time.sleep(1.0)                               # let every client process import
+    t0 = time.perf_counter()
+    start_evt.set()
+    res = [out_q.get() for _ in ps]
+    dt = time.perf_counter() - t0
+    for p in ps:
+        p.join()
+    _throughput.retries = sum(r[2] for r in res)
+    return dt, sum(r[0] for r in res), sum(r[1] for r in res)
 
 
 def main():
@@ -109,6 +141,7 @@ def main():
                     help="upload: PDF/XLSX/DOCX attachments through POST /upload/ "
                          "(parsing on the server, RFQ_PARSER_PROCS workers)")
     ap.add_argument("--parser-procs", type=int, default=8)
+    ap.add_argument("--client-procs", type=int, default=4)
     a = ap.parse_args()
 
     from replisense_rfq_amd.utils import synth
@@ -141,7 +174,14 @@ def main():
                              docgen.rfq_attachment(synth.make_rfq(700_000 + i), f)))
         else:
             docs = [synth.make_rfq(700_000 + i).text for i in range(a.requests)]
-        dt, ok, bad = asyncio.run(_throughput(url, docs, a.clients))
+        dt, ok, bad = _throughput(url, docs, a.clients, a.client_procs)
+        try:
+            import httpx
+
+            m = httpx.get(url + "/metrics", timeout=10.0).json().get("data", {})
+            eng = m.get("engine") or m.get("router") or {}
+        except Exception:                      # metrics are diagnostics only
+            eng = {}
         q = statistics.quantiles(lat, n=10) if len(lat) >= 2 else [lat[0]] * 9
         print(json.dumps({
             "metric": "http_rfq_docs_per_sec", "mode": a.mode,
@@ -151,6 +191,10 @@ def main():
             "p50_parse_text_http_s": round(statistics.median(lat), 4),
             "p90_parse_text_http_s": round(q[8], 4),
             "baseline_p50_s": 0.883, "server_startup_s": round(startup, 1),
+            "engine": {k: eng[k] for k in ("steps", "graph_steps", "preempted", "blocks",
+                                           "forward_s", "execute_s", "post_s", "running", "replicas",
+                                           "outstanding")
+                       if k in eng},
             "data": "synthetic RFQ documents, random-init weights"}), flush=True)
     finally:
         try:
