@@ -20,6 +20,9 @@ void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*
 void launch_skinny_gemm_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
                              unsigned*, hipStream_t);
+void launch_skinny_gemm_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
+                             int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*,
+                             int, int, int, hipStream_t);
 void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
@@ -139,6 +142,37 @@ void skinny_gemm_norm(const Tensor& x, const Tensor& w, const Tensor& y, const T
                                bpm(residual), residual.stride(0), bp(norm_w), bpm(out),
                                out.stride(0), (float)eps,
                                reinterpret_cast<unsigned*>(counter.data_ptr()), cur_stream());
+}
+
+// qkv = x . w^T (skinny, M <= 16) with NeoX RoPE on q/k and the paged KV append in the
+// epilogue (= skinny_gemm followed by rope_kv); only qkv's q columns are written.
+void skinny_gemm_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
+                      const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
+                      const Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(qkv); CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(qkv);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm_rope: w must be contiguous [N, K]");
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm_rope: M must be in [1, 16]");
+  TORCH_CHECK((cfg & 1) && !(cfg & 16), "skinny_gemm_rope: cfg must select NT = 2, plain x");
+  TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N == (Hq + 2 * Hkv) * 128,
+              "skinny_gemm_rope: w must be [(Hq + 2 Hkv) * 128, K], K % 128 == 0");
+  TORCH_CHECK(qkv.size(0) == M && qkv.size(1) == N && qkv.stride(0) % 4 == 0 &&
+                  x.stride(0) % 8 == 0,
+              "skinny_gemm_rope: qkv shape / alignment");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == 128,
+              "skinny_gemm_rope: cos_sin must be fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == 128 &&
+                  k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  v_cache.sizes() == k_cache.sizes(),
+              "skinny_gemm_rope: cache must be [blocks, Hkv, BS, 128]");
+  TORCH_CHECK(positions.numel() >= M && slot_mapping.numel() >= M, "skinny_gemm_rope: metadata");
+  rfq::launch_skinny_gemm_rope(bp(x), x.stride(0), bp(w), N, K, bpm(qkv), qkv.stride(0), M,
+                               (int)cfg, positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
+                               slot_mapping.data_ptr<int32_t>(), bpm(k_cache), bpm(v_cache),
+                               (int)Hq, (int)Hkv, k_cache.size(2), cur_stream());
 }
 
 void silu_mul(const Tensor& gate_up, const Tensor& out) {
@@ -427,6 +461,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
   m.def("skinny_gemm_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
         "float eps, Tensor(c!) out, Tensor(d!) counter, int cfg) -> ()");
+  m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
   // host-side setup of the custom all-reduce regions (no tensor dispatch)
@@ -467,6 +503,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("skinny_gemm_norm", &skinny_gemm_norm);
+  m.impl("skinny_gemm_rope", &skinny_gemm_rope);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);

@@ -127,20 +127,40 @@ __device__ __forceinline__ void last_block_add_norm(const bf16_t* Y, int64_t ldy
   }
 }
 
-template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false>
+// Optional epilogue of the fused QKV projection on the latency path: NeoX RoPE on
+// q and k and the paged KV-cache append (rope_kv.hip) applied to the fp32
+// accumulators.  The workgroup's two 16-feature tiles are the rotate-half partners
+// [h*128 + 16j, +16) and [h*128 + 64 + 16j, +16) of one head, so every lane holds both
+// halves of its 4 rotary pairs in the same accumulator slots: no shuffles.  q goes
+// back to Y (attention reads it there), k/v go straight to the cache.
+struct RopeEpi {
+  const int32_t* positions;
+  const float* cos_sin;          // [max_pos, 128] fp32: cos at [d], sin at [64 + d]
+  const int32_t* slots;          // KV slot per token, -1 = padding (no cache write)
+  bf16_t* k_cache;               // [blocks, Hkv, BS, 128]
+  bf16_t* v_cache;
+  int Hq, Hkv, BS;
+};
+
+template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false,
+          bool ROPE = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
-    bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep) {
+    bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep, RopeEpi re = RopeEpi{}) {
+  static_assert(!ROPE || (MT == 1 && NT == 2 && !NORM && !GX), "RoPE epilogue: MT=1, NT=2");
   __shared__ f32x4 red[NW][NT * MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * (16 * NT);
+  // ROPE: block b owns head b/4, rotary pair block b%4 (features n0 and n0 + 64)
+  const int n0 = ROPE ? (blockIdx.x >> 2) * 128 + (blockIdx.x & 3) * 16 : blockIdx.x * (16 * NT);
+  constexpr int ASTRIDE = ROPE ? 64 : 16;
   const int nks = K >> 7;
   const int ks0 = wave * nks / NW, ks1 = (wave + 1) * nks / NW;
 
   const bf16_t* wp[NT];
 #pragma unroll
-  for (int a = 0; a < NT; ++a) wp[a] = W + (int64_t)(n0 + a * 16 + r) * K + g * (CMAP ? 8 : 32);
+  for (int a = 0; a < NT; ++a)
+    wp[a] = W + (int64_t)(n0 + a * ASTRIDE + r) * K + g * (CMAP ? 8 : 32);
   constexpr int JS = CMAP ? 32 : 8;                 // element stride between MFMA chunks
   const bf16_t* xp[MT];
   bool xv[MT];
@@ -213,6 +233,57 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 #pragma unroll
       for (int t = 0; t < MT; ++t) red[wave][a * MT + t][lane] = acc[a][t];
     __syncthreads();
+  }
+  if constexpr (ROPE) {
+    if (wave != 0) return;
+    f32x4 x1 = NW == 1 ? acc[0][0] : red[0][0][lane];
+    f32x4 x2 = NW == 1 ? acc[1][0] : red[0][1][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) {
+      x1 += red[w2][0][lane];
+      x2 += red[w2][1][lane];
+    }
+    const int m = r;                                   // token (MT = 1)
+    if (m >= M) return;
+    const int h = blockIdx.x >> 2;                     // head in [q | k | v]
+    const int d0 = (blockIdx.x & 3) * 16 + g * 4;      // rotary index of x1[0]
+    float o1[4], o2[4];
+    if (h < re.Hq + re.Hkv) {
+      const float* cs = re.cos_sin + (int64_t)re.positions[m] * 128;
+      const float4 c = *reinterpret_cast<const float4*>(cs + d0);
+      const float4 sn = *reinterpret_cast<const float4*>(cs + 64 + d0);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o1[i] = x1[i] * cc[i] - x2[i] * ss[i];
+        o2[i] = x2[i] * cc[i] + x1[i] * ss[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o1[i] = x1[i];
+        o2[i] = x2[i];
+      }
+    }
+    uint2 v1, v2;
+    v1.x = pack_bf16x2(o1[0], o1[1]);
+    v1.y = pack_bf16x2(o1[2], o1[3]);
+    v2.x = pack_bf16x2(o2[0], o2[1]);
+    v2.y = pack_bf16x2(o2[2], o2[3]);
+    bf16_t* dst;
+    if (h < re.Hq) {
+      dst = Y + (int64_t)m * ldy + h * 128;
+    } else {
+      const int slot = re.slots[m];
+      if (slot < 0) return;                            // padding row: no KV write
+      const bool is_k = h < re.Hq + re.Hkv;
+      const int kvh = is_k ? h - re.Hq : h - re.Hq - re.Hkv;
+      dst = (is_k ? re.k_cache : re.v_cache) +
+            (((int64_t)(slot / re.BS) * re.Hkv + kvh) * re.BS + slot % re.BS) * 128;
+    }
+    *reinterpret_cast<uint2*>(dst + d0) = v1;
+    *reinterpret_cast<uint2*>(dst + 64 + d0) = v2;
+    return;
   }
   // D layout (16x16): lane holds rows (g*4 + i) = output features, col r = token.
   for (int tile = wave; tile < NT * MT; tile += NW) {
@@ -319,6 +390,22 @@ static void skinny_dispatch(const bf16_t* X, int64_t ldx, const bf16_t* W, int N
 void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
                         int64_t ldy, int M, int cfg, hipStream_t s) {
   skinny_dispatch(X, ldx, W, N, K, Y, ldy, M, cfg, false, NormEpi{}, s);
+}
+
+// Fused QKV projection + RoPE + KV append (M <= 16, N = (Hq + 2 Hkv) * 128; cfg bit 0
+// must select NT = 2; bit 1 picks 4 or 8 waves).  Only the q columns of Y are written.
+void launch_skinny_gemm_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                             bf16_t* Y, int64_t ldy, int M, int cfg, const int32_t* positions,
+                             const float* cos_sin, const int32_t* slots, bf16_t* k_cache,
+                             bf16_t* v_cache, int Hq, int Hkv, int BS, hipStream_t s) {
+  const RopeEpi re{positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, BS};
+  const dim3 grid(N / 32);
+  if (cfg & 2)
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 8, 2, true, false, false, false, true>), grid,
+                       dim3(512), 0, s, X, ldx, W, K, Y, ldy, M, NormEpi{}, re);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 4, 2, true, false, false, false, true>), grid,
+                       dim3(256), 0, s, X, ldx, W, K, Y, ldy, M, NormEpi{}, re);
 }
 
 // Y = X W^T, then residual <- Y + residual, out <- rmsnorm(residual) * norm_w (M <= 16,

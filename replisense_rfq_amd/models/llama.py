@@ -6,7 +6,7 @@ MLP).  A forward pass consumes a *mixed* token batch laid out as
 
   embed -> for each layer:
      fused_add_rms_norm -> QKV GEMM (hipBLASLt) -> rope_kv (q in place, k/v into
-     the paged cache) -> attn_decode (split-K MFMA; decode rows and short grammar
+     the paged cache; on the latency path one skinny GEMM does both) -> attn_decode (split-K MFMA; decode rows and short grammar
      jump-forward extends) + attn_prefill (varlen causal MFMA flash; prompt
      chunks) -> O GEMM -> [all-reduce]
      -> fused_add_rms_norm -> gate|up GEMM -> silu_mul -> down GEMM -> [all-reduce]
@@ -125,8 +125,8 @@ class DecoderLM:
         for li in range(L):
             lw = w["layers"][li]
             kc, vc = self.kv_k[li], self.kv_v[li]
-            qkv = ops.linear(x, lw["qkv"])
-            ops.rope_kv(qkv, m.positions, self.cos_sin, m.slot_mapping, kc, vc, hq, hkv)
+            qkv = ops.qkv_rope(x, lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
+                               hq, hkv)
             if D > 0:
                 po, pm = dec_parts if dec_parts is not None else (attn, attn)
                 ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,

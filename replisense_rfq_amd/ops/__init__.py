@@ -18,7 +18,8 @@ __all__ = [
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
-    "set_norm_plan", "norm_plan", "norm_counter", "linear_add_norm",
+    "set_norm_plan", "norm_plan", "norm_counter", "linear_add_norm", "set_rope_plan",
+    "rope_plan", "qkv_rope",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -143,6 +144,42 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     _native.ops().skinny_gemm_norm(x, w, y, residual, norm_w, eps, out,
                                    norm_counter(x.device), cfg)
     return True
+
+
+# (M, N, K) -> skinny cfg (NT = 2) whose epilogue applies RoPE to q/k and appends k/v
+# to the paged cache (gemm_skinny.hip RopeEpi), or absent = linear + rope_kv.
+_ROPE_PLAN: dict[tuple[int, int, int], int] = {}
+ROPE_FUSE_MAX_M = 16
+
+
+def set_rope_plan(plan: dict) -> None:
+    _ROPE_PLAN.clear()
+    _ROPE_PLAN.update(plan)
+
+
+def rope_plan(M: int, N: int, K: int) -> int:
+    if not _ROPE_PLAN or M > ROPE_FUSE_MAX_M:
+        return -1
+    for m in _TUNED_MS:
+        if m >= M:
+            return _ROPE_PLAN.get((m, N, K), -1)
+    return -1
+
+
+def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
+    """qkv = x w^T, then NeoX RoPE on q (in place) and k, k/v appended to the paged
+    cache.  Small M: one skinny kernel does all of it in its epilogue when the start-up
+    plan measured that faster (then only the q columns of the result are written)."""
+    if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+        cfg = rope_plan(x.shape[0], w.shape[0], x.shape[1])
+        if cfg >= 0:
+            qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+            _native.ops().skinny_gemm_rope(x, w, qkv, positions, cos_sin, slot_mapping, k_cache,
+                                           v_cache, Hq, Hkv, cfg)
+            return qkv
+    qkv = linear(x, w)
+    rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
+    return qkv
 
 
 # (N, K) -> (quantum q, table) where table[j] is the row-chunk split (in units of q

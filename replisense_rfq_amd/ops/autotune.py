@@ -14,8 +14,8 @@ import os
 
 import torch
 
-from . import (_native, set_linear_plan, set_norm_plan, set_silu_plan, set_split_plan, silu_linear,
-               silu_mul)
+from . import (_native, set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan,
+               set_split_plan, silu_linear, silu_mul)
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -160,6 +160,46 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
     return plan, report
 
 
+def tune_rope(ws: list[torch.Tensor], ms: list[int], cos_sin: torch.Tensor, hq: int, hkv: int,
+              reps: int = 2, margin: float = 0.97):
+    """QKV projection followed by rope_kv (planned GEMM + rope_kv.hip) vs the skinny
+    kernel with the RoPE / KV-append epilogue (NT = 2 tiles, 4 or 8 waves)."""
+    from . import ROPE_FUSE_MAX_M, linear, rope_kv
+
+    ops = _native.ops()
+    N, K = ws[0].shape
+    plan, report = {}, []
+    if K % 128 or N != (hq + 2 * hkv) * 128:
+        return plan, report
+    dev, dt = ws[0].device, ws[0].dtype
+    for M in ms:
+        if M > ROPE_FUSE_MAX_M:
+            continue
+        x = torch.randn(M, K, device=dev, dtype=dt)
+        qkv = torch.empty(M, N, device=dev, dtype=dt)
+        nb = M // 32 + 2
+        kc = torch.zeros(nb, hkv, 32, 128, device=dev, dtype=dt)
+        vc = torch.zeros_like(kc)
+        pos = torch.arange(100, 100 + M, device=dev, dtype=torch.int32)
+        slots = torch.arange(M, device=dev, dtype=torch.int32)
+
+        def ref(w):
+            linear(x, w, out=qkv)
+            rope_kv(qkv, pos, cos_sin, slots, kc, vc, hq, hkv)
+
+        t_ref = _time(ref, ws, reps)
+        best, t_best = -1, t_ref * margin
+        for c in (13, 15):
+            t = _time(lambda w, c=c: ops.skinny_gemm_rope(x, w, qkv, pos, cos_sin, slots, kc, vc,
+                                                          hq, hkv, c), ws, reps)
+            if t < t_best:
+                best, t_best = c, t
+        if best >= 0:
+            plan[(M, N, K)] = best
+        report.append(("qkv+rope", M, N, K, round(t_ref, 1), best, round(min(t_best, t_ref), 1)))
+    return plan, report
+
+
 def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0) -> list:
     """Row-chunk plan from measured single-GEMM times.
 
@@ -234,6 +274,10 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
         splan, sreport = tune_silu_down(groups["down"], ms)
         set_silu_plan(splan)
         report += sreport
+    if os.environ.get("RFQ_FUSE_ROPE", "1") != "0" and getattr(model, "cos_sin", None) is not None:
+        rplan, rreport = tune_rope(groups["qkv"], ms, model.cos_sin, model.hq, model.hkv)
+        set_rope_plan(rplan)
+        report += rreport
     tp = getattr(model, "tp", None)
     if os.environ.get("RFQ_FUSE_NORM", "1") != "0" and not (tp is not None and tp.enabled):
         # TP = 1 only: with TP an all-reduce sits between the projection and the norm

@@ -281,6 +281,35 @@ def test_skinny_gemm_fused_add_norm(gpu, M, gated, cfg):
     assert int(counter[0]) == 0, "ticket counter not reset"
 
 
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("cfg", [13, 15])
+def test_skinny_gemm_rope_kv(gpu, M, cfg):
+    """QKV skinny GEMM with the RoPE + paged-KV-append epilogue == fp32 GEMM followed by
+    the rope_kv oracle (q columns of the output, k/v pages of the cache); padding rows
+    (slot -1) write nothing."""
+    torch.manual_seed(M * 13 + cfg)
+    Hq, Hkv, K = 8, 2, 512
+    N = (Hq + 2 * Hkv) * 128
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.05).to(BF)
+    cos_sin = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(4 * 32, device=gpu)[:M].to(torch.int32)
+    if M > 1:
+        slots[-1] = -1
+    kc = torch.zeros(4, Hkv, 32, 128, device=gpu, dtype=BF)
+    vc = torch.zeros_like(kc)
+    qkv = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm_rope(x, w, qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, cfg)
+    exp = (x.float() @ w.float().t()).cpu()
+    kc_e, vc_e = torch.zeros(kc.shape), torch.zeros(vc.shape)
+    ref.rope_kv(exp, pos.cpu(), cos_sin.cpu(), slots.cpu(), kc_e, vc_e, Hq, Hkv)
+    q = Hq * 128
+    _close(qkv[:, :q], exp[:, :q], 2e-2, 1e-2, f"rope q M={M} cfg={cfg}")
+    _close(kc, kc_e, 2e-2, 1e-2, f"rope k cache M={M} cfg={cfg}")
+    _close(vc, vc_e, 2e-2, 1e-2, f"v cache M={M} cfg={cfg}")
+
+
 @pytest.mark.parametrize("T", [3, 40, 100, 200])
 @pytest.mark.parametrize("grouped", [False, True])
 def test_moe_expert_parallel_partial(gpu, T, grouped, monkeypatch):
