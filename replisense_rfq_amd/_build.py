@@ -104,9 +104,12 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> Path:
         futs = [ex.submit(_compile, s, KERNEL_FLAGS + [f"-I{CSRC / 'kernels'}"], headers, "k")
                 for s in kernel_srcs]
         futs.append(ex.submit(_compile, CSRC / "bindings" / "torch_ops.cpp", bind_flags, [], "b"))
+        futs.append(ex.submit(_compile, CSRC / "bindings" / "gemm_lt.cpp",
+                              bind_flags + [f"-I{ROCM / 'include'}"], [], "b"))
         objs = [f.result() for f in futs]
     libs = [f"-L{tdir / 'lib'}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-            f"-Wl,-rpath,{tdir / 'lib'}"]
+            f"-Wl,-rpath,{tdir / 'lib'}", f"-L{ROCM / 'lib'}", "-lhipblaslt",
+            f"-Wl,-rpath,{ROCM / 'lib'}"]
     _link(C_SO, objs, libs, "C" + ARCH)
     if verbose:
         print(f"[rfq build] {C_SO}")

@@ -200,7 +200,7 @@ def split_chunks(M: int, N: int, K: int) -> list[int] | None:
     p = _SPLIT_PLAN.get((N, K))
     if p is None:
         return None
-    q, table = p
+    q, table = p[0], p[1]
     j = -(-M // q)
     if j >= len(table) or table[j] is None:
         return None
@@ -211,6 +211,25 @@ def split_chunks(M: int, N: int, K: int) -> list[int] | None:
             rows.append(r)
         left -= r
     return rows
+
+
+_LT_BAD: set = set()        # (algo, M) pairs hipBLASLt rejected: plain matmul for those
+
+
+def _lt_or_torch(x, w, out) -> None:
+    """out = x w^T with the algorithm the start-up plan measured fastest for this
+    M bucket (csrc/bindings/gemm_lt.cpp), else torch.matmul."""
+    M, N, K = x.shape[0], w.shape[0], x.shape[1]
+    p = _SPLIT_PLAN.get((N, K))
+    if p is not None and len(p) > 2:
+        q, algos = p[0], p[2]
+        j = -(-M // q)
+        a = algos[j] if j < len(algos) else -1
+        if a >= 0 and (a, M) not in _LT_BAD:
+            if _native.ops().lt_matmul(x, w, out, a) == 0:
+                return
+            _LT_BAD.add((a, M))
+    torch.matmul(x, w.t(), out=out)
 
 
 def linear(x, w, out=None, plan: int | None = None):
@@ -227,16 +246,15 @@ def linear(x, w, out=None, plan: int | None = None):
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
             _native.ops().skinny_gemm(x, w, out, cfg)
             return out
-        if _SPLIT_PLAN and M > SKINNY_MAX_M:
-            rows = split_chunks(M, N, K)
-            if rows is not None and len(rows) > 1:
-                if out is None:
-                    out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-                a = 0
-                for r in rows:
-                    torch.matmul(x[a:a + r], w.t(), out=out[a:a + r])
-                    a += r
-                return out
+        if _SPLIT_PLAN and M > SKINNY_MAX_M and (N, K) in _SPLIT_PLAN:
+            if out is None:
+                out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            rows = split_chunks(M, N, K) or [M]
+            a = 0
+            for r in rows:
+                _lt_or_torch(x[a:a + r], w, out[a:a + r])
+                a += r
+            return out
     if out is None:
         return x @ w.t()
     torch.matmul(x, w.t(), out=out)

@@ -26,7 +26,7 @@ SPLIT_REPORT: list = []
 CANDIDATES = (12, 13, 14, 15)
 
 
-def _time(fn, ws, reps: int) -> float:
+def _time(fn, ws, reps: int, graph: bool = True) -> float:
     """µs per call of fn(w) over the weight list, replayed from a captured hipGraph:
     the decode steps these plans serve run as graphs, so host launch cost must not
     enter the comparison (eager timing of 1-2 µs-scale kernels measures Python)."""
@@ -34,7 +34,7 @@ def _time(fn, ws, reps: int) -> float:
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     g = None
-    if os.environ.get("RFQ_TUNE_GRAPHS", "1") != "0":
+    if graph and os.environ.get("RFQ_TUNE_GRAPHS", "1") != "0":
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -228,10 +228,18 @@ def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0
     return table
 
 
+LT_CANDIDATES = int(os.environ.get("RFQ_GEMM_LT_CANDIDATES", "6"))   # heuristic algorithms timed per (M bucket, N, K)
+
+
 def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], quantum: int = 256,
-               reps: int = 4) -> tuple[dict, list]:
-    """Time hipBLASLt at every multiple of ``quantum`` rows up to ``max_m[name]`` for
-    each projection and derive the M-split plan (see ops.split_chunks)."""
+               reps: int = 3) -> tuple[dict, list]:
+    """For each projection and every multiple of ``quantum`` rows up to ``max_m[name]``:
+    time torch.matmul (hipBLASLt's first heuristic choice) and the heuristic's top
+    LT_CANDIDATES algorithms called directly (csrc/bindings/gemm_lt.cpp), keep the
+    fastest per bucket, then derive the M-split plan over the best times (see
+    ops.split_chunks / ops.linear)."""
+    ops = _native.ops()
+    lt_on = os.environ.get("RFQ_GEMM_LT", "0") == "1"     # measured neutral: off by default
     plan, report = {}, []
     for name, ws in groups.items():
         N, K = ws[0].shape
@@ -241,13 +249,26 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
         w = ws[0]
         x = torch.randn(J * quantum, K, device=w.device, dtype=w.dtype)
         out = torch.empty(J * quantum, N, device=w.device, dtype=w.dtype)
-        times = [0.0]
+        times, algos, n_lt = [0.0], [-1], 0
         for j in range(1, J + 1):
             m = j * quantum
-            times.append(_time(lambda w_, m=m: torch.matmul(x[:m], w_.t(), out=out[:m]),
-                               [w], reps))
+            t_best = _time(lambda w_, m=m: torch.matmul(x[:m], w_.t(), out=out[:m]), [w], reps,
+                           graph=False)
+            a_best = -1
+            if lt_on:
+                for a in ops.lt_heuristic(m, N, K, LT_CANDIDATES):
+                    if ops.lt_matmul(x[:m], w, out[:m], a) != 0:
+                        continue                     # algorithm rejects this shape
+                    t = _time(lambda w_, m=m, a=a: ops.lt_matmul(x[:m], w_, out[:m], a), [w],
+                              reps, graph=False)
+                    if t < 0.98 * t_best:
+                        t_best, a_best = t, a
+            n_lt += a_best >= 0
+            times.append(t_best)
+            algos.append(a_best)
         table = plan_splits(times)
-        plan[(N, K)] = (quantum, table)
+        plan[(N, K)] = (quantum, table, algos)
+        report.append(("lt:" + name, J * quantum, N, K, J, f"{n_lt}/{J} buckets", 0.0))
         for j, parts in enumerate(table):
             if parts is not None:
                 t_split = sum(times[c] for c in parts)

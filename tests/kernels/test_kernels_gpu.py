@@ -281,6 +281,28 @@ def test_skinny_gemm_fused_add_norm(gpu, M, gated, cfg):
     assert int(counter[0]) == 0, "ticket counter not reset"
 
 
+@pytest.mark.parametrize("M", [200, 512, 1000])
+def test_lt_matmul_every_heuristic_algo(gpu, M):
+    """Direct hipBLASLt calls (gemm_lt.cpp) with each of the heuristic's top algorithms
+    == fp32 x w^T, including a row-strided output slice; an out-of-range index fails
+    with a non-zero status instead of launching."""
+    torch.manual_seed(M)
+    N, K = 1536, 1024
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.03).to(BF)
+    exp = x.float() @ w.float().t()
+    algos = torch.ops.rfq_amd.lt_heuristic(M, N, K, 6)
+    assert len(algos) >= 1
+    buf = torch.zeros(M, N + 64, device=gpu, dtype=BF)
+    for a in algos:
+        out = buf[:, :N]
+        out.fill_(float("nan"))
+        assert torch.ops.rfq_amd.lt_matmul(x, w, out, a) == 0
+        _close(out, exp, 2e-2, 1e-2, f"lt_matmul algo {a}")
+        assert torch.all(buf[:, N:] == 0)
+    assert torch.ops.rfq_amd.lt_matmul(x, w, buf[:, :N], 10 ** 6) != 0
+
+
 @pytest.mark.parametrize("M", [1, 3, 16])
 @pytest.mark.parametrize("cfg", [13, 15])
 def test_skinny_gemm_rope_kv(gpu, M, cfg):
@@ -343,16 +365,22 @@ def test_linear_m_split_plan(gpu):
     torch.manual_seed(11)
     w = (torch.randn(512, 1024, device=gpu) * 0.03).to(BF)
     plan, _ = tune_split({"t": [w]}, {"t": 1024}, quantum=128, reps=1)
-    q, table = plan[(512, 1024)]
-    assert q == 128 and len(table) == 9
+    q, table, algos = plan[(512, 1024)]
+    assert q == 128 and len(table) == 9 and len(algos) == 9
     forced = plan_splits([0.0] + [1.0] * 8 + [100.0], margin=1.0, launch_us=0.0)
-    ops.set_split_plan({(512, 1024): (128, forced)})
     try:
+        # forced multi-chunk split, each chunk on its bucket's measured algorithm
+        ops.set_split_plan({(512, 1024): (128, forced, algos + [-1])})
         M = 128 * 8 + 77
         rows = ops.split_chunks(M, 512, 1024)
         assert rows is not None and len(rows) > 1 and sum(rows) == M
         x = torch.randn(M, 1024, device=gpu, dtype=BF)
         out = ops.linear(x, w)
         _close(out, x.float() @ w.float().t(), 1e-2, 1e-2, "split linear")
+        # the measured plan itself, every M in the tuned range
+        ops.set_split_plan(plan)
+        for M in (65, 128, 300, 777, 1024):
+            xm = x[:M]
+            _close(ops.linear(xm, w), xm.float() @ w.float().t(), 1e-2, 1e-2, f"lt plan M={M}")
     finally:
         ops.set_split_plan({})
