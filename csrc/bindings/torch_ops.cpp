@@ -39,6 +39,8 @@ void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t
                            hipStream_t);
 void launch_sample_final(const float*, const int32_t*, int, int, int, int32_t*, hipStream_t);
 void launch_moe_topk(const bf16_t*, int64_t, int, int, int, float*, int32_t*, bool, hipStream_t);
+void launch_moe_route(const bf16_t*, int64_t, const bf16_t*, int, int, int, int, float*, int32_t*,
+                      bool, hipStream_t);
 void launch_moe_align(const int32_t*, int, int, int, int32_t*, int32_t*, int32_t*, int32_t*,
                       int32_t*, int, int, hipStream_t);
 void launch_moe_gather(const bf16_t*, int64_t, const int32_t*, int, int, int, bf16_t*, hipStream_t);
@@ -53,6 +55,10 @@ void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
 uint32_t car_read_error(const void*);
 void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
                        int, bf16_t*, int64_t, int, int, int, bool, bool, hipStream_t);
+void launch_moe_skinny_splitk(const bf16_t*, int64_t, const int32_t*, int, const int32_t*,
+                              const bf16_t*, int, float*, int64_t, int, int, int, int, hipStream_t);
+void launch_moe_combine_splitk(const float*, int, int64_t, const int32_t*, const float*, int, int,
+                               int, bf16_t*, int64_t, hipStream_t);
 }  // namespace rfq
 
 namespace {
@@ -324,6 +330,24 @@ void moe_topk(const Tensor& router_logits, int64_t topk, bool renorm, const Tens
                        weights.data_ptr<float>(), ids.data_ptr<int32_t>(), renorm, cur_stream());
 }
 
+// router logits (x . router^T) + softmax top-k in one launch, one workgroup per token
+void moe_route(const Tensor& x, const Tensor& router, int64_t topk, bool renorm,
+               const Tensor& weights, const Tensor& ids) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(router); CHECK_ROWMAJOR(x);
+  CHECK_I32(ids);
+  TORCH_CHECK(router.dim() == 2 && router.is_contiguous() && router.size(1) == x.size(1),
+              "moe_route: router must be contiguous [E, d]");
+  const int T = x.size(0), d = x.size(1), E = router.size(0);
+  TORCH_CHECK(E <= 16 && topk >= 1 && topk <= 8 && topk <= E && d % 8 == 0 &&
+                  x.stride(0) % 8 == 0,
+              "moe_route: E <= 16, topk <= 8, d % 8 == 0");
+  TORCH_CHECK(weights.scalar_type() == at::kFloat && weights.numel() >= (int64_t)T * topk &&
+                  ids.numel() >= (int64_t)T * topk,
+              "moe_route: outputs");
+  rfq::launch_moe_route(bp(x), x.stride(0), bp(router), T, d, E, (int)topk,
+                        weights.data_ptr<float>(), ids.data_ptr<int32_t>(), renorm, cur_stream());
+}
+
 // Sort (token, k) pairs by expert, pad each expert's segment to a multiple of
 // `block_m`.  Outputs: sorted_ids [max_padded] (token*k+slot, or -1 padding),
 // expert_of_block [max_blocks], expert_offsets [E+1], num_blocks [1].
@@ -344,6 +368,41 @@ void moe_skinny(const Tensor& x, const Tensor& sorted_ids, int64_t topk,
   rfq::launch_moe_skinny(bp(x), x.stride(0), sorted_ids.data_ptr<int32_t>(), (int)topk,
                          expert_offsets.data_ptr<int32_t>(), bp(w), K, bpm(out), out.stride(0), E,
                          n_out, (int)max_rows, gated, gather, cur_stream());
+}
+
+// w2 of the MoE latency path with split-K: yf [splits, rows, n_out] fp32 partials
+void moe_skinny_splitk(const Tensor& x, const Tensor& sorted_ids, int64_t topk,
+                       const Tensor& expert_offsets, const Tensor& w, const Tensor& yf,
+                       int64_t max_rows, int64_t splits) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_BF16(w); CHECK_I32(sorted_ids);
+  CHECK_I32(expert_offsets);
+  TORCH_CHECK(w.dim() == 3 && w.is_contiguous(), "moe_skinny_splitk: w must be [E, N, K]");
+  TORCH_CHECK(yf.scalar_type() == at::kFloat && yf.dim() == 3 && yf.is_contiguous(),
+              "moe_skinny_splitk: yf must be fp32 [splits, rows, N] contiguous");
+  TORCH_CHECK(splits == 2 || splits == 4, "moe_skinny_splitk: splits in {2, 4}");
+  const int E = w.size(0), K = w.size(2), n_out = w.size(1);
+  TORCH_CHECK(x.size(1) == K && K % 128 == 0 && n_out % 16 == 0, "moe_skinny_splitk: shapes");
+  TORCH_CHECK(yf.size(0) >= splits && yf.size(2) == n_out && yf.size(1) >= sorted_ids.numel() &&
+                  x.size(0) >= sorted_ids.numel() && x.stride(0) % 8 == 0,
+              "moe_skinny_splitk: rows / alignment");
+  TORCH_CHECK(expert_offsets.numel() >= E + 1, "moe_skinny_splitk: expert_offsets too small");
+  rfq::launch_moe_skinny_splitk(bp(x), x.stride(0), sorted_ids.data_ptr<int32_t>(), (int)topk,
+                                expert_offsets.data_ptr<int32_t>(), bp(w), K,
+                                yf.data_ptr<float>(), yf.stride(0), E, n_out, (int)max_rows,
+                                (int)splits, cur_stream());
+}
+
+void moe_combine_splitk(const Tensor& yf, int64_t splits, const Tensor& inv_pos,
+                        const Tensor& weights, int64_t topk, const Tensor& out) {
+  CHECK_DEV(yf); CHECK_I32(inv_pos); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(yf.scalar_type() == at::kFloat && yf.dim() == 3 && yf.is_contiguous() &&
+                  yf.size(0) >= splits && yf.size(2) == out.size(1) && out.size(1) % 8 == 0,
+              "moe_combine_splitk: yf must be fp32 [splits, rows, d]");
+  TORCH_CHECK(weights.scalar_type() == at::kFloat, "weights fp32");
+  const int T = out.size(0), d = out.size(1);
+  rfq::launch_moe_combine_splitk(yf.data_ptr<float>(), (int)splits, yf.stride(0),
+                                 inv_pos.data_ptr<int32_t>(), weights.data_ptr<float>(), T,
+                                 (int)topk, d, bpm(out), out.stride(0), cur_stream());
 }
 
 // ---- custom all-reduce (csrc/comm/custom_ar.hip)
@@ -489,12 +548,18 @@ TORCH_LIBRARY(rfq_amd, m) {
         "Tensor seeds, Tensor(a!) part_val, Tensor(b!) part_idx) -> ()");
   m.def("sample_final(Tensor part_val, Tensor part_idx, Tensor(a!) out) -> ()");
   m.def("moe_topk(Tensor router_logits, int topk, bool renorm, Tensor(a!) weights, Tensor(b!) ids) -> ()");
+  m.def("moe_route(Tensor x, Tensor router, int topk, bool renorm, Tensor(a!) weights, "
+        "Tensor(b!) ids) -> ()");
   m.def("moe_align(Tensor topk_ids, int E, int block_m, Tensor(a!) sorted_ids, Tensor(b!) inv_pos, "
         "Tensor(c!) expert_of_block, Tensor(d!) expert_offsets, Tensor(e!) num_blocks) -> ()");
   m.def("moe_gather(Tensor x, Tensor sorted_ids, int topk, Tensor(a!) out) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
         "Tensor num_blocks) -> ()");
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
+  m.def("moe_skinny_splitk(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
+        "Tensor(a!) yf, int max_rows, int splits) -> ()");
+  m.def("moe_combine_splitk(Tensor yf, int splits, Tensor inv_pos, Tensor weights, int topk, "
+        "Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
@@ -513,8 +578,11 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("sample_partial", &sample_partial);
   m.impl("sample_final", &sample_final);
   m.impl("moe_topk", &moe_topk);
+  m.impl("moe_route", &moe_route);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gather", &moe_gather);
   m.impl("moe_grouped_gemm", &moe_grouped_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("moe_skinny_splitk", &moe_skinny_splitk);
+  m.impl("moe_combine_splitk", &moe_combine_splitk);
 }

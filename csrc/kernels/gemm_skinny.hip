@@ -431,22 +431,31 @@ void launch_skinny_gemm_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
 //   GATED:  the tile computes the gate rows [n0, n0+16) and the matching up rows
 //           [up_off + n0, ...) of w13 together and writes silu(gate) * up — the
 //           w13 GEMM, SwiGLU and its [rows, 2F] intermediate in one pass.
-template <int MT, bool GATED, bool GATHER, int NW, int U>
+//   SPLIT > 1 (w2 only): the SPLIT workgroups of a tile each stream one K slice and
+//           write fp32 partials to Yf[slice][row][n] (slab stride `slab` floats);
+//           moe_combine_splitk sums the slices while it combines the top-k pairs.
+//           w2 has only 256 output tiles per expert against K = 14336, so without
+//           it one decode token's 2 experts keep too few bytes in flight per CU.
+template <int MT, bool GATED, bool GATHER, int NW, int U, int SPLIT = 1>
 __global__ __launch_bounds__(NW * 64) void moe_skinny_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const int32_t* __restrict__ sorted_ids, int topk,
     const int32_t* __restrict__ expert_offsets, const bf16_t* __restrict__ W,
     int64_t w_expert_stride, int K, int up_off, bf16_t* __restrict__ Y, int64_t ldy,
-    int tiles_per_expert) {
+    int tiles_per_expert, float* __restrict__ Yf = nullptr, int64_t slab = 0) {
   constexpr int NT = GATED ? 2 : 1;
+  static_assert(SPLIT == 1 || !GATED, "split-K is for the plain (w2) projection");
   __shared__ f32x4 red[NW][NT * MT][64];
-  const int e = blockIdx.x / tiles_per_expert, tile = blockIdx.x % tiles_per_expert;
+  const int per_e = tiles_per_expert * SPLIT;
+  const int e = blockIdx.x / per_e, rem = blockIdx.x % per_e;
+  const int tile = rem / SPLIT, slice = rem % SPLIT;
   const int r0 = expert_offsets[e], r1 = expert_offsets[e + 1];
   if (r0 >= r1) return;                              // expert not routed this step
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = tile * 16;
-  const int nks = K >> 7;
-  const int ks0 = wave * nks / NW, ks1 = (wave + 1) * nks / NW;
+  const int nks_all = K >> 7;
+  const int sl0 = slice * nks_all / SPLIT, nks = (slice + 1) * nks_all / SPLIT - sl0;
+  const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
   const bf16_t* we = W + (int64_t)e * w_expert_stride;
   const bf16_t* wp[NT];
   wp[0] = we + (int64_t)(n0 + r) * K + g * 8;
@@ -540,10 +549,14 @@ __global__ __launch_bounds__(NW * 64) void moe_skinny_kernel(
       }
       const int row = mb + t * 16 + r;
       if (row < r1) {
-        uint2 v;
-        v.x = pack_bf16x2(s[0], s[1]);
-        v.y = pack_bf16x2(s[2], s[3]);
-        *reinterpret_cast<uint2*>(Y + (int64_t)row * ldy + n0 + g * 4) = v;
+        if constexpr (SPLIT > 1) {
+          *reinterpret_cast<f32x4*>(Yf + slice * slab + (int64_t)row * ldy + n0 + g * 4) = s;
+        } else {
+          uint2 v;
+          v.x = pack_bf16x2(s[0], s[1]);
+          v.y = pack_bf16x2(s[2], s[3]);
+          *reinterpret_cast<uint2*>(Y + (int64_t)row * ldy + n0 + g * 4) = v;
+        }
       }
     }
     __syncthreads();                                   // red is reused by the next chunk
@@ -554,12 +567,51 @@ template <int MT, bool GATED, bool GATHER>
 static void moe_skinny_cfg(const bf16_t* X, int64_t ldx, const int32_t* sorted_ids, int topk,
                            const int32_t* expert_offsets, const bf16_t* W, int64_t wstride,
                            int K, int up_off, bf16_t* Y, int64_t ldy, int E, int n_out,
-                           hipStream_t s) {
+                           int max_rows, hipStream_t s) {
   constexpr int U = MT == 1 ? 4 : (MT == 2 ? 3 : 2);
   const int tiles = n_out / 16;
-  hipLaunchKernelGGL((moe_skinny_kernel<MT, GATED, GATHER, 4, U>), dim3(E * tiles), dim3(256), 0,
-                     s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, up_off, Y, ldy,
-                     tiles);
+  // Long-K, few-tile projections (w2: 4096 outputs x K = 14336) launch only 256
+  // workgroups per routed expert.  With at most 2 (token, expert) pairs (one decode
+  // token: 2 experts) 8 waves split K so each CU keeps twice the bytes in flight
+  // (tools/bench_moe_skinny.py, w2 at 2 experts: 83.2 -> 67.1 us); with more experts
+  // there are enough workgroups and 4 waves are faster (5 experts: 144 vs 157 us).
+  static const int nw_env = [] {
+    const char* v = getenv("RFQ_MOE_SKINNY_NW");
+    return v ? atoi(v) : 0;
+  }();
+  const bool wide = nw_env ? nw_env == 8 : (!GATED && K >= 8192 && max_rows <= 2);
+  if (wide)
+    hipLaunchKernelGGL((moe_skinny_kernel<MT, GATED, GATHER, 8, U>), dim3(E * tiles), dim3(512),
+                       0, s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, up_off, Y,
+                       ldy, tiles);
+  else
+    hipLaunchKernelGGL((moe_skinny_kernel<MT, GATED, GATHER, 4, U>), dim3(E * tiles), dim3(256),
+                       0, s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, up_off, Y,
+                       ldy, tiles);
+}
+
+// Split-K w2 (plain X, no gather): Yf [SPLIT][rows][n_out] fp32 partial slabs.
+void launch_moe_skinny_splitk(const bf16_t* X, int64_t ldx, const int32_t* sorted_ids, int topk,
+                              const int32_t* expert_offsets, const bf16_t* W, int K, float* Yf,
+                              int64_t slab, int E, int n_out, int max_rows, int splits,
+                              hipStream_t s) {
+  const int tiles = n_out / 16;
+  const int64_t wstride = (int64_t)n_out * K;
+#define SPK_CASE(mt, u)                                                                        \
+  if (splits == 4)                                                                             \
+    hipLaunchKernelGGL((moe_skinny_kernel<mt, false, false, 4, u, 4>), dim3(E * tiles * 4),     \
+                       dim3(256), 0, s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K,\
+                       0, nullptr, (int64_t)n_out, tiles, Yf, slab);                           \
+  else                                                                                         \
+    hipLaunchKernelGGL((moe_skinny_kernel<mt, false, false, 4, u, 2>), dim3(E * tiles * 2),     \
+                       dim3(256), 0, s, X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K,\
+                       0, nullptr, (int64_t)n_out, tiles, Yf, slab);
+  const int MT = max_rows <= 16 ? 1 : (max_rows <= 32 ? 2 : (max_rows <= 48 ? 3 : 4));
+  if (MT == 1) { SPK_CASE(1, 4) }
+  else if (MT == 2) { SPK_CASE(2, 3) }
+  else if (MT == 3) { SPK_CASE(3, 2) }
+  else { SPK_CASE(4, 2) }
+#undef SPK_CASE
 }
 
 // gated: W [E, 2*n_out, K] (gate | up), Y [rows, n_out] = silu(X W_g^T) * (X W_u^T)
@@ -574,16 +626,16 @@ void launch_moe_skinny(const bf16_t* X, int64_t ldx, const int32_t* sorted_ids, 
   case mt:                                                                                     \
     if (gated && gather)                                                                       \
       moe_skinny_cfg<mt, true, true>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K,  \
-                                     n_out, Y, ldy, E, n_out, s);                              \
+                                     n_out, Y, ldy, E, n_out, max_rows, s);                              \
     else if (gated)                                                                            \
       moe_skinny_cfg<mt, true, false>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, \
-                                      n_out, Y, ldy, E, n_out, s);                             \
+                                      n_out, Y, ldy, E, n_out, max_rows, s);                             \
     else if (gather)                                                                           \
       moe_skinny_cfg<mt, false, true>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride, K, \
-                                      0, Y, ldy, E, n_out, s);                                 \
+                                      0, Y, ldy, E, n_out, max_rows, s);                                 \
     else                                                                                       \
       moe_skinny_cfg<mt, false, false>(X, ldx, sorted_ids, topk, expert_offsets, W, wstride,   \
-                                       K, 0, Y, ldy, E, n_out, s);                             \
+                                       K, 0, Y, ldy, E, n_out, max_rows, s);                             \
     break;
   switch (MT) {
     MS_CASE(1)

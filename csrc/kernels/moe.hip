@@ -51,6 +51,89 @@ __global__ void moe_topk_kernel(const bf16_t* __restrict__ logits, int64_t strid
   }
 }
 
+// ------------------------------------------- fused router GEMV + top-k (small T)
+// Latency path (T <= 64 tokens): one workgroup per token computes the E router
+// logits (x . router_w^T, fp32 accumulate, rounded to bf16 like the hipBLASLt GEMM the
+// throughput path uses) and the softmax top-k in one launch, instead of a
+// 16x16-tile library GEMM plus moe_topk_kernel.
+constexpr int kRouteMaxE = 16;
+
+// EP: compile-time expert count (8 for Mixtral; 16 covers the rest, rows >= E are
+// read as row 0 and ignored) so every router/x load of a thread is issued before the
+// first FMA waits: one memory round trip instead of one per expert row.
+template <int EP>
+__global__ __launch_bounds__(256) void moe_route_kernel(
+    const bf16_t* __restrict__ x, int64_t x_stride, const bf16_t* __restrict__ router, int d,
+    int E, int k, float* __restrict__ w_out, int32_t* __restrict__ id_out, bool renorm) {
+  __shared__ float part[EP][4];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = d >> 3;
+  const s16x8* xr = reinterpret_cast<const s16x8*>(x + (int64_t)t * x_stride);
+  float acc[EP];
+#pragma unroll
+  for (int e = 0; e < EP; ++e) acc[e] = 0.f;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += 2 * blockDim.x) {
+    const int c1 = c0 + blockDim.x;
+    const bool has1 = c1 < nch;
+    s16x8 xv[2], wv[2][EP];
+    xv[0] = xr[c0];
+    xv[1] = xr[has1 ? c1 : c0];
+#pragma unroll
+    for (int e = 0; e < EP; ++e) {
+      const s16x8* rr = reinterpret_cast<const s16x8*>(router + (int64_t)(e < E ? e : 0) * d);
+      wv[0][e] = rr[c0];
+      wv[1][e] = rr[has1 ? c1 : c0];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !has1) break;
+      float xf[8];
+      unpack8(xv[h], xf);
+#pragma unroll
+      for (int e = 0; e < EP; ++e) {
+        float wf[8];
+        unpack8(wv[h][e], wf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[e] += xf[i] * wf[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EP; ++e) {
+    const float v = wave_sum(acc[e]);
+    if (lane == 0) part[e][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float l[EP];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    const float v = part[e][0] + part[e][1] + part[e][2] + part[e][3];
+    l[e] = bf2f(f2bf(v));                      // the bf16 logits of the GEMM path
+    mx = fmaxf(mx, l[e]);
+  }
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) den += __expf(l[e] - mx);
+  uint32_t taken = 0;
+  float sel_sum = 0.f, wsel[8];
+  int isel[8];
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((taken >> e) & 1u) && (best < 0 || l[e] > bv)) { bv = l[e]; best = e; }
+    taken |= 1u << best;
+    wsel[j] = __expf(bv - mx) / den;
+    isel[j] = best;
+    sel_sum += wsel[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    w_out[(int64_t)t * k + j] = renorm ? wsel[j] / sel_sum : wsel[j];
+    id_out[(int64_t)t * k + j] = isel[j];
+  }
+}
+
 // ------------------------------------------------------------ align (one block)
 // Counting sort of the T*k (token, slot) pairs by expert; each expert segment is
 // padded to a multiple of block_m with -1 entries.
@@ -351,6 +434,33 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
   }
 }
 
+// Split-K variant: y = sum over `splits` fp32 slabs (moe_skinny split-K w2 partials).
+__global__ __launch_bounds__(256) void moe_combine_splitk_kernel(
+    const float* __restrict__ yf, int splits, int64_t slab, const int32_t* __restrict__ inv_pos,
+    const float* __restrict__ wts, int T, int k, int d, bf16_t* __restrict__ out,
+    int64_t out_stride) {
+  const int cpr = d >> 3;
+  const int64_t total = (int64_t)T * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / cpr;
+    const int c = (int)(i - t * cpr);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = wts[t * k + j];
+      if (wj == 0.f) continue;        // pair routed to another rank's expert (EP)
+      const int p = inv_pos[t * k + j];
+      for (int sl = 0; sl < splits; ++sl) {
+        const float4* src = reinterpret_cast<const float4*>(yf + sl * slab + (int64_t)p * d) + 2 * c;
+        const float4 a = src[0], b = src[1];
+        acc[0] += wj * a.x; acc[1] += wj * a.y; acc[2] += wj * a.z; acc[3] += wj * a.w;
+        acc[4] += wj * b.x; acc[5] += wj * b.y; acc[6] += wj * b.z; acc[7] += wj * b.w;
+      }
+    }
+    reinterpret_cast<s16x8*>(out + t * out_stride)[c] = pack8(acc);
+  }
+}
+
 static inline int moe_stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
@@ -360,6 +470,15 @@ void launch_moe_topk(const bf16_t* logits, int64_t stride, int T, int E, int k, 
                      int32_t* ids, bool renorm, hipStream_t s) {
   if (T == 0) return;
   moe_topk_kernel<<<(T + 127) / 128, 128, 0, s>>>(logits, stride, T, E, k, w, ids, renorm);
+}
+
+void launch_moe_route(const bf16_t* x, int64_t x_stride, const bf16_t* router, int T, int d,
+                      int E, int k, float* w, int32_t* ids, bool renorm, hipStream_t s) {
+  if (T == 0) return;
+  if (E <= 8)
+    moe_route_kernel<8><<<T, 256, 0, s>>>(x, x_stride, router, d, E, k, w, ids, renorm);
+  else
+    moe_route_kernel<kRouteMaxE><<<T, 256, 0, s>>>(x, x_stride, router, d, E, k, w, ids, renorm);
 }
 
 void launch_moe_align(const int32_t* ids, int n, int E, int block_m, int32_t* sorted_ids,
@@ -393,6 +512,14 @@ void launch_moe_grouped_gemm(const bf16_t* x, const bf16_t* w, bf16_t* out,
   else
     moe_grouped_gemm_kernel<<<max_blocks * (N / kBN), 256, 0, s>>>(x, w, out, expert_of_block,
                                                                     num_blocks, N, K, E);
+}
+
+void launch_moe_combine_splitk(const float* yf, int splits, int64_t slab, const int32_t* inv_pos,
+                               const float* w, int T, int k, int d, bf16_t* out,
+                               int64_t out_stride, hipStream_t s) {
+  if (T == 0) return;
+  moe_combine_splitk_kernel<<<moe_stream_grid((int64_t)T * (d >> 3)), 256, 0, s>>>(
+      yf, splits, slab, inv_pos, w, T, k, d, out, out_stride);
 }
 
 void launch_moe_combine(const bf16_t* y, const int32_t* inv_pos, const float* w, int T, int k,

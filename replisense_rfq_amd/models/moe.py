@@ -10,6 +10,8 @@ is used instead.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
@@ -20,6 +22,8 @@ from ..ops import reference as ref
 BLOCK_M = 128
 BLOCK_S = 16            # expert segment padding on the small-batch path
 SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
+# K slices of the latency-path w2 (gemm_skinny.hip moe_skinny_kernel SPLIT): 0/1 = off
+W2_SPLITS = int(os.environ.get("RFQ_MOE_W2_SPLITS", "2"))
 
 
 @dataclass
@@ -38,6 +42,7 @@ class MoEBuffers:
     h13: torch.Tensor
     act: torch.Tensor
     y: torch.Tensor
+    yf: torch.Tensor | None = None     # [W2_SPLITS, rows, d] fp32 split-K w2 partials
 
     @classmethod
     def allocate(cls, max_tokens: int, topk: int, E: int, d: int, F: int, device,
@@ -60,6 +65,9 @@ class MoEBuffers:
             h13=torch.empty(cap, 2 * F, dtype=dtype, device=device),
             act=torch.empty(cap, F, dtype=dtype, device=device),
             y=torch.empty(cap, d, dtype=dtype, device=device),
+            yf=(torch.empty(W2_SPLITS, n + (E + 2) * BLOCK_S, d, dtype=torch.float32,
+                            device=device)
+                if max_tokens <= SKINNY_MAX_TOKENS and W2_SPLITS > 1 else None),
         )
 
 
@@ -73,9 +81,8 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     kernel computes and get combine weight 0; the TP all-reduce after the MLP sums
     the ranks' partial outputs (each expert runs on exactly one rank)."""
     T = x.shape[0]
-    logits = x @ router_w.t()
     if not x.is_cuda:
-        return ref.moe_forward(x, w13, w2, logits, topk, expert_offset)
+        return ref.moe_forward(x, w13, w2, x @ router_w.t(), topk, expert_offset)
     E = w13.shape[0]
     ep = E != router_w.shape[0]
     assert bufs is not None and T <= bufs.max_tokens
@@ -87,9 +94,9 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     if ep:
         E = E + 1                  # + the dummy segment for remote experts
     if T <= SKINNY_MAX_TOKENS:
-        # decode / short-extend steps: stream only the routed experts' weights,
-        # gather rows on the fly, SwiGLU fused into the w13 pass
-        ops.moe_topk(logits, topk, True, w, ids)
+        # decode / short-extend steps: router GEMV + top-k in one kernel, stream only
+        # the routed experts' weights, gather rows on the fly, SwiGLU fused into w13
+        ops.moe_route(x, router_w, topk, True, w, ids)
         if ep:
             _localize(ids, w, expert_offset, E - 1)
         cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
@@ -101,10 +108,17 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         act = bufs.act[:cap]
         y = bufs.y[:cap]
         ops.moe_skinny(x, sorted_ids, topk, bufs.expert_offsets, w13, act, True, True, n)
-        ops.moe_skinny(act, sorted_ids, topk, bufs.expert_offsets, w2, y, False, False, n)
         assert act.shape[1] == F
+        if bufs.yf is not None:
+            # split-K w2: fp32 partial slabs, summed inside the top-k combine
+            ops.moe_skinny_splitk(act, sorted_ids, topk, bufs.expert_offsets, w2, bufs.yf, n,
+                                  W2_SPLITS)
+            ops.moe_combine_splitk(bufs.yf, W2_SPLITS, bufs.inv_pos[:n], w, topk, out)
+            return out
+        ops.moe_skinny(act, sorted_ids, topk, bufs.expert_offsets, w2, y, False, False, n)
         ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
         return out
+    logits = x @ router_w.t()
     if not torch.cuda.is_current_stream_capturing():
         return _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset, E)
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M

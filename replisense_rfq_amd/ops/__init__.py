@@ -19,7 +19,7 @@ __all__ = [
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
     "set_norm_plan", "norm_plan", "norm_counter", "linear_add_norm", "set_rope_plan",
-    "rope_plan", "qkv_rope",
+    "rope_plan", "qkv_rope", "moe_route",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -382,10 +382,28 @@ def moe_grouped_gemm(x, w, out, expert_of_block, num_blocks):
     _native.ops().moe_grouped_gemm(x, w, out, expert_of_block, num_blocks)
 
 
+def moe_route(x, router_w, topk, renorm, weights, ids):
+    """Router logits (x . router_w^T, bf16-rounded) + softmax top-k in one kernel (GPU,
+    small T); CPU: the same two steps in torch."""
+    if _gpu(x):
+        _native.ops().moe_route(x, router_w, topk, renorm, weights, ids)
+    else:
+        moe_topk(x @ router_w.t(), topk, renorm, weights, ids)
+
+
 def moe_skinny(x, sorted_ids, topk, expert_offsets, w, out, gated, gather, max_rows):
     """Per-expert weight-streaming GEMM (small token counts); see gemm_skinny.hip."""
     _native.ops().moe_skinny(x, sorted_ids, topk, expert_offsets, w, out, gated, gather,
                              max_rows)
+
+
+def moe_skinny_splitk(x, sorted_ids, topk, expert_offsets, w, yf, max_rows, splits):
+    """Latency-path w2 with split-K: fp32 partial slabs yf[splits, rows, N]."""
+    _native.ops().moe_skinny_splitk(x, sorted_ids, topk, expert_offsets, w, yf, max_rows, splits)
+
+
+def moe_combine_splitk(yf, splits, inv_pos, weights, topk, out):
+    _native.ops().moe_combine_splitk(yf, splits, inv_pos, weights, topk, out)
 
 
 def moe_combine(y, inv_pos, weights, topk, out):

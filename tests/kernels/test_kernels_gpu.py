@@ -281,6 +281,52 @@ def test_skinny_gemm_fused_add_norm(gpu, M, gated, cfg):
     assert int(counter[0]) == 0, "ticket counter not reset"
 
 
+@pytest.mark.parametrize("splits", [0, 2, 4])
+@pytest.mark.parametrize("T", [1, 3, 37])
+def test_moe_latency_path_w2_splitk(gpu, T, splits, monkeypatch):
+    """Latency-path MoE (route -> align -> gated w13 -> w2 -> combine) with the w2
+    split into 0/2/4 K slices (fp32 partials summed in the combine) == the oracle."""
+    from replisense_rfq_amd.models import moe as M
+
+    monkeypatch.setattr(M, "W2_SPLITS", splits)
+    torch.manual_seed(70 + T)
+    d, F, E, k = 512, 1024, 8, 2
+    x = (torch.randn(T, d, device=gpu) * 0.5).to(BF)
+    router = (torch.randn(E, d, device=gpu) * 0.05).to(BF)
+    w13 = (torch.randn(E, 2 * F, d, device=gpu) / math.sqrt(d)).to(BF)
+    w2 = (torch.randn(E, d, F, device=gpu) / math.sqrt(F)).to(BF)
+    bufs = M.MoEBuffers.allocate(T, k, E, d, F, gpu)
+    assert (bufs.yf is not None) == (splits > 1)
+    out = M.moe_mlp(x, router, w13, w2, k, bufs)
+    logits = (x @ router.t()).cpu()
+    exp = ref.moe_forward(x.cpu(), w13.cpu(), w2.cpu(), logits, k)
+    _close(out, exp, 3e-2, 2e-2, f"moe latency path T={T} splits={splits}")
+
+
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (5, 8, 2), (64, 8, 2), (3, 16, 4)])
+def test_moe_route_matches_gemm_topk(gpu, T, E, k):
+    """Fused router GEMV + top-k == bf16 router GEMM followed by the top-k oracle
+    (same experts; weights within bf16-logit rounding)."""
+    torch.manual_seed(T * 7 + E)
+    d = 4096
+    x = torch.randn(T, d, device=gpu, dtype=BF)
+    router = (torch.randn(E, d, device=gpu) * 0.05).to(BF)
+    w = torch.empty(T, k, device=gpu)
+    ids = torch.empty(T, k, device=gpu, dtype=torch.int32)
+    ops.moe_route(x, router, k, True, w, ids)
+    logits = (x.float() @ router.float().t()).to(BF)
+    w_e, i_e = ref.moe_topk(logits.cpu(), k, True)
+    # rows whose k-th and (k+1)-th logits are within summation-order rounding may
+    # legitimately pick either expert: compare the others
+    srt = logits.float().cpu().sort(1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]) > 0.1 if k < E else torch.ones(T, dtype=torch.bool)
+    assert clear.any()
+    got, exp = ids.cpu().long().sort(1).values, i_e.long().sort(1).values
+    assert torch.equal(got[clear], exp[clear])
+    _close(w.cpu()[clear].sort(1).values, w_e.float()[clear].sort(1).values, 2e-2, 0,
+           "moe_route weights")
+
+
 @pytest.mark.parametrize("M", [200, 512, 1000])
 def test_lt_matmul_every_heuristic_algo(gpu, M):
     """Direct hipBLASLt calls (gemm_lt.cpp) with each of the heuristic's top algorithms
