@@ -15,8 +15,8 @@ typedef uint16_t bf16_t;
 void launch_rms_norm(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
 void launch_fused_add_rms_norm(const bf16_t*, int64_t, bf16_t*, int64_t, const bf16_t*, bf16_t*,
                                int64_t, int, int, float, hipStream_t);
-void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
-                        hipStream_t);
+void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, int64_t, bf16_t*, int64_t,
+                        int, int, hipStream_t);
 void launch_skinny_gemm_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
                              unsigned*, hipStream_t);
@@ -102,7 +102,8 @@ void fused_add_rms_norm(const Tensor& x, const Tensor& residual, const Tensor& w
 void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm: w must be contiguous [N, K]");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0,
+              "skinny_gemm: w must be row-major [N, K] with 16-byte aligned rows");
   const bool gated = cfg & 16;          // x = [M, 2K] gate|up, B operand silu(gate)*up
   const int M = x.size(0), K = gated ? x.size(1) / 2 : x.size(1), N = w.size(0);
   const int nt = (cfg & 1) ? 2 : 1;  // bits 2-3 select the load variant
@@ -112,8 +113,9 @@ void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cf
               "skinny_gemm: K % 128 and N % tile required");
   TORCH_CHECK(out.size(0) == M && out.size(1) == N, "skinny_gemm: out shape");
   TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "skinny_gemm: alignment");
-  rfq::launch_skinny_gemm(bp(x), x.stride(0), bp(w), N, K, bpm(out), out.stride(0), M, (int)cfg,
-                          cur_stream());
+  TORCH_CHECK(w.stride(0) >= K, "skinny_gemm: w row stride < K");
+  rfq::launch_skinny_gemm(bp(x), x.stride(0), bp(w), N, K, w.stride(0), bpm(out), out.stride(0), M,
+                          (int)cfg, cur_stream());
 }
 
 // y = x . w^T (skinny, M <= 16), then residual <- y + residual and

@@ -145,7 +145,7 @@ struct RopeEpi {
 template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false,
           bool ROPE = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
-    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
+    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K, int64_t wstr,
     bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep, RopeEpi re = RopeEpi{}) {
   static_assert(!ROPE || (MT == 1 && NT == 2 && !NORM && !GX), "RoPE epilogue: MT=1, NT=2");
   __shared__ f32x4 red[NW][NT * MT][64];
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   const bf16_t* wp[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a)
-    wp[a] = W + (int64_t)(n0 + a * ASTRIDE + r) * K + g * (CMAP ? 8 : 32);
+    wp[a] = W + (int64_t)(n0 + a * ASTRIDE + r) * wstr + g * (CMAP ? 8 : 32);
   constexpr int JS = CMAP ? 32 : 8;                 // element stride between MFMA chunks
   const bf16_t* xp[MT];
   bool xv[MT];
@@ -329,29 +329,29 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 }
 
 template <int MT, int NT, int NW, int U>
-static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
-                       int64_t ldy, int M, int variant, bool norm, const NormEpi& ep,
+static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, int64_t wstr,
+                       bf16_t* Y, int64_t ldy, int M, int variant, bool norm, const NormEpi& ep,
                        hipStream_t s) {
   dim3 grid(N / (16 * NT));
   if constexpr (MT == 1) {  // fused add + RMSNorm epilogue (M <= 16): contiguous-k, plain loads
     if (norm) {
       if (variant >= 4)
         hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, true, true>), grid,
-                           dim3(NW * 64), 0, s, X, ldx, W, K, Y, ldy, M, ep);
+                           dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
       else
         hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, false, true>), grid,
-                           dim3(NW * 64), 0, s, X, ldx, W, K, Y, ldy, M, ep);
+                           dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
       return;
     }
   }
   if (variant >= 4) {   // gated X (silu(gate) * up), contiguous-k, plain loads
     hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, true, false, true>), grid, dim3(NW * 64),
-                       0, s, X, ldx, W, K, Y, ldy, M, ep);
+                       0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
     return;
   }
 #define SK_LAUNCH(cm, nt)                                                                   \
   hipLaunchKernelGGL((skinny_gemm_kernel<MT, NT, NW, U, cm, nt>), grid, dim3(NW * 64), 0, s, \
-                     X, ldx, W, K, Y, ldy, M, ep)
+                     X, ldx, W, K, wstr, Y, ldy, M, ep)
   switch (variant) {
     case 0: SK_LAUNCH(false, true); break;
     case 1: SK_LAUNCH(true, true); break;
@@ -365,17 +365,17 @@ static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int
 // [3:2] variant (bit2 contiguous k-map, bit3 plain loads instead of non-temporal),
 // bit 4: gated X (x is [M, 2K] gate|up; B operand = silu(gate) * up).
 static void skinny_dispatch(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
-                            bf16_t* Y, int64_t ldy, int M, int cfg, bool norm, const NormEpi& ep,
-                            hipStream_t s) {
+                            int64_t wstr, bf16_t* Y, int64_t ldy, int M, int cfg, bool norm,
+                            const NormEpi& ep, hipStream_t s) {
   const int MT = (M + 15) / 16;
   const int v = (cfg & 16) ? 4 : ((cfg >> 2) & 3);
 #define SK_CASE(mt, u1, u2)                                                                    \
   case mt:                                                                                     \
     switch (cfg & 3) {                                                                         \
-      case 0: launch_cfg<mt, 1, 4, u1>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
-      case 1: launch_cfg<mt, 2, 4, u2>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
-      case 2: launch_cfg<mt, 1, 8, u1>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;     \
-      default: launch_cfg<mt, 2, 8, u2>(X, ldx, W, N, K, Y, ldy, M, v, norm, ep, s); break;    \
+      case 0: launch_cfg<mt, 1, 4, u1>(X, ldx, W, N, K, wstr, Y, ldy, M, v, norm, ep, s); break;     \
+      case 1: launch_cfg<mt, 2, 4, u2>(X, ldx, W, N, K, wstr, Y, ldy, M, v, norm, ep, s); break;     \
+      case 2: launch_cfg<mt, 1, 8, u1>(X, ldx, W, N, K, wstr, Y, ldy, M, v, norm, ep, s); break;     \
+      default: launch_cfg<mt, 2, 8, u2>(X, ldx, W, N, K, wstr, Y, ldy, M, v, norm, ep, s); break;    \
     }                                                                                          \
     break;
   switch (MT) {
@@ -387,9 +387,9 @@ static void skinny_dispatch(const bf16_t* X, int64_t ldx, const bf16_t* W, int N
 #undef SK_CASE
 }
 
-void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
-                        int64_t ldy, int M, int cfg, hipStream_t s) {
-  skinny_dispatch(X, ldx, W, N, K, Y, ldy, M, cfg, false, NormEpi{}, s);
+void launch_skinny_gemm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, int64_t wstr,
+                        bf16_t* Y, int64_t ldy, int M, int cfg, hipStream_t s) {
+  skinny_dispatch(X, ldx, W, N, K, wstr, Y, ldy, M, cfg, false, NormEpi{}, s);
 }
 
 // Fused QKV projection + RoPE + KV append (M <= 16, N = (Hq + 2 Hkv) * 128; cfg bit 0
@@ -399,13 +399,14 @@ void launch_skinny_gemm_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
                              const float* cos_sin, const int32_t* slots, bf16_t* k_cache,
                              bf16_t* v_cache, int Hq, int Hkv, int BS, hipStream_t s) {
   const RopeEpi re{positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, BS};
+  const int64_t wstr = K;
   const dim3 grid(N / 32);
   if (cfg & 2)
     hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 8, 2, true, false, false, false, true>), grid,
-                       dim3(512), 0, s, X, ldx, W, K, Y, ldy, M, NormEpi{}, re);
+                       dim3(512), 0, s, X, ldx, W, K, wstr, Y, ldy, M, NormEpi{}, re);
   else
     hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 4, 2, true, false, false, false, true>), grid,
-                       dim3(256), 0, s, X, ldx, W, K, Y, ldy, M, NormEpi{}, re);
+                       dim3(256), 0, s, X, ldx, W, K, wstr, Y, ldy, M, NormEpi{}, re);
 }
 
 // Y = X W^T, then residual <- Y + residual, out <- rmsnorm(residual) * norm_w (M <= 16,
@@ -415,7 +416,7 @@ void launch_skinny_gemm_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
                              int64_t res_stride, const bf16_t* norm_w, bf16_t* out,
                              int64_t out_stride, float eps, unsigned* counter, hipStream_t s) {
   const NormEpi ep{residual, res_stride, norm_w, out, out_stride, eps, counter};
-  skinny_dispatch(X, ldx, W, N, K, Y, ldy, M, cfg, true, ep, s);
+  skinny_dispatch(X, ldx, W, N, K, (int64_t)K, Y, ldy, M, cfg, true, ep, s);
 }
 
 // ---------------------------------------------------------------------------
