@@ -19,7 +19,7 @@ void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int, int, int64_t
                         int, int, hipStream_t);
 void launch_skinny_gemm_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
-                             unsigned*, hipStream_t);
+                             unsigned*, float*, hipStream_t);
 void launch_skinny_gemm_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*,
                              int, int, int, hipStream_t);
@@ -124,7 +124,7 @@ void skinny_gemm(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cf
 // owned by the stream (the kernel leaves it at zero).
 void skinny_gemm_norm(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& residual,
                       const Tensor& norm_w, double eps, const Tensor& out, const Tensor& counter,
-                      int64_t cfg) {
+                      const Tensor& partials, int64_t cfg) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_BF16(residual);
   CHECK_BF16(norm_w); CHECK_BF16(out); CHECK_I32(counter);
   CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(y); CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
@@ -146,10 +146,14 @@ void skinny_gemm_norm(const Tensor& x, const Tensor& w, const Tensor& y, const T
                   out.stride(0) % 8 == 0,
               "skinny_gemm_norm: alignment");
   TORCH_CHECK(counter.is_cuda() && counter.numel() >= 1, "skinny_gemm_norm: counter");
+  TORCH_CHECK(!(cfg & 64) || (partials.is_cuda() && partials.scalar_type() == at::kFloat &&
+                              partials.numel() >= 2 * (int64_t)M * N),
+              "skinny_gemm_norm: split-K needs an fp32 partials workspace of 2*M*N");
   rfq::launch_skinny_gemm_norm(bp(x), x.stride(0), bp(w), N, K, bpm(y), y.stride(0), M, (int)cfg,
                                bpm(residual), residual.stride(0), bp(norm_w), bpm(out),
                                out.stride(0), (float)eps,
-                               reinterpret_cast<unsigned*>(counter.data_ptr()), cur_stream());
+                               reinterpret_cast<unsigned*>(counter.data_ptr()),
+                               (cfg & 64) ? partials.data_ptr<float>() : nullptr, cur_stream());
 }
 
 // qkv = x . w^T (skinny, M <= 16) with NeoX RoPE on q/k and the paged KV append in the
@@ -521,7 +525,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("silu_mul(Tensor gate_up, Tensor(a!) out) -> ()");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
   m.def("skinny_gemm_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
-        "float eps, Tensor(c!) out, Tensor(d!) counter, int cfg) -> ()");
+        "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) partials, int cfg) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "

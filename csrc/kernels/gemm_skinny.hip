@@ -73,11 +73,13 @@ struct NormEpi {
   int64_t out_stride;
   float eps;
   unsigned* counter;
+  float* partials;    // split-K (KS > 1): fp32 partial slabs [KS][M][N], slab stride pslab
+  int64_t pslab;
 };
 
 constexpr int kNormMaxChunks = 4;       // hidden <= 8 * threads * 4 (8192 at 256 threads)
 
-template <int NTH>
+template <int NTH, int KS = 1>
 __device__ __forceinline__ void last_block_add_norm(const bf16_t* Y, int64_t ldy, int N, int M,
                                                     const NormEpi& ep, float* scratch) {
   const int nchunk = N >> 3;
@@ -93,13 +95,32 @@ __device__ __forceinline__ void last_block_add_norm(const bf16_t* Y, int64_t ldy
       const int c = threadIdx.x + k * NTH;
       if (c < nchunk) {
         float a[8], b[8];
-        const gu64* yq = (const gu64*)(yr + c);
-        const unsigned long long y0 = __hip_atomic_load(yq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long y1 = __hip_atomic_load(yq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (KS == 1) {
+          const gu64* yq = (const gu64*)(yr + c);
+          const unsigned long long y0 = __hip_atomic_load(yq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long y1 = __hip_atomic_load(yq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          a[i] = bf2f((bf16_t)(y0 >> (16 * i)));
-          a[4 + i] = bf2f((bf16_t)(y1 >> (16 * i)));
+          for (int i = 0; i < 4; ++i) {
+            a[i] = bf2f((bf16_t)(y0 >> (16 * i)));
+            a[4 + i] = bf2f((bf16_t)(y1 >> (16 * i)));
+          }
+        } else {
+          // sum the K slices' fp32 partials (sc1 loads), round like the GEMM output
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = 0.f;
+#pragma unroll
+          for (int sl = 0; sl < KS; ++sl) {
+            const gu64* pq = (const gu64*)(ep.partials + sl * ep.pslab + (int64_t)m * N + c * 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const unsigned long long u =
+                  __hip_atomic_load(pq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              a[2 * q] += __uint_as_float((uint32_t)u);
+              a[2 * q + 1] += __uint_as_float((uint32_t)(u >> 32));
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = bf2f(f2bf(a[i]));
         }
         unpack8(rr[c], b);
 #pragma unroll
@@ -142,20 +163,26 @@ struct RopeEpi {
   int Hq, Hkv, BS;
 };
 
+// KS > 1 (NORM only): the KS workgroups of an output tile each stream one K slice and
+// publish fp32 partials; the last workgroup sums them before the add + RMSNorm.  For
+// N = 4096 projections (o, down: 256 tiles) this doubles the workgroups in flight.
 template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false,
-          bool ROPE = false>
+          bool ROPE = false, int KS = 1>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K, int64_t wstr,
     bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep, RopeEpi re = RopeEpi{}) {
   static_assert(!ROPE || (MT == 1 && NT == 2 && !NORM && !GX), "RoPE epilogue: MT=1, NT=2");
+  static_assert(KS == 1 || (NORM && MT == 1), "split-K only with the norm epilogue");
   __shared__ f32x4 red[NW][NT * MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   // ROPE: block b owns head b/4, rotary pair block b%4 (features n0 and n0 + 64)
-  const int n0 = ROPE ? (blockIdx.x >> 2) * 128 + (blockIdx.x & 3) * 16 : blockIdx.x * (16 * NT);
+  const int bt = KS > 1 ? blockIdx.x / KS : blockIdx.x, slice = KS > 1 ? blockIdx.x % KS : 0;
+  const int n0 = ROPE ? (bt >> 2) * 128 + (bt & 3) * 16 : bt * (16 * NT);
   constexpr int ASTRIDE = ROPE ? 64 : 16;
-  const int nks = K >> 7;
-  const int ks0 = wave * nks / NW, ks1 = (wave + 1) * nks / NW;
+  const int nks_all = K >> 7;
+  const int sl0 = slice * nks_all / KS, nks = (slice + 1) * nks_all / KS - sl0;
+  const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
 
   const bf16_t* wp[NT];
 #pragma unroll
@@ -293,7 +320,16 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 #pragma unroll
     for (int w2 = 1; w2 < NW; ++w2) s += red[w2][tile][lane];
     const int m = t * 16 + r;
-    if (m < M) {
+    if (KS > 1 && m < M) {   // fp32 partial of this K slice, write-through (sc1)
+      const int Nn = (gridDim.x / KS) * 16 * NT;
+      gu64* pq = (gu64*)(ep.partials + slice * ep.pslab + (int64_t)m * Nn + n0 + a * 16 + g * 4);
+      __hip_atomic_store(pq, (unsigned long long)__float_as_uint(s[0]) |
+                                 ((unsigned long long)__float_as_uint(s[1]) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pq + 1, (unsigned long long)__float_as_uint(s[2]) |
+                                     ((unsigned long long)__float_as_uint(s[3]) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (m < M) {
       uint2 v;
       v.x = pack_bf16x2(s[0], s[1]);
       v.y = pack_bf16x2(s[2], s[3]);
@@ -324,7 +360,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (threadIdx.x == 0)
       __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_block_add_norm<NW * 64>(Y, ldy, gridDim.x * 16 * NT, M, ep, nscratch);
+    last_block_add_norm<NW * 64, KS>(Y, ldy, (gridDim.x / KS) * 16 * NT, M, ep, nscratch);
   }
 }
 
@@ -335,9 +371,16 @@ static void launch_cfg(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int
   dim3 grid(N / (16 * NT));
   if constexpr (MT == 1) {  // fused add + RMSNorm epilogue (M <= 16): contiguous-k, plain loads
     if (norm) {
-      if (variant >= 4)
+      const dim3 g2(grid.x * 2);
+      if (variant >= 4 && ep.partials)
+        hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, true, true, false, 2>),
+                           g2, dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
+      else if (variant >= 4)
         hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, true, true>), grid,
                            dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
+      else if (ep.partials)
+        hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, false, true, false, 2>),
+                           g2, dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
       else
         hipLaunchKernelGGL((skinny_gemm_kernel<1, NT, NW, U, true, false, false, true>), grid,
                            dim3(NW * 64), 0, s, X, ldx, W, K, wstr, Y, ldy, M, ep);
@@ -411,11 +454,15 @@ void launch_skinny_gemm_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
 
 // Y = X W^T, then residual <- Y + residual, out <- rmsnorm(residual) * norm_w (M <= 16,
 // N <= 8192; counter: one zero-initialised uint32 per stream, left at zero).
+// cfg bit 6 (64): split K in two slices per tile (partials: fp32 [2][M][N] workspace).
 void launch_skinny_gemm_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
                              bf16_t* Y, int64_t ldy, int M, int cfg, bf16_t* residual,
                              int64_t res_stride, const bf16_t* norm_w, bf16_t* out,
-                             int64_t out_stride, float eps, unsigned* counter, hipStream_t s) {
-  const NormEpi ep{residual, res_stride, norm_w, out, out_stride, eps, counter};
+                             int64_t out_stride, float eps, unsigned* counter, float* partials,
+                             hipStream_t s) {
+  const NormEpi ep{residual,          res_stride, norm_w, out, out_stride, eps, counter,
+                   (cfg & 64) ? partials : nullptr, (int64_t)M * N};
+  cfg &= 63;
   skinny_dispatch(X, ldx, W, N, K, (int64_t)K, Y, ldy, M, cfg, true, ep, s);
 }
 

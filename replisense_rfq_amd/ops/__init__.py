@@ -18,7 +18,8 @@ __all__ = [
     "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
-    "set_norm_plan", "norm_plan", "norm_counter", "linear_add_norm", "set_rope_plan",
+    "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
+    "set_rope_plan",
     "rope_plan", "qkv_rope", "moe_route",
 ]
 
@@ -112,11 +113,22 @@ def norm_counter(device) -> torch.Tensor:
     """The zero-initialised ticket counter of the fused-norm GEMM (one per device; the
     kernels of a stream run in order and each leaves it at zero).  Allocated before
     any graph capture (ops.autotune) so captured graphs bake in a stable pointer."""
+    return _norm_ws(device)[0]
+
+
+def norm_partials(device) -> torch.Tensor:
+    """fp32 workspace for the split-K fused-norm variant: 2 K slices x 16 rows x 8192."""
+    return _norm_ws(device)[1]
+
+
+def _norm_ws(device):
     d = torch.device(device)
-    c = _NORM_COUNTERS.get(d)
-    if c is None:
-        c = _NORM_COUNTERS[d] = torch.zeros(64, dtype=torch.int32, device=d)
-    return c
+    ws = _NORM_COUNTERS.get(d)
+    if ws is None:
+        ws = _NORM_COUNTERS[d] = (torch.zeros(64, dtype=torch.int32, device=d),
+                                  torch.empty(2 * NORM_FUSE_MAX_M * 8192, dtype=torch.float32,
+                                              device=d))
+    return ws
 
 
 def norm_plan(M: int, N: int, K: int, gated: bool) -> int:
@@ -142,7 +154,7 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
         return False
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     _native.ops().skinny_gemm_norm(x, w, y, residual, norm_w, eps, out,
-                                   norm_counter(x.device), cfg)
+                                   norm_counter(x.device), norm_partials(x.device), cfg)
     return True
 
 

@@ -123,7 +123,7 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
     """o / down projection followed by the residual-add RMSNorm: the planned GEMM path
     (linear or silu_linear) + fused_add_rms_norm vs the skinny kernel that runs the
     norm in its last workgroup (one launch instead of two)."""
-    from . import NORM_FUSE_MAX_M, fused_add_rms_norm, linear, norm_counter
+    from . import NORM_FUSE_MAX_M, fused_add_rms_norm, linear, norm_counter, norm_partials
 
     ops = _native.ops()
     N, K = ws[0].shape
@@ -131,7 +131,7 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
     if K % 128 or N % 16 or N % 8 or N > 8192:
         return plan, report
     dev, dt = ws[0].device, ws[0].dtype
-    counter = norm_counter(dev)
+    counter, partials = norm_counter(dev), norm_partials(dev)
     for M in ms:
         if M > NORM_FUSE_MAX_M:
             continue
@@ -146,11 +146,12 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
 
         t_ref = _time(ref, ws, reps)
         best, t_best = -1, t_ref * margin
-        for c in ((16, 17, 18, 19) if gated else CANDIDATES):
+        base = (16, 17, 18, 19) if gated else CANDIDATES
+        for c in base + tuple(b | 64 for b in base):       # | 64: two K slices per tile
             if c & 1 and N % 32:
                 continue
             t = _time(lambda w, c=c: ops.skinny_gemm_norm(x, w, y, res, norm_w, eps, out,
-                                                          counter, c), ws, reps)
+                                                          counter, partials, c), ws, reps)
             if t < t_best:
                 best, t_best = c, t
         if best >= 0:
