@@ -31,6 +31,11 @@ void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, co
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
                         float, int, int, hipStream_t);
+void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16_t*,
+                               const int32_t*, int, const int32_t*, const int32_t*,
+                               const int32_t*, int, const int32_t*, const int32_t*, int, int,
+                               bf16_t*, int64_t, int32_t*, float*, float*, int, int, float, int,
+                               bool, hipStream_t);
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                          const int32_t*, int, bf16_t*, int64_t, int, int, float, hipStream_t);
@@ -265,6 +270,44 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
                           (float)scale, num_splits, tiles_per_item, cur_stream());
+}
+
+// Shared-prefix (cascade) decode attention, num_splits == 1; see attn_decode.hip.
+// ws_i32 >= 2 + nseq + rows int32; pre_o >= rows*Hq*128, pre_ml >= rows*Hq*2 fp32.
+void attn_decode_shared(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                        const Tensor& block_tables, const Tensor& seq_q_start,
+                        const Tensor& seq_q_len, const Tensor& seq_kv_len, const Tensor& work_seq,
+                        const Tensor& work_ct, const Tensor& out, const Tensor& ws_i32,
+                        const Tensor& pre_o, const Tensor& pre_ml, int64_t Hq, int64_t Hkv,
+                        double scale, int64_t tiles_per_item, bool run_meta) {
+  CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode_shared: tiles_per_item");
+  CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
+  CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
+  CHECK_I32(work_seq); CHECK_I32(work_ct); CHECK_I32(ws_i32);
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 32 && k_cache.size(3) == 128 &&
+                  k_cache.size(1) == Hkv,
+              "attn_decode_shared: cache must be [blocks, Hkv, 32, 128]");
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "attn_decode_shared: GQA group must be <= 16");
+  const int rows = out.size(0);
+  const int nseq = seq_q_len.numel();
+  TORCH_CHECK(q.size(0) >= rows, "attn_decode_shared: q has fewer rows than out");
+  TORCH_CHECK(work_seq.numel() == work_ct.numel(), "work list mismatch");
+  TORCH_CHECK(block_tables.size(0) >= nseq && seq_kv_len.numel() >= nseq &&
+                  seq_q_start.numel() >= nseq,
+              "attn_decode_shared: per-sequence arrays mismatch");
+  TORCH_CHECK(ws_i32.numel() >= 2 + nseq + rows, "attn_decode_shared: int32 workspace too small");
+  TORCH_CHECK(pre_o.scalar_type() == at::kFloat && pre_ml.scalar_type() == at::kFloat &&
+                  pre_o.numel() >= (int64_t)rows * Hq * 128 &&
+                  pre_ml.numel() >= (int64_t)rows * Hq * 2,
+              "attn_decode_shared: prefix partial buffers too small / not fp32");
+  rfq::launch_attn_decode_shared(
+      bp(q), q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int32_t>(),
+      block_tables.stride(0), seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
+      seq_kv_len.data_ptr<int32_t>(), nseq, work_seq.data_ptr<int32_t>(),
+      work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out), out.stride(0),
+      ws_i32.data_ptr<int32_t>(), pre_o.data_ptr<float>(), pre_ml.data_ptr<float>(), Hq, Hkv,
+      (float)scale, tiles_per_item, run_meta, cur_stream());
 }
 
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
@@ -547,6 +590,10 @@ TORCH_LIBRARY(rfq_amd, m) {
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
         "int num_splits, int tiles_per_item=1) -> ()");
+  m.def("attn_decode_shared(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
+        "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
+        "Tensor work_ct, Tensor(a!) out, Tensor(b!) ws_i32, Tensor(c!) pre_o, Tensor(d!) pre_ml, "
+        "int Hq, int Hkv, float scale, int tiles_per_item, bool run_meta) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale) -> ()");
@@ -580,6 +627,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("embed", &embed);
   m.impl("rope_kv", &rope_kv);
   m.impl("attn_decode", &attn_decode);
+  m.impl("attn_decode_shared", &attn_decode_shared);
   m.impl("attn_prefill", &attn_prefill);
   m.impl("sample_partial", &sample_partial);
   m.impl("sample_final", &sample_final);

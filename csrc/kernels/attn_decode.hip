@@ -25,15 +25,74 @@
 //     attn_decode_reduce; with one split the kernel writes bf16 output directly.
 //   The split size is derived per sequence from its context length on device, so a
 //   hipGraph captured with a fixed split count stays balanced as contexts grow.
+//
+// Shared-prefix (cascade) mode, large decode batches: every RFQ request starts with the
+// same system prompt + template, whose KV pages the prefix cache shares.  Reading those
+// pages once per sequence is ~half of the decode KV traffic.  attn_prefix_meta finds on
+// device the longest run of leading pages that decode sequence 0 shares with the other
+// sequences (P pages; sequences sharing fewer than kMinPrefixPages opt out), then
+//   * MODE 2 (prefix): the MFMA columns are (q row, head) pairs of EIGHT different
+//     sequences (NT = 2, G = 4), so each prefix K/V page is read once per 8 rows;
+//     writes the unnormalised O, running max and sum per (row, head);
+//   * MODE 1 (suffix): the normal per-sequence kernel over keys [P*32, kv_len) that
+//     merges the prefix partial into its registers before the bf16 store.
+// Everything is derived on device, so captured decode graphs stay valid.
 #include "common.h"
 
 namespace rfq {
 
 constexpr int kD = 128;
 constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
+constexpr int kMinPrefixPages = 4;
+
+struct PrefixArgs {
+  const int32_t* meta;     // [0] shared prefix length in tokens (P * kPage), [1] row count
+  const int32_t* pflag;    // per sequence: 1 = keys [0, P*32) come from the prefix pass
+  const int32_t* rowlist;  // q rows of the participating sequences (meta[1] of them)
+  float* pre_o;            // [rows][Hq][128] unnormalised prefix output
+  float* pre_ml;           // [rows][Hq][2] running max (log2 domain), softmax sum
+};
+
+// Single workgroup: P = min over participating sequences of the shared leading page run.
+__global__ __launch_bounds__(1024) void attn_prefix_meta_kernel(
+    const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_q_start,
+    const int32_t* __restrict__ seq_q_len, const int32_t* __restrict__ seq_kv_len, int nseq,
+    int32_t* __restrict__ meta, int32_t* __restrict__ pflag, int32_t* __restrict__ rowlist) {
+  __shared__ int32_t ref[256];
+  __shared__ int32_t s_min, s_cnt, s_cand;
+  const int tid = threadIdx.x;
+  const int ref_len = nseq > 0 ? min(min((seq_kv_len[0] - seq_q_len[0]) / kPage, bt_stride), 256) : 0;
+  if (tid < ref_len) ref[tid] = block_tables[tid];
+  if (tid == 0) { s_min = 1 << 30; s_cnt = 0; s_cand = 0; }
+  __syncthreads();
+  for (int s = tid; s < nseq; s += blockDim.x) {
+    const int cap = min(ref_len, (seq_kv_len[s] - seq_q_len[s]) / kPage);
+    const int32_t* bt = block_tables + (int64_t)s * bt_stride;
+    int m = 0;
+    while (m < cap && bt[m] == ref[m]) ++m;
+    pflag[s] = m;
+    if (m >= kMinPrefixPages) {
+      atomicMin(&s_min, m);
+      atomicAdd(&s_cand, 1);
+    }
+  }
+  __syncthreads();
+  const int P = s_cand < 2 ? 0 : s_min;     // sequence 0 alone shares nothing
+  for (int s = tid; s < nseq; s += blockDim.x) {
+    const int on = P > 0 && pflag[s] >= P;   // each thread rereads only what it wrote
+    pflag[s] = on;
+    if (on) {
+      const int ql = seq_q_len[s], q0 = seq_q_start[s];
+      const int base = atomicAdd(&s_cnt, ql);
+      for (int i = 0; i < ql; ++i) rowlist[base + i] = q0 + i;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) { meta[0] = P * kPage; meta[1] = s_cnt; }
+}
 
 // (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over
-template <int NT>
+template <int NT, int MODE = 0>
 __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -41,35 +100,53 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
-    int num_splits) {
+    int num_splits, PrefixArgs px = PrefixArgs{}) {
   __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
   const int split = blockIdx.x, kvh = blockIdx.y, w = blockIdx.z;
   const int lane = threadIdx.x;
   const int g = lane >> 4;   // 16-lane group
   const int c = lane & 15;   // MFMA column
   const int G = Hq / Hkv;
-  const int seq = work_seq[w];
-  if (seq < 0) return;       // padding work item (graph-captured buckets)
-  const int ql = seq_q_len[seq];
-  const int kvl = seq_kv_len[seq];
-  // NT column tiles per work item share every K fragment and V tile they load
   bool act[NT], cvalid[NT];
   int h[NT], qrow[NT], lim[NT];
+  int seq, ql, kvl, base = 0;
+  if constexpr (MODE == 2) {
+    // columns are (row, head) pairs of the participating rows, 16 * NT per work item
+    const int P = px.meta[0], nrow = px.meta[1];
+    if (P == 0 || w * 16 * NT >= nrow * G) return;
+    seq = 0; ql = 1; kvl = P;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int tile = work_ct[w] * NT + t;
-    act[t] = tile * 16 < ql * G;                       // wave-uniform
-    const int col = tile * 16 + c;
-    cvalid[t] = col < ql * G;
-    const int qi = cvalid[t] ? col / G : 0;
-    h[t] = kvh * G + (cvalid[t] ? col % G : 0);
-    qrow[t] = seq_q_start[seq] + qi;
-    lim[t] = kvl - ql + qi + 1;                        // keys [0, lim) visible
+    for (int t = 0; t < NT; ++t) {
+      const int col = (w * NT + t) * 16 + c;
+      act[t] = (w * NT + t) * 16 < nrow * G;           // wave-uniform
+      cvalid[t] = col < nrow * G;
+      qrow[t] = px.rowlist[cvalid[t] ? col / G : 0];
+      h[t] = kvh * G + (cvalid[t] ? col % G : 0);
+      lim[t] = P;                                      // the whole prefix is visible
+    }
+  } else {
+    seq = work_seq[w];
+    if (seq < 0) return;       // padding work item (graph-captured buckets)
+    ql = seq_q_len[seq];
+    kvl = seq_kv_len[seq];
+    if constexpr (MODE == 1) base = px.pflag[seq] ? px.meta[0] : 0;
+    // NT column tiles per work item share every K fragment and V tile they load
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int tile = work_ct[w] * NT + t;
+      act[t] = tile * 16 < ql * G;                       // wave-uniform
+      const int col = tile * 16 + c;
+      cvalid[t] = col < ql * G;
+      const int qi = cvalid[t] ? col / G : 0;
+      h[t] = kvh * G + (cvalid[t] ? col % G : 0);
+      qrow[t] = seq_q_start[seq] + qi;
+      lim[t] = kvl - ql + qi + 1;                        // keys [0, lim) visible
+    }
   }
 
-  int tps = (kvl + num_splits - 1) / num_splits;
+  int tps = (kvl - base + num_splits - 1) / num_splits;
   tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = split * tps;
+  const int start = base + split * tps;
   const int end = min(kvl, start + tps);
 
   float m_run[NT], l_run[NT];
@@ -194,6 +271,32 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     l_tot += __shfl_xor(l_tot, 16, 64);
     l_tot += __shfl_xor(l_tot, 32, 64);
     if (!cvalid[t]) continue;
+    if constexpr (MODE == 2) {
+      const int64_t pidx = (int64_t)qrow[t] * Hq + h[t];
+      float* po = px.pre_o + pidx * kD;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[t][m];
+      if (g == 0) {
+        px.pre_ml[pidx * 2 + 0] = m_run[t];
+        px.pre_ml[pidx * 2 + 1] = l_tot;
+      }
+      continue;
+    }
+    if (MODE == 1 && num_splits == 1 && base > 0) {
+      // merge the shared-prefix partial of this (row, head) column
+      const int64_t pidx = (int64_t)qrow[t] * Hq + h[t];
+      const float pm = px.pre_ml[pidx * 2 + 0], pl = px.pre_ml[pidx * 2 + 1];
+      const float* po = px.pre_o + pidx * kD;
+      const float mt = fmaxf(m_run[t], pm);
+      const float mu = mt == -INFINITY ? 0.f : mt;
+      const float a1 = fast_exp2(m_run[t] - mu), a2 = fast_exp2(pm - mu);
+      l_tot = l_tot * a1 + pl * a2;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(po + 16 * m + 4 * g);
+        o[t][m] = o[t][m] * a1 + pv * a2;
+      }
+    }
     if (num_splits == 1) {
       const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
       bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
@@ -274,6 +377,43 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
   if (num_splits > 1)
     attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                         num_splits);
+}
+
+// Shared-prefix decode attention (num_splits == 1): meta pass, prefix pass over the rows
+// of the participating sequences (8 rows per wave), suffix pass per sequence + merge.
+// ws_i32: [2 + nseq + rows] int32; pre_o: rows*Hq*128 fp32; pre_ml: rows*Hq*2 fp32.
+void launch_attn_decode_shared(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
+                               const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
+                               const int32_t* seq_q_start, const int32_t* seq_q_len,
+                               const int32_t* seq_kv_len, int nseq, const int32_t* work_seq,
+                               const int32_t* work_ct, int W, int rows, bf16_t* out,
+                               int64_t out_stride, int32_t* ws_i32, float* pre_o, float* pre_ml,
+                               int Hq, int Hkv, float scale, int tiles_per_item, bool run_meta,
+                               hipStream_t s) {
+  if (W == 0 || rows == 0) return;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  PrefixArgs px{ws_i32, ws_i32 + 2, ws_i32 + 2 + nseq, pre_o, pre_ml};
+  if (run_meta)
+    attn_prefix_meta_kernel<<<1, 1024, 0, s>>>(block_tables, bt_stride, seq_q_start, seq_q_len,
+                                                seq_kv_len, nseq, ws_i32, ws_i32 + 2,
+                                                ws_i32 + 2 + nseq);
+  const int G = Hq / Hkv;
+  const dim3 gp(1, Hkv, (rows * G + 31) / 32);
+  attn_decode_kernel<2, 2><<<gp, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                             bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                             work_seq, work_ct, out, out_stride, nullptr, nullptr,
+                                             Hq, Hkv, scale_log2, 1, px);
+  const dim3 grid(1, Hkv, W);
+  if (tiles_per_item == 2)
+    attn_decode_kernel<2, 1><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                 bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                 work_seq, work_ct, out, out_stride, nullptr,
+                                                 nullptr, Hq, Hkv, scale_log2, 1, px);
+  else
+    attn_decode_kernel<1, 1><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                 bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                 work_seq, work_ct, out, out_stride, nullptr,
+                                                 nullptr, Hq, Hkv, scale_log2, 1, px);
 }
 
 }  // namespace rfq

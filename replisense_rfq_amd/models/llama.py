@@ -120,6 +120,14 @@ class DecoderLM:
         if D > 0 and m.decode_splits > 1 and x.is_cuda:
             dec_parts = (torch.empty(D * hq * m.decode_splits * 128, device=self.device),
                          torch.empty(D * hq * m.decode_splits * 2, device=self.device))
+        shared = None
+        if (D >= ops.SHARED_PREFIX_MIN_ROWS and dec_parts is None and x.is_cuda
+                and ops.SHARED_PREFIX_MIN_ROWS > 0):
+            # cascade attention over the shared prompt pages (meta computed in layer 0)
+            nseq = m.dec_q_len.shape[0]
+            shared = (torch.empty(2 + nseq + D, dtype=torch.int32, device=self.device),
+                      torch.empty(D * hq * 128, device=self.device),
+                      torch.empty(D * hq * 2, device=self.device))
         moe_bufs = self.moe_buffers(T) if (cfg.is_moe and x.is_cuda) else None
         L = cfg.n_layers
         for li in range(L):
@@ -127,7 +135,12 @@ class DecoderLM:
             kc, vc = self.kv_k[li], self.kv_v[li]
             qkv = ops.qkv_rope(x, lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
                                hq, hkv)
-            if D > 0:
+            if shared is not None:
+                ops.attn_decode_shared(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start,
+                                       m.dec_q_len, m.dec_kv_len, m.dec_work_seq, m.dec_work_ct,
+                                       attn[:D], *shared, hq, hkv, self.scale, m.decode_tiles,
+                                       li == 0)
+            elif D > 0:
                 po, pm = dec_parts if dec_parts is not None else (attn, attn)
                 ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                                 m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,

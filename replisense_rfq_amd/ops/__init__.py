@@ -20,7 +20,7 @@ __all__ = [
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
     "set_rope_plan",
-    "rope_plan", "qkv_rope", "moe_route",
+    "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -329,6 +329,28 @@ def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_
         _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
                                   work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
                                   num_splits, tiles_per_item)
+    else:
+        ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
+                         out, Hq, Hkv, scale)
+
+
+# decode batches at least this large use the shared-prefix (cascade) attention path
+# (0 = off, the default: measured neutral on the RFQ bench, profiles/r1_experiments_rejected.md §8)
+SHARED_PREFIX_MIN_ROWS = int(os.environ.get("RFQ_SHARED_PREFIX_MIN_ROWS", "0"))
+
+
+def attn_decode_shared(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq,
+                       work_ct, out, ws_i32, pre_o, pre_ml, Hq, Hkv, scale, tiles_per_item=1,
+                       run_meta=True):
+    """attn_decode (one split) with the shared system-prompt pages attended once per 8
+    rows instead of once per sequence (csrc/kernels/attn_decode.hip, cascade mode).
+    run_meta=False reuses the prefix metadata an earlier layer of the step computed in
+    ws_i32 (same block tables).  Workspaces: ws_i32 int32 >= 2 + nseq + rows, pre_o fp32
+    >= rows*Hq*128, pre_ml fp32 >= rows*Hq*2."""
+    if _gpu(q):
+        _native.ops().attn_decode_shared(q, k_cache, v_cache, block_tables, q_start, q_len,
+                                         kv_len, work_seq, work_ct, out, ws_i32, pre_o, pre_ml,
+                                         Hq, Hkv, scale, tiles_per_item, run_meta)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
                          out, Hq, Hkv, scale)

@@ -140,6 +140,74 @@ def test_attn_decode(gpu, Hq, Hkv, splits, tiles):
     _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits} tiles={tiles}")
 
 
+@pytest.mark.parametrize("Hq,Hkv,tiles", [(32, 8, 1), (32, 8, 2), (8, 1, 1)])
+@pytest.mark.parametrize("share", [True, False])
+def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
+    """Cascade decode attention == per-sequence attention: sequences whose leading pages
+    equal sequence 0's (>= 4 pages, and before their queries) get the shared pages from
+    the 8-rows-per-wave prefix pass; others (2 shared pages, too short, unrelated,
+    padding) attend in full."""
+    torch.manual_seed(11)
+    G = Hq // Hkv
+    nblocks = 2048
+    k, v = _paged_cache(nblocks, Hkv, gpu, seed=12)
+    rng = torch.Generator().manual_seed(13)
+    perm = torch.randperm(nblocks - 1, generator=rng).tolist()
+    common = perm[:12]
+    nxt = 12
+    cases = [(1, 400, 12)] + [(1, int(torch.randint(230, 900, (1,), generator=rng)), 7 + i % 4)
+                               for i in range(30)]
+    cases += [(5, 300, 9), (1, 500, 2), (1, 333, 0), (1, 100, 12), (9, 240, 12), (1, 1, -1)]
+    maxb = max((kv + 31) // 32 for _, kv, _ in cases)
+    bt = torch.full((len(cases), maxb), nblocks - 1, dtype=torch.int32)
+    for i, (ql, kvl, sh) in enumerate(cases):
+        nb = (kvl + 31) // 32
+        for j in range(nb):
+            if share and j < sh:
+                bt[i, j] = common[j]
+            elif sh >= 0:
+                bt[i, j] = perm[nxt]
+                nxt += 1
+    qlens = [c[0] for c in cases]
+    kvlens = [c[1] for c in cases]
+    T = sum(qlens)
+    qs = [sum(qlens[:i]) for i in range(len(qlens))]
+    ws, wct = [], []
+    for i, ql in enumerate(qlens[:-1]):
+        for ct in range(((ql * G + 15) // 16 + tiles - 1) // tiles):
+            ws.append(i)
+            wct.append(ct)
+    ws.append(-1)
+    wct.append(0)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
+    q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
+    bt = bt.to(gpu)
+    args = (q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct))
+    scale = 1 / math.sqrt(128)
+    out = torch.zeros(T, Hq * 128, device=gpu, dtype=BF)
+    wsi = torch.full((2 + len(cases) + T,), -7, dtype=torch.int32, device=gpu)
+    pre_o = torch.empty(T * Hq * 128, device=gpu)
+    pre_ml = torch.empty(T * Hq * 2, device=gpu)
+    ops.attn_decode_shared(*args, out, wsi, pre_o, pre_ml, Hq, Hkv, scale, tiles, True)
+    torch.cuda.synchronize()
+    meta = wsi.cpu()
+    if share:
+        assert meta[0].item() == 7 * 32
+        flags = meta[2:2 + len(cases)].tolist()
+        assert flags[:32] == [1] * 32 and flags[32:] == [0, 0, 0, 1, 0]
+        assert meta[1].item() == 31 + 5 + 9
+    else:
+        assert meta[0].item() == 0 and meta[1].item() == 0
+    exp = torch.zeros(T, Hq * 128, dtype=BF)
+    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
+                     torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
+    _close(out[:T - 1], exp[:T - 1], 2e-2, 0, f"attn_decode_shared Hq={Hq} share={share}")
+    # a later layer of the same step reuses the metadata
+    out2 = torch.zeros_like(out)
+    ops.attn_decode_shared(*args, out2, wsi, pre_o, pre_ml, Hq, Hkv, scale, tiles, False)
+    torch.testing.assert_close(out2[:T - 1], out[:T - 1], rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
 def test_attn_prefill(gpu, Hq, Hkv):
     torch.manual_seed(6)
