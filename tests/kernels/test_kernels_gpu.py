@@ -50,11 +50,14 @@ def test_fused_add_rms_norm(gpu, rows, d):
 
 def test_silu_mul_and_embed(gpu):
     torch.manual_seed(2)
-    gu = torch.randn(37, 2 * 14336, device=gpu, dtype=BF)
-    out = ops.silu_mul(gu)
-    exp = torch.empty_like(out)
-    ref.silu_mul(gu, exp)
-    _close(out, exp, 1e-2, 1e-2, "silu_mul")
+    # full width, a TP=8 shard (row slice narrower than one workgroup), and a
+    # row-strided view of a wider buffer
+    for rows, F, pad in ((37, 14336, 0), (70000, 1792, 0), (5, 1800, 24)):
+        gu = torch.randn(rows, 2 * F + pad, device=gpu, dtype=BF)[:, :2 * F]
+        out = ops.silu_mul(gu)
+        exp = torch.empty_like(out)
+        ref.silu_mul(gu, exp)
+        _close(out, exp, 1e-2, 1e-2, f"silu_mul rows={rows} F={F}")
     table = torch.randn(1000, 4096, device=gpu, dtype=BF)
     ids = torch.randint(0, 1000, (19,), device=gpu, dtype=torch.int32)
     assert torch.equal(ops.embed(ids, table), table[ids.long()])
