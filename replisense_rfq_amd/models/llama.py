@@ -22,6 +22,7 @@ hipGraph by the engine (engine/graphs.py).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -87,6 +88,11 @@ class DecoderLM:
         self.kv_k = None
         self.kv_v = None
         self._moe_bufs: dict[int, MoEBuffers] = {}
+        # Megatron sequence parallelism for steps of >= sp_min_tokens tokens (TP > 1):
+        # the residual stream lives sharded by token rows; each all-reduce becomes a
+        # reduce-scatter (then the residual-add RMSNorm runs on 1/W of the rows) and an
+        # all-gather before the next column-parallel GEMM.  0 = off (SURVEY.md §2.3 SP).
+        self.sp_min_tokens = int(os.environ.get("RFQ_SP_MIN_TOKENS", "0"))
 
     # ------------------------------------------------------------------ KV pool
     def attach_kv_cache(self, k_pool: torch.Tensor, v_pool: torch.Tensor) -> None:
@@ -107,50 +113,22 @@ class DecoderLM:
     # ------------------------------------------------------------------ forward
     def forward(self, m: ForwardMeta) -> torch.Tensor:
         cfg, w = self.cfg, self.w
-        T, D = m.num_tokens, m.num_decode
+        T = m.num_tokens
         eps = cfg.rms_eps
-        hq, hkv = self.hq, self.hkv
-        qd = hq * cfg.head_dim
+        qd = self.hq * cfg.head_dim
 
+        if self.tp.enabled and 0 < self.sp_min_tokens <= T:
+            return self._forward_sp(m)
         h = ops.embed(m.input_ids[:T], w["embed"])
         residual = h
         x = ops.rms_norm(h, w["layers"][0]["attn_norm"], eps)
         attn = torch.empty((T, qd), dtype=self.dtype, device=self.device)
-        dec_parts = None
-        if D > 0 and m.decode_splits > 1 and x.is_cuda:
-            dec_parts = (torch.empty(D * hq * m.decode_splits * 128, device=self.device),
-                         torch.empty(D * hq * m.decode_splits * 2, device=self.device))
-        shared = None
-        if (D >= ops.SHARED_PREFIX_MIN_ROWS and dec_parts is None and x.is_cuda
-                and ops.SHARED_PREFIX_MIN_ROWS > 0):
-            # cascade attention over the shared prompt pages (meta computed in layer 0)
-            nseq = m.dec_q_len.shape[0]
-            shared = (torch.empty(2 + nseq + D, dtype=torch.int32, device=self.device),
-                      torch.empty(D * hq * 128, device=self.device),
-                      torch.empty(D * hq * 2, device=self.device))
+        dec_parts, shared = self._attn_scratch(m, x)
         moe_bufs = self.moe_buffers(T) if (cfg.is_moe and x.is_cuda) else None
         L = cfg.n_layers
         for li in range(L):
             lw = w["layers"][li]
-            kc, vc = self.kv_k[li], self.kv_v[li]
-            qkv = ops.qkv_rope(x, lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
-                               hq, hkv)
-            if shared is not None:
-                ops.attn_decode_shared(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start,
-                                       m.dec_q_len, m.dec_kv_len, m.dec_work_seq, m.dec_work_ct,
-                                       attn[:D], *shared, hq, hkv, self.scale, m.decode_tiles,
-                                       li == 0)
-            elif D > 0:
-                po, pm = dec_parts if dec_parts is not None else (attn, attn)
-                ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
-                                m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
-                                hq, hkv, self.scale,
-                                m.decode_splits if dec_parts is not None else 1,
-                                m.decode_tiles)
-            if m.num_prefill_tokens > 0:
-                ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
-                                 m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
-                                 self.scale)
+            self._attend(li, x, attn, m, dec_parts, shared)
             # TP = 1 latency path: the o / down skinny GEMM runs the residual-add
             # RMSNorm in its last workgroup when the start-up plan measured it faster
             fuse = not self.tp.enabled and T <= ops.NORM_FUSE_MAX_M
@@ -173,6 +151,94 @@ class DecoderLM:
             ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
+
+    def _forward_sp(self, m: ForwardMeta) -> torch.Tensor:
+        """Sequence-parallel forward (TP group of W ranks, T tokens padded to Tp = W*n).
+
+        Per layer: AG(x shard) -> QKV / attention / O (rows [0, T) real) -> RS ->
+        residual-add RMSNorm on this rank's n rows -> AG -> gate|up / down -> RS ->
+        residual-add RMSNorm.  Same bytes on the wire as two all-reduces, but the
+        norms and the residual stream cost 1/W; padding rows are zero and never read
+        back.  The final shard is gathered once before the vocab-parallel LM head."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        T, W, eps = m.num_tokens, tp.world, cfg.rms_eps
+        n = -(-T // W)
+        Tp, lo = n * W, tp.rank * n
+        d = cfg.hidden
+        h = torch.zeros((Tp, d), dtype=self.dtype, device=self.device)
+        ops.embed(m.input_ids[:T], w["embed"], out=h[:T])
+        residual = h[lo:lo + n].clone()
+        xs = ops.rms_norm(residual, w["layers"][0]["attn_norm"], eps)
+        x = torch.empty((Tp, d), dtype=self.dtype, device=self.device)
+        part = torch.empty((Tp, d), dtype=self.dtype, device=self.device)
+        shard = torch.empty((n, d), dtype=self.dtype, device=self.device)
+        attn = torch.zeros((Tp, self.hq * cfg.head_dim), dtype=self.dtype, device=self.device)
+        dec_parts, shared = self._attn_scratch(m, x)
+        moe_bufs = self.moe_buffers(Tp) if (cfg.is_moe and x.is_cuda) else None
+        L = cfg.n_layers
+        for li in range(L):
+            lw = w["layers"][li]
+            tp.all_gather_rows(x, xs)
+            self._attend(li, x, attn, m, dec_parts, shared)
+            ops.linear(attn, lw["o"], out=part)
+            tp.reduce_scatter_rows(shard, part)
+            ops.fused_add_rms_norm(shard, residual, lw["mlp_norm"], eps, out=xs)
+            tp.all_gather_rows(x, xs)
+            nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
+            if cfg.is_moe:
+                mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
+                             expert_offset=self.expert_offset)
+            else:
+                mo = ops.silu_linear(ops.linear(x, lw["gate_up"]), lw["down"])
+            tp.reduce_scatter_rows(shard, mo)
+            ops.fused_add_rms_norm(shard, residual, nxt, eps, out=xs)
+        tp.all_gather_rows(x, xs)
+        x = x[:T]
+        xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
+        return ops.linear(xs, w["lm_head"])
+
+    def _attn_scratch(self, m: ForwardMeta, x: torch.Tensor):
+        """Split-K partials for decode attention and cascade-attention scratch."""
+        D, hq = m.num_decode, self.hq
+        dec_parts = None
+        if D > 0 and m.decode_splits > 1 and x.is_cuda:
+            dec_parts = (torch.empty(D * hq * m.decode_splits * 128, device=self.device),
+                         torch.empty(D * hq * m.decode_splits * 2, device=self.device))
+        shared = None
+        if (D >= ops.SHARED_PREFIX_MIN_ROWS and dec_parts is None and x.is_cuda
+                and ops.SHARED_PREFIX_MIN_ROWS > 0):
+            # cascade attention over the shared prompt pages (meta computed in layer 0)
+            nseq = m.dec_q_len.shape[0]
+            shared = (torch.empty(2 + nseq + D, dtype=torch.int32, device=self.device),
+                      torch.empty(D * hq * 128, device=self.device),
+                      torch.empty(D * hq * 2, device=self.device))
+        return dec_parts, shared
+
+    def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared) -> None:
+        """QKV GEMM + RoPE + paged-KV append, then decode / prefill attention into
+        ``attn`` (rows [0, T) of x and attn; rows past T are SP padding)."""
+        T, D = m.num_tokens, m.num_decode
+        hq, hkv = self.hq, self.hkv
+        lw = self.w["layers"][li]
+        kc, vc = self.kv_k[li], self.kv_v[li]
+        qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
+                           hq, hkv)
+        if shared is not None:
+            ops.attn_decode_shared(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start,
+                                   m.dec_q_len, m.dec_kv_len, m.dec_work_seq, m.dec_work_ct,
+                                   attn[:D], *shared, hq, hkv, self.scale, m.decode_tiles,
+                                   li == 0)
+        elif D > 0:
+            po, pm = dec_parts if dec_parts is not None else (attn, attn)
+            ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
+                            m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
+                            hq, hkv, self.scale,
+                            m.decode_splits if dec_parts is not None else 1,
+                            m.decode_tiles)
+        if m.num_prefill_tokens > 0:
+            ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
+                             m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
+                             self.scale)
 
     # ------------------------------------------------------------- conveniences
     def weight_bytes(self) -> int:

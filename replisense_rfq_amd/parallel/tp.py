@@ -81,6 +81,24 @@ class TPContext:
             out[0].copy_(inp)
         return out
 
+    def reduce_scatter_rows(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """Sequence-parallel hand-off: sum ``inp`` [W*n, d] over ranks, keep rows
+        [rank*n, (rank+1)*n) in ``out`` [n, d].  One RCCL reduce-scatter moves half an
+        all-reduce's bytes per rank over the xGMI ring."""
+        if self.world > 1:
+            dist.reduce_scatter_tensor(out, inp, group=self.group)
+        else:
+            out.copy_(inp)
+        return out
+
+    def all_gather_rows(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out [W*n, d] <- concat over ranks of inp [n, d] (rank order)."""
+        if self.world > 1:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        else:
+            out.copy_(inp)
+        return out
+
     def broadcast_obj(self, obj, src: int = 0):
         if self.world == 1:
             return obj

@@ -19,7 +19,7 @@ def _port():
     return p
 
 
-def _forward_worker(rank, world, port, q):
+def _forward_worker(rank, world, port, q, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -33,7 +33,8 @@ def _forward_worker(rank, world, port, q):
     full = init_weights(cfg, SINGLE, "cpu", seed=11)
     tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
     m = DecoderLM(cfg, "cpu", tp=tp, weights=shard_weights(full, cfg, tp))
-    T, nb = 40, 4
+    m.sp_min_tokens = 1 if sp else 0
+    T, nb = (39 if sp else 40), 4  # 39: SP pads the last rank's row shard
     shape = (cfg.n_layers, nb, m.hkv, 32, 128)
     m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16), torch.zeros(shape, dtype=torch.bfloat16))
     g = torch.Generator().manual_seed(0)
@@ -80,7 +81,7 @@ def _engine_worker(rank, world, port, q, control="shm"):
     dist.destroy_process_group()
 
 
-def _moe_forward_worker(rank, world, port, q, ep):
+def _moe_forward_worker(rank, world, port, q, ep, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -94,7 +95,8 @@ def _moe_forward_worker(rank, world, port, q, ep):
     full = init_weights(cfg, SINGLE, "cpu", seed=5)
     tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
     m = DecoderLM(cfg, "cpu", tp=tp, weights=shard_weights(full, cfg, tp, moe_ep=ep), moe_ep=ep)
-    T, nb = 24, 2
+    m.sp_min_tokens = 1 if sp else 0
+    T, nb = (23 if sp else 24), 2
     shape = (cfg.n_layers, nb, m.hkv, 32, 128)
     m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16),
                       torch.zeros(shape, dtype=torch.bfloat16))
@@ -121,24 +123,29 @@ def _moe_forward_worker(rank, world, port, q, ep):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("ep", [False, True])
-def test_tp2_mixtral_forward_matches_tp1(ep):
+@pytest.mark.parametrize("ep,sp", [(False, False), (True, False), (True, True)])
+def test_tp2_mixtral_forward_matches_tp1(ep, sp):
     """Mixtral MoE under TP=2: FFN-split experts (ep=False) or whole experts per
-    rank (expert parallelism, ep=True) both reproduce the single-device logits."""
+    rank (expert parallelism, ep=True) both reproduce the single-device logits,
+    also with the sequence-parallel residual stream (sp=True)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    mp.start_processes(_moe_forward_worker, args=(2, port, q, ep), nprocs=2,
+    mp.start_processes(_moe_forward_worker, args=(2, port, q, ep, sp), nprocs=2,
                        start_method="spawn")
     assert q.get(timeout=10) < 0.02
 
 
 @pytest.mark.timeout(600)
-def test_tp2_forward_matches_tp1():
+@pytest.mark.parametrize("sp", [False, True])
+def test_tp2_forward_matches_tp1(sp):
+    """Llama TP=2 logits == TP=1; sp=True runs the Megatron sequence-parallel
+    forward (reduce-scatter / all-gather of token rows, padded odd T)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    mp.start_processes(_forward_worker, args=(2, port, q), nprocs=2, start_method="spawn")
+    mp.start_processes(_forward_worker, args=(2, port, q, sp), nprocs=2,
+                       start_method="spawn")
     assert q.get(timeout=10) < 0.02
 
 
