@@ -2,27 +2,32 @@
 """RFQ extraction benchmark — BASELINE.json metric:
 "RFQ docs/sec whole-node + p50 /parse-text/ latency, Llama-3-8B TP=1 and 70B TP=8".
 
-One process per GPU (torchrun).  Each TP group is one engine replica (default
-Llama-3-8B, TP=1 => DP=N replicas, weak scaling: every replica processes the same
-number of documents per step).  A *step* = one wave of ``--docs-per-step``
-synthetic RFQ documents per replica pushed through the full extraction path:
-prompt build (8,000-char truncation + byte-identical template) -> Llama-3 chat
-tokenisation -> continuous-batching engine (chunked prefill, prefix cache,
-grammar-constrained Gumbel sampling at T=0.1, jump-forward, hipGraph decode) ->
-detokenise -> JSON recovery + pydantic validation (rfq_agent.py:185-206).
+One process per GPU.  Each TP group is one engine replica (default Llama-3-8B,
+TP=1 => DP=N replicas; weak scaling: every replica serves the same stream).
+
+Workload: every replica serves ONE continuous stream of synthetic RFQ documents
+through the full extraction path — prompt build (8,000-char truncation +
+byte-identical template, rfq_agent.py:147-151) -> Llama-3 chat tokenisation ->
+continuous-batching engine (chunked prefill, prefix cache, grammar-constrained
+Gumbel sampling at T=0.1, jump-forward, hipGraph decode) -> detokenise -> JSON
+recovery + pydantic validation (rfq_agent.py:185-206).  ``--max-num-seqs``
+documents are kept in flight; a finished document is immediately replaced by
+the next one (production continuous batching).
+
+A *step* is one fixed slice of that stream: ``--docs-per-step`` completed
+documents per replica.  ``--warmup`` steps absorb the ramp-up (first prefill
+wave, survivorship bias of the in-flight mix); then exactly ``--steps`` steps
+are timed, bracketed by barrier + ``torch.cuda.synchronize()`` on both sides,
+and the MAX over ranks is reported.  Documents count only when they complete
+inside the timed window (the stream's in-flight state carries across the
+boundaries, as in a running server).  After the timed region the in-flight
+remainder is aborted and the single-request p50 latency of the same path (the
+reference's 0.883 s p50 Groq server time) is measured on replica 0.
+
 Weights are random-init (no checkpoints offline); documents are synthetic with
-the reference's length distribution.
-
-Timed region: exactly --steps steps (= steps x docs-per-step documents per replica),
-bracketed by barrier + cuda synchronize on both sides; the max over ranks is
-reported.  Default ``--mode stream`` feeds those documents as one continuous
-stream (at most --max-num-seqs in flight, new documents admitted as others
-finish — production continuous batching); ``--mode wave`` drains each step's
-batch before starting the next.  After it, the single-request p50
-latency of the same path (the reference's 0.883 s p50 Groq server time,
-BASELINE.md) is measured on replica 0.
-
-Prints ONE JSON line on rank 0.
+the reference's length distribution.  ``--gpus N`` without a
+torchrun environment re-launches this script under torch.distributed.run with N
+ranks (before any GPU call).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -30,21 +35,12 @@ import argparse
 import json
 import os
 import queue
+import socket
 import statistics
+import subprocess
 import sys
 import threading
 import time
-
-import torch
-import torch.distributed as dist
-
-from replisense_rfq_amd.engine.engine import LLMEngine
-from replisense_rfq_amd.parallel.tp import init_distributed, split_groups
-from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
-from replisense_rfq_amd.service.hints import estimate_line_items
-from replisense_rfq_amd.service.prompt import register_prompt_prefix
-from replisense_rfq_amd.utils import synth
-from replisense_rfq_amd.utils.config import EngineConfig
 
 BASELINE_P50_S = 0.883          # Groq llama3-70b p50 server time per request
 BASELINE_DOCS_PER_S = 1.0 / BASELINE_P50_S
@@ -53,12 +49,14 @@ BASELINE_DOCS_PER_S = 1.0 / BASELINE_P50_S
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--docs-per-step", type=int, default=3072)
-    ap.add_argument("--max-num-seqs", type=int, default=3072)
+    ap.add_argument("--docs-per-step", type=int, default=512,
+                    help="completed documents per replica that make one step")
+    ap.add_argument("--max-num-seqs", type=int, default=3072,
+                    help="documents in flight per replica")
     ap.add_argument("--latency-runs", type=int, default=15)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-jump-forward", action="store_true")
@@ -67,106 +65,142 @@ def parse():
     ap.add_argument("--kv-fraction", type=float, default=0.85,
                     help="fraction of free HBM for the paged KV pool (288 GB per MI355X)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--mode", choices=("stream", "wave"), default="stream",
-                    help="stream: the K*docs-per-step documents of the timed region are one "
-                         "continuous-batching stream (max-num-seqs in flight); wave: each step "
-                         "is a closed batch that drains before the next starts")
+    ap.add_argument("--time-budget", type=float, default=0.0,
+                    help="seconds; if > 0 the latency phase is skipped once this much wall "
+                         "time has passed (the JSON line is always printed)")
     return ap.parse_args()
 
 
-class Replica:
-    def __init__(self, engine: LLMEngine, dp_rank: int, seed: int):
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _self_launch(args) -> int:
+    """`bench.py --gpus N` outside torchrun: start N ranks under torch.distributed.run
+    as a child process (never exec: no GPU has been touched in this process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+class DocStream:
+    """One replica's continuous document stream over an LLMEngine.
+
+    A producer thread builds and tokenises prompts ahead of the engine (as the
+    HTTP front-end does while the engine steps); the engine loop keeps
+    ``in_flight`` documents admitted and counts completions.  ``run_until(n)``
+    steps the engine until ``n`` documents have completed in total and returns,
+    leaving the in-flight documents in place for the next call.
+    """
+
+    def __init__(self, engine, dp_rank: int, seed: int, in_flight: int):
+        from replisense_rfq_amd.service.extract import build_messages
+        from replisense_rfq_amd.service.prompt import register_prompt_prefix
+        from replisense_rfq_amd.utils import synth
+
         self.engine = engine
         self.tok = engine.tokenizer
         register_prompt_prefix(self.tok)         # what the service's EngineBackend does
-        self.dp_rank = dp_rank
-        self.seed = seed
-        self.wave = 0
-        self.last = {}
+        self.in_flight = in_flight
+        self.base = (seed * 7919 + dp_rank) * 1_000_003
+        self.ready: queue.Queue = queue.Queue(maxsize=max(64, in_flight))
+        self.stop = threading.Event()
+        self.live = 0
+        self.completed = 0
+        self.finished = []                       # sequences completed in the current window
+        self._build, self._synth = build_messages, synth
+        self.thread = threading.Thread(target=self._produce, name="bench-tokenize", daemon=True)
+        self.thread.start()
 
-    def docs(self, n: int):
-        base = (self.seed * 7919 + self.dp_rank) * 1_000_003 + self.wave * 10_007
-        self.wave += 1
-        return [synth.make_rfq(base + i) for i in range(n)]
+    def _produce(self):
+        i = 0
+        while not self.stop.is_set():
+            d = self._synth.make_rfq(self.base + i)
+            ids = self.tok.chat_ids(self._build(d.text))
+            params = self.engine.default_params(seed=(self.base + i) & 0xFFFFFF,
+                                                **self._synth.decode_hints(d))
+            while not self.stop.is_set():
+                try:
+                    self.ready.put((ids, params), timeout=0.1)
+                    break
+                except queue.Full:
+                    continue
+            i += 1
 
-    def run_wave(self, n: int, waves: int = 1) -> int:
-        """Push n * waves documents through the service path.  As in the HTTP server
-        (requests are tokenised by the API front-end while the engine steps), a
-        producer thread builds and tokenises the prompts and the engine admits each
-        one as soon as it is ready, so prompt preparation overlaps GPU execution."""
-        t0 = time.perf_counter()
-        docs = [d for _ in range(waves) for d in self.docs(n)]
-        n = len(docs)
+    def _top_up(self, block: bool):
         eng = self.engine
-        wave = self.wave
-        ready: queue.SimpleQueue = queue.SimpleQueue()
-        prep = {}
+        while self.live < self.in_flight:
+            try:
+                ids, params = self.ready.get(block=block and not eng.has_work(), timeout=1.0)
+            except queue.Empty:
+                return
+            eng.add_request(ids, params)
+            self.live += 1
 
-        def produce():
-            ts = time.perf_counter()
-            for i, d in enumerate(docs):
-                ids = self.tok.chat_ids(build_messages(d.text))
-                ready.put((ids, eng.default_params(seed=(wave * 100_003 + i) & 0xFFFFFF,
-                                                   min_items=estimate_line_items(d.text))))
-            prep["s"] = time.perf_counter() - ts
-            ready.put(None)
+    def run_until(self, target: int):
+        eng = self.engine
+        while self.completed < target:
+            self._top_up(block=True)
+            if not eng.has_work():
+                continue
+            done = eng.step()
+            self.live -= len(done)
+            self.completed += len(done)
+            self.finished.extend(done)
 
-        old_switch = sys.getswitchinterval()
-        sys.setswitchinterval(2e-4)        # the step loop re-takes the GIL promptly
-        th = threading.Thread(target=produce, name="bench-tokenize", daemon=True)
-        th.start()
-        seqs, producing = [], True
+    def close(self):
+        self.stop.set()
         try:
             while True:
-                while producing:
-                    try:
-                        item = ready.get() if not eng.has_work() else ready.get_nowait()
-                    except queue.Empty:
-                        break
-                    if item is None:
-                        producing = False
-                    else:
-                        seqs.append(eng.add_request(*item))
-                if eng.has_work():
-                    eng.step()
-                elif not producing:
-                    break
-        finally:
-            sys.setswitchinterval(old_switch)
-            th.join()
-        t1 = t0 + prep.get("s", 0.0)
-        t2 = time.perf_counter()
-        ok = 0
-        for s in seqs:
-            out = parse_and_validate_response(eng.decode_text(s), "direct_text_input")
-            ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
-        eng.runner.tp.enabled and eng.shutdown()
-        self.phases = {"prep_s_overlapped": round(t1 - t0, 2), "engine_s": round(t2 - t0, 2),
-                       "post_s": round(time.perf_counter() - t2, 2)}
-        self.last = dict(
-            prompt_tokens=sum(s.prompt_len for s in seqs) / n,
-            completion_tokens=sum(s.num_generated for s in seqs) / n,
-            sampled_tokens=sum(s.num_sampled for s in seqs) / n,
-            prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n,
-            valid=ok / n)
-        return ok
+                self.ready.get_nowait()
+        except queue.Empty:
+            pass
+        self.thread.join(timeout=10)
+        if self.engine.has_work():
+            self.engine.abort_all("abort")
+        self.live = 0
 
-    def latency(self, runs: int) -> list[float]:
-        out = []
-        self.lat_detail = []
-        eng = self.engine
-        for i in range(runs):
-            d = synth.make_rfq(10_000_000 + self.dp_rank * 1000 + i)
-            t0 = time.perf_counter()
-            ids = self.tok.chat_ids(build_messages(d.text))
-            s, = eng.generate([ids], eng.default_params(min_items=estimate_line_items(d.text)))
-            parse_and_validate_response(eng.decode_text(s), "direct_text_input")
-            out.append(time.perf_counter() - t0)
-            sp = s.span()
-            self.lat_detail.append((s.num_generated, s.num_sampled, sp.get("ttft_ms") or 0.0,
-                                    out[-1]))
-        eng.runner.tp.enabled and eng.shutdown()      # release the TP workers' loop
-        return out
+
+def validate(engine, seqs) -> dict:
+    """Post-process the window's completions like the service does and report the
+    per-document token shape."""
+    from replisense_rfq_amd.service.extract import parse_and_validate_response
+
+    n = max(1, len(seqs))
+    ok = 0
+    for s in seqs:
+        out = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
+        ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
+    return dict(
+        prompt_tokens=sum(s.prompt_len for s in seqs) / n,
+        completion_tokens=sum(s.num_generated for s in seqs) / n,
+        sampled_tokens=sum(s.num_sampled for s in seqs) / n,
+        prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n,
+        valid=ok / n)
+
+
+def latency(engine, dp_rank: int, runs: int):
+    """Single-request end-to-end latency of the extraction path (idle engine)."""
+    from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
+    from replisense_rfq_amd.utils import synth
+
+    out, detail = [], []
+    tok = engine.tokenizer
+    for i in range(runs):
+        d = synth.make_rfq(10_000_000 + dp_rank * 1000 + i)
+        t0 = time.perf_counter()
+        ids = tok.chat_ids(build_messages(d.text))
+        s, = engine.generate([ids], engine.default_params(**synth.decode_hints(d)))
+        parse_and_validate_response(engine.decode_text(s), "direct_text_input")
+        out.append(time.perf_counter() - t0)
+        detail.append((s.num_generated, s.num_sampled, s.span().get("ttft_ms") or 0.0, out[-1]))
+    return out, detail
 
 
 def _single_stream(detail):
@@ -186,17 +220,23 @@ def _single_stream(detail):
             "baseline_decode_tok_s": 350.0}
 
 
-def sync():
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-
-
 def main():
     args = parse()
+    t_start = time.perf_counter()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args))
+
+    import torch
+    import torch.distributed as dist
+
+    from replisense_rfq_amd.engine.engine import LLMEngine
+    from replisense_rfq_amd.parallel.tp import init_distributed, split_groups
+    from replisense_rfq_amd.utils.config import EngineConfig
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     wctx = init_distributed()
     tp, dp_rank, dp_world = split_groups(args.tp) if world > 1 else (wctx, 0, 1)
     cfg = EngineConfig.from_env(
@@ -207,50 +247,69 @@ def main():
     t_init = time.perf_counter()
     engine = LLMEngine(cfg, tp=tp)
     t_init = time.perf_counter() - t_init
-    rep = Replica(engine, dp_rank, args.seed)
+    on_gpu = engine.device.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     def phase(fn):
-        """TP rank 0 drives `fn`; the other ranks of its group mirror the steps."""
+        """TP rank 0 drives `fn`; the other ranks of its group mirror the steps
+        until rank 0 releases them (engine.shutdown)."""
         if tp.rank == 0:
             r = fn()
-        else:
-            engine.worker_loop()
-            r = None
-        return r
+            if tp.enabled:
+                engine.shutdown()
+            return r
+        engine.worker_loop()
+        return None
 
-    for _ in range(args.warmup):
-        phase(lambda: rep.run_wave(args.docs_per_step))
+    stream = DocStream(engine, dp_rank, args.seed, args.max_num_seqs) if tp.rank == 0 else None
+    per = args.docs_per_step
+    phase(lambda: stream.run_until(args.warmup * per))
+    if stream is not None:
+        stream.finished.clear()
+    steps0 = engine.num_steps
     barrier()
     sync()
     t0 = time.perf_counter()
-    if args.mode == "stream":
-        phase(lambda: rep.run_wave(args.docs_per_step, waves=args.steps))
-    else:
-        for _ in range(args.steps):
-            phase(lambda: rep.run_wave(args.docs_per_step))
+    phase(lambda: stream.run_until((args.warmup + args.steps) * per))
     sync()
     barrier()
     dt = time.perf_counter() - t0
-    steps_before = engine.num_steps
+    steps_timed = engine.num_steps - steps0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64,
-                         device=engine.device if engine.device.type == "cuda" else "cpu")
+        t = torch.tensor([dt], dtype=torch.float64, device=engine.device if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    lat = []
-    if args.latency_runs and dp_rank == 0:
-        lat = phase(lambda: rep.latency(args.latency_runs)) or []
+    shape = {}
+    if stream is not None:
+        done_in_window = stream.completed - args.warmup * per
+        shape = validate(engine, stream.finished[:2048])
+        stream.close()
+    stats = engine.stats()
+
+    lat, detail = [], []
+    run_lat = bool(args.latency_runs) and (
+        not args.time_budget or time.perf_counter() - t_start < args.time_budget)
+    if world > 1:                 # every rank must take the same branch
+        f = torch.tensor([int(run_lat)], device=engine.device if on_gpu else "cpu")
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        run_lat = bool(f.item())
+    if run_lat and dp_rank == 0:
+        r = phase(lambda: latency(engine, dp_rank, args.latency_runs))
+        if r is not None:
+            lat, detail = r
     barrier()
 
     if rank == 0:
-        docs = args.docs_per_step * dp_world * args.steps
+        docs = per * dp_world * args.steps
         value = docs / dt
         p50 = statistics.median(lat) if lat else None
-        st = engine.stats()
         out = {
             "metric": "rfq_docs_per_sec_whole_node",
             "value": round(value, 3),
@@ -264,36 +323,29 @@ def main():
             "vs_baseline": round(value / BASELINE_DOCS_PER_S, 2),
             "dtype": "bf16",
             "data": "synthetic RFQ documents (reference length distribution), random-init weights",
-            "config": {"model": args.model, "global_batch": args.docs_per_step * dp_world,
-                       "seq_len": int(rep.last.get("prompt_tokens", 0) +
-                                      rep.last.get("completion_tokens", 0)),
+            "config": {"model": args.model, "global_batch": per * dp_world,
+                       "seq_len": int(shape.get("prompt_tokens", 0) +
+                                      shape.get("completion_tokens", 0)),
                        "parallelism": f"dp{dp_world}" + (f"-tp{args.tp}" if args.tp > 1 else ""),
-                       "docs_per_step_per_replica": args.docs_per_step,
+                       "step": f"{per} completed documents per replica of a continuous stream",
+                       "in_flight_per_replica": args.max_num_seqs,
                        "temperature": cfg.temperature, "grammar": cfg.grammar,
-                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
-                       "mode": args.mode, "max_num_seqs": args.max_num_seqs},
+                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs},
             "p50_parse_text_latency_s": round(p50, 4) if p50 is not None else None,
-            "single_stream": _single_stream(getattr(rep, "lat_detail", [])),
+            "single_stream": _single_stream(detail),
             "latency_vs_baseline_p50": round(BASELINE_P50_S / p50, 2) if p50 else None,
             "baseline": "vs_baseline = docs/s / (1 / 0.883 s), the reference's single-stream "
-                        "Groq llama3-70b p50 server time (BASELINE.md)",
-            "per_doc": {k: round(v, 2) for k, v in rep.last.items()},
+                        "Groq llama3-70b p50 server time (BASELINE.md); the same-path latency "
+                        "comparison is latency_vs_baseline_p50",
+            "per_doc": {k: round(v, 2) for k, v in shape.items()},
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
                        "gemm_tune_s": round(engine.tune_s, 1),
-                       "wave_phases": getattr(rep, "phases", None),
-                       "engine_steps": steps_before, "graph_steps": st.get("graph_steps"),
-                       "kv_blocks": st.get("blocks"), "preempted": st.get("preempted"),
-                       "host_s": {k: round(st.get(k, 0), 2) for k in
-                                  ("schedule_s", "pack_s", "forward_s", "post_s")}},
+                       "timed_engine_steps": steps_timed,
+                       "docs_completed_in_window_rank0": done_in_window,
+                       "graph_steps": stats.get("graph_steps"), "steps": stats.get("steps"),
+                       "kv_blocks": stats.get("blocks"), "preempted": stats.get("preempted"),
+                       "wall_s": round(time.perf_counter() - t_start, 1)},
         }
-        for r in getattr(engine, "gemm_plan", None) or []:
-            print("[bench] gemm plan %s M=%d N=%d K=%d hipblaslt %.1fus -> %s %.1fus"
-                  % (r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6]),
-                  file=sys.stderr)
-        from replisense_rfq_amd.ops.autotune import SPLIT_REPORT
-        for r in SPLIT_REPORT:
-            print("[bench] gemm split %s M=%d N=%d K=%d one call %.1fus -> %s %.1fus" % r,
-                  file=sys.stderr)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -180,3 +180,15 @@ def reference_like_completion(doc: RFQDoc, seed: int = 0) -> str:
         "missing_fields": ["response_due_date"], "requires_review": r.random() < 0.3,
     }
     return json.dumps(obj, ensure_ascii=False, indent=r.choice([None, 2]))
+
+
+def decode_hints(doc: RFQDoc) -> dict:
+    """Bench-only decoding hints for a synthetic document (SamplingParams keywords).
+
+    Random-init weights carry no knowledge of when an extraction is complete, so the
+    benchmark shapes each constrained decode like the document's extraction: one
+    ``line_items`` object per part the document mentions (the regex estimate the
+    service used to apply)."""
+    from ..service.hints import estimate_line_items
+
+    return {"min_items": estimate_line_items(doc.text)}

@@ -1,17 +1,20 @@
 """The bench.py driver contract, rehearsed on CPU with gloo: torchrun launch, one
-JSON line from rank 0 with the required keys, TP and DP layouts (the GPU box
-runs the same script over RCCL)."""
+JSON line from rank 0 with the required keys, TP and DP layouts, self-launch of
+N ranks from ``--gpus N`` and the driver's exact step flags inside a time budget
+(the GPU box runs the same script over RCCL)."""
 import json
 import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
         "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+SMALL = ["--docs-per-step", "2", "--max-num-seqs", "2", "--latency-runs", "2"]
 
 
 def _port():
@@ -22,19 +25,49 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("tp,par", [(2, "dp1-tp2"), (1, "dp2")])
-def test_bench_torchrun_gloo(tp, par):
-    model = "tiny-llama-tp" if tp > 1 else "tiny-llama"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
-           "--gpus", "2", "--steps", "1", "--warmup", "0", "--model", model, "--tp", str(tp),
-           "--docs-per-step", "2", "--max-num-seqs", "2", "--latency-runs", "2"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
-                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+def _run(cmd, timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert KEYS <= set(out)
+    return out
+
+
+@pytest.mark.parametrize("tp,par", [(2, "dp1-tp2"), (1, "dp2")])
+def test_bench_torchrun_gloo(tp, par):
+    model = "tiny-llama-tp" if tp > 1 else "tiny-llama"
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                str(_port()), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                "--model", model, "--tp", str(tp)] + SMALL)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == par
     assert out["per_doc"]["valid"] == 1.0 and out["p50_parse_text_latency_s"] > 0
+
+
+def test_bench_self_launch():
+    """`bench.py --gpus 2` outside torchrun starts 2 ranks itself (never a silent
+    1-GPU run labelled whole-node)."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                "--model", "tiny-llama"] + SMALL)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0 and out["engine"]["docs_completed_in_window_rank0"] >= 4
+
+
+def test_bench_driver_flags_time_budget():
+    """The driver's exact step flags (`--gpus 1 --steps 20 --warmup 5`) on the tiny
+    model: a step is a fixed slice of completed documents, so the whole run is
+    bounded and the reported time covers exactly the timed steps."""
+    t0 = time.perf_counter()
+    out = _run([sys.executable, "bench.py", "--gpus", "1", "--steps", "20", "--warmup", "5",
+                "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
+                "--latency-runs", "2"], timeout=300)
+    wall = time.perf_counter() - t0
+    assert wall < 240, wall
+    assert out["steps"] == 20 and out["warmup"] == 5
+    assert out["ms_per_step"] * 20 / 1e3 < wall
+    assert out["engine"]["docs_completed_in_window_rank0"] >= 40
+    assert out["per_doc"]["valid"] == 1.0
