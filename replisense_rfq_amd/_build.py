@@ -119,7 +119,9 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> Path:
 def build_runtime(verbose: bool = False) -> Path:
     import pybind11
 
-    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    # test_*.cpp are stand-alone sanitizer harnesses with their own main()
+    # (tests/engine/test_runtime_sanitized.py); they never ship in _runtime.so.
+    srcs = sorted(s for s in (CSRC / "runtime").glob("*.cpp") if not s.name.startswith("test_"))
     hdrs = sorted((CSRC / "runtime").glob("*.h"))
     flags = ["-O3", "-fPIC", "-std=c++17", "-fvisibility=hidden",
              f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
