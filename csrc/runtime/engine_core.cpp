@@ -46,7 +46,7 @@ int32_t EngineCore::add(const int32_t* prompt, int32_t n, const SeqParams& p, do
   s.t_arrival = t_arrival;
   if (p.grammar && grammar_) {
     std::vector<int32_t> forced;
-    s.gs = grammar_->initial(forced, p.min_items);
+    s.gs = grammar_->initial(forced, p.min_items, p.profile, s.p.max_tokens);
     s.has_gs = true;
     s.tokens.insert(s.tokens.end(), forced.begin(), forced.end());
     s.num_forced += (int32_t)forced.size();
@@ -455,7 +455,7 @@ std::vector<int32_t> EngineCore::post(const int32_t* sampled, int32_t n, double 
     if (!s.t_first_token) s.t_first_token = now;
     if (s.has_gs) {
       forced.clear();
-      const bool ok = grammar_->advance(s.gs, tok, forced);
+      const bool ok = grammar_->advance(s.gs, tok, forced, s.p.max_tokens - s.generated());
       s.tokens.insert(s.tokens.end(), forced.begin(), forced.end());
       s.num_forced += (int32_t)forced.size();
       s.mask_idx = grammar_->mask(s.gs);

@@ -42,6 +42,7 @@ struct SeqParams {
   int64_t seed = 0;
   bool grammar = true;
   int32_t min_items = 0;
+  int32_t profile = 0;                   // grammar profile (grammar.h Profile)
 };
 
 struct Seq {

@@ -25,31 +25,57 @@ static std::vector<T> vec(const py::dict& d, const char* k) {
 static Grammar* make_grammar(const py::dict& d) {
   auto* g = new Grammar();
   auto ops = vec<int32_t>(d, "ops");
-  for (size_t i = 0; i + 5 <= ops.size(); i += 5)
-    g->ops.push_back(Op{ops[i], ops[i + 1], ops[i + 2], ops[i + 3], ops[i + 4]});
+  for (size_t i = 0; i + 6 <= ops.size(); i += 6)
+    g->ops.push_back(Op{ops[i], ops[i + 1], ops[i + 2], ops[i + 3], ops[i + 4], ops[i + 5]});
   g->lit_off = vec<int32_t>(d, "lit_off");
   g->lit_tok = vec<int32_t>(d, "lit_tok");
   g->lit1_off = vec<int32_t>(d, "lit1_off");
   g->lit1_tok = vec<int32_t>(d, "lit1_tok");
+  g->lit_first = vec<int32_t>(d, "lit_first");
   g->choice_off = vec<int32_t>(d, "choice_off");
   auto alts = vec<int32_t>(d, "alts");
-  for (size_t i = 0; i + 7 <= alts.size(); i += 7)
-    g->alts.push_back(Alt{alts[i], alts[i + 1], alts[i + 2], alts[i + 3], alts[i + 4], alts[i + 5],
-                          alts[i + 6]});
+  for (size_t i = 0; i + 6 <= alts.size(); i += 6)
+    g->alts.push_back(Alt{alts[i], alts[i + 1], alts[i + 2], alts[i + 3], alts[i + 4], alts[i + 5]});
   g->alt_rest = vec<int32_t>(d, "alt_rest");
-  g->choice_mask = vec<int32_t>(d, "choice_mask");
-  g->choice_mask_close = vec<int32_t>(d, "choice_mask_close");
+  g->choice_masks = vec<int32_t>(d, "choice_masks");
   g->max_items = vec<int32_t>(d, "max_items");
   g->honors_min = vec<int32_t>(d, "honors_min");
+  g->caps = vec<int32_t>(d, "caps");
   g->num_masks = vec<int32_t>(d, "num_masks");
-  g->null_rest = vec<int32_t>(d, "null_rest");
+  g->num_caps = vec<int32_t>(d, "num_caps");
+  g->fin = vec<int32_t>(d, "fin");
+  g->fin1 = vec<int32_t>(d, "fin1");
+  g->close_alt = vec<int32_t>(d, "close_alt");
+  g->null_ids = vec<int32_t>(d, "null_ids");
   g->tok_class = vec<uint8_t>(d, "tok_class");
   g->tok_chars = vec<uint8_t>(d, "tok_chars");
   g->tok_digits = vec<uint8_t>(d, "tok_digits");
-  auto sc = vec<int32_t>(d, "scalars");  // str_mask quote zero dot null_first end0 end1 end2 start
-  g->str_mask = sc[0]; g->quote = sc[1]; g->zero = sc[2]; g->dot = sc[3]; g->null_first = sc[4];
-  g->end_tok[0] = sc[5]; g->end_tok[1] = sc[6]; g->end_tok[2] = sc[7]; g->start_pc = sc[8];
+  g->tok_utf = vec<uint8_t>(d, "tok_utf");
+  auto sm = vec<int32_t>(d, "str_masks");
+  if (sm.size() != STR_SUBS) throw py::value_error("str_masks must hold 5 rows");
+  std::copy(sm.begin(), sm.end(), g->str_masks);
+  // quote zero dot backslash slack start ncap cont
+  auto sc = vec<int32_t>(d, "scalars");
+  g->quote = sc[0]; g->zero = sc[1]; g->dot = sc[2]; g->backslash = sc[3]; g->slack = sc[4];
+  g->start_pc = sc[5]; g->ncap = sc[6]; g->cont = sc[7];
+  const size_t nops = g->ops.size(), nch = g->choice_off.size() - 1;
+  if (g->fin.size() != nops * NPROF || g->fin1.size() != nops * NPROF ||
+      g->close_alt.size() != nch * NPROF || g->choice_masks.size() != nch * 8 ||
+      g->caps.size() != (size_t)g->ncap * NPROF || g->null_ids.empty() ||
+      g->tok_utf.size() != g->tok_class.size() ||
+      g->num_caps.size() * NUM_PHASES != g->num_masks.size() * 2)
+    throw py::value_error("inconsistent grammar tables");
   return g;
+}
+
+static py::tuple state_tuple(const State& s) {
+  return py::make_tuple(s.pc, s.sub, s.cnt, s.rem, s.minv, s.prof);
+}
+
+static State state_of(const py::tuple& st) {
+  if (st.size() != 6) throw py::value_error("grammar state must have 6 fields");
+  return State{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
+               st[3].cast<int32_t>(), st[4].cast<int32_t>(), st[5].cast<int32_t>()};
 }
 
 PYBIND11_MODULE(_runtime, m) {
@@ -57,32 +83,30 @@ PYBIND11_MODULE(_runtime, m) {
 
   py::class_<Grammar, std::shared_ptr<Grammar>>(m, "Grammar")
       .def(py::init(&make_grammar))
-      .def("initial", [](const Grammar& g, int32_t min_items) {
+      .def("initial", [](const Grammar& g, int32_t min_items, int32_t profile, int32_t budget) {
         std::vector<int32_t> forced;
-        State s = g.initial(forced, min_items);
-        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem, s.minv), forced);
-      }, py::arg("min_items") = 0)
-      .def("advance", [](const Grammar& g, py::tuple st, int32_t tok) {
-        State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
-                st[3].cast<int32_t>(), st[4].cast<int32_t>()};
+        State s = g.initial(forced, min_items, profile, budget);
+        return py::make_tuple(state_tuple(s), forced);
+      }, py::arg("min_items") = 0, py::arg("profile") = 0, py::arg("budget") = NO_BUDGET)
+      .def("advance", [](const Grammar& g, py::tuple st, int32_t tok, int32_t budget) {
+        State s = state_of(st);
         std::vector<int32_t> forced;
-        if (!g.advance(s, tok, forced)) throw py::value_error("token not allowed by grammar");
-        return py::make_tuple(py::make_tuple(s.pc, s.sub, s.cnt, s.rem, s.minv), forced);
-      })
-      .def("mask", [](const Grammar& g, py::tuple st) {
-        State s{st[0].cast<int32_t>(), st[1].cast<int32_t>(), st[2].cast<int32_t>(),
-                st[3].cast<int32_t>(), st[4].cast<int32_t>()};
-        return g.mask(s);
-      })
-      // states: int32 [n, 5] updated in place; tokens: int32 [n]
+        if (!g.advance(s, tok, forced, budget)) throw py::value_error("token not allowed by grammar");
+        return py::make_tuple(state_tuple(s), forced);
+      }, py::arg("state"), py::arg("token"), py::arg("budget") = NO_BUDGET)
+      .def("mask", [](const Grammar& g, py::tuple st) { return g.mask(state_of(st)); })
+      .def("close_cost", [](const Grammar& g, py::tuple st) { return g.close_cost(state_of(st)); })
+      // states: int32 [n, 6] updated in place; tokens, budgets: int32 [n]
       // returns (mask_idx[n] (-1 = finished), forced_offsets[n+1], forced_tokens, ok[n])
       .def("batch_advance", [](const Grammar& g, py::array_t<int32_t, py::array::c_style> states,
-                               arr<int32_t> tokens) {
+                               arr<int32_t> tokens, arr<int32_t> budgets) {
         const py::ssize_t n = tokens.size();
-        if (states.ndim() != 2 || states.shape(0) != n || states.shape(1) != 5)
-          throw py::value_error("states must be int32 [n, 5]");
+        if (states.ndim() != 2 || states.shape(0) != n || states.shape(1) != 6)
+          throw py::value_error("states must be int32 [n, 6]");
+        if (budgets.size() != n) throw py::value_error("budgets must be int32 [n]");
         auto S = states.mutable_unchecked<2>();
         const int32_t* tk = tokens.data();
+        const int32_t* bg = budgets.data();
         py::array_t<int32_t> masks(n), offs(n + 1);
         py::array_t<bool> ok(n);
         auto M = masks.mutable_unchecked<1>();
@@ -94,10 +118,11 @@ PYBIND11_MODULE(_runtime, m) {
           py::gil_scoped_release nogil;
           for (py::ssize_t i = 0; i < n; ++i) {
             O(i) = (int32_t)forced.size();
-            State s{S(i, 0), S(i, 1), S(i, 2), S(i, 3), S(i, 4)};
-            const bool good = g.advance(s, tk[i], forced);
+            State s{S(i, 0), S(i, 1), S(i, 2), S(i, 3), S(i, 4), S(i, 5)};
+            const bool good = g.advance(s, tk[i], forced, bg[i]);
             K(i) = good;
             S(i, 0) = s.pc; S(i, 1) = s.sub; S(i, 2) = s.cnt; S(i, 3) = s.rem; S(i, 4) = s.minv;
+            S(i, 5) = s.prof;
             M(i) = g.mask(s);
           }
           O(n) = (int32_t)forced.size();
@@ -106,6 +131,7 @@ PYBIND11_MODULE(_runtime, m) {
         std::copy(forced.begin(), forced.end(), ft.mutable_data());
         return py::make_tuple(masks, offs, ft, ok);
       })
+      .def_readonly("slack", &Grammar::slack)
       .def("num_ops", [](const Grammar& g) { return (int)g.ops.size(); });
 
   py::class_<BlockManager>(m, "BlockManager")
@@ -168,8 +194,9 @@ PYBIND11_MODULE(_runtime, m) {
              return new EngineCore(cfg, std::const_pointer_cast<const Grammar>(g));
            }), py::arg("config"), py::arg("grammar") = nullptr)
       .def("add", [](EngineCore& e, arr<int32_t> prompt, float temperature, int32_t max_tokens,
-                     int64_t seed, bool grammar, int32_t min_items, double t_arrival) {
-        SeqParams p{temperature, max_tokens, seed, grammar, min_items};
+                     int64_t seed, bool grammar, int32_t min_items, int32_t profile,
+                     double t_arrival) {
+        SeqParams p{temperature, max_tokens, seed, grammar, min_items, profile};
         return e.add(prompt.data(), (int32_t)prompt.size(), p, t_arrival);
       })
       .def("schedule_and_pack", [](EngineCore& e, py::array_t<int32_t, py::array::c_style> header,

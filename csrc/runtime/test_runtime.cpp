@@ -6,9 +6,10 @@
 //
 //  1. BlockManager fuzz: random allocate / release / register / match_prefix
 //     against a shadow model of refcounts, checking every invariant.
-//  2. Grammar random walks: from initial(min_items), repeatedly pick a random
-//     token allowed by the current mask row and advance — every pick must be
-//     accepted and every walk must finish inside the token budget.
+//  2. Grammar random walks: from initial(min_items, profile, budget), repeatedly
+//     pick a random token allowed by the current mask row and advance — every
+//     pick must be accepted and every walk must finish inside its token budget
+//     (random budgets 200..1200 exercise the close-out).
 // Prints "OK ..." and exits 0 on success; any violation aborts.
 #include <cstdio>
 #include <cstdlib>
@@ -70,30 +71,40 @@ static Blob read_blob(const char* path) {
 static Grammar build(const Blob& b) {
   Grammar g;
   auto ops = b.get<int32_t>("ops");
-  for (size_t i = 0; i + 5 <= ops.size(); i += 5)
-    g.ops.push_back(Op{ops[i], ops[i + 1], ops[i + 2], ops[i + 3], ops[i + 4]});
+  for (size_t i = 0; i + 6 <= ops.size(); i += 6)
+    g.ops.push_back(Op{ops[i], ops[i + 1], ops[i + 2], ops[i + 3], ops[i + 4], ops[i + 5]});
   g.lit_off = b.get<int32_t>("lit_off");
   g.lit_tok = b.get<int32_t>("lit_tok");
   g.lit1_off = b.get<int32_t>("lit1_off");
   g.lit1_tok = b.get<int32_t>("lit1_tok");
+  g.lit_first = b.get<int32_t>("lit_first");
   g.choice_off = b.get<int32_t>("choice_off");
   auto a = b.get<int32_t>("alts");
-  for (size_t i = 0; i + 7 <= a.size(); i += 7)
-    g.alts.push_back(Alt{a[i], a[i + 1], a[i + 2], a[i + 3], a[i + 4], a[i + 5], a[i + 6]});
+  for (size_t i = 0; i + 6 <= a.size(); i += 6)
+    g.alts.push_back(Alt{a[i], a[i + 1], a[i + 2], a[i + 3], a[i + 4], a[i + 5]});
   g.alt_rest = b.get<int32_t>("alt_rest");
-  g.choice_mask = b.get<int32_t>("choice_mask");
-  g.choice_mask_close = b.get<int32_t>("choice_mask_close");
+  g.choice_masks = b.get<int32_t>("choice_masks");
   g.max_items = b.get<int32_t>("max_items");
   g.honors_min = b.get<int32_t>("honors_min");
+  g.caps = b.get<int32_t>("caps");
   g.num_masks = b.get<int32_t>("num_masks");
-  g.null_rest = b.get<int32_t>("null_rest");
+  g.num_caps = b.get<int32_t>("num_caps");
+  g.fin = b.get<int32_t>("fin");
+  g.fin1 = b.get<int32_t>("fin1");
+  g.close_alt = b.get<int32_t>("close_alt");
+  g.null_ids = b.get<int32_t>("null_ids");
   g.tok_class = b.get<uint8_t>("tok_class");
   g.tok_chars = b.get<uint8_t>("tok_chars");
   g.tok_digits = b.get<uint8_t>("tok_digits");
+  g.tok_utf = b.get<uint8_t>("tok_utf");
+  auto sm = b.get<int32_t>("str_masks");
+  CHECK(sm.size() == STR_SUBS);
+  for (int i = 0; i < STR_SUBS; ++i) g.str_masks[i] = sm[i];
   auto sc = b.get<int32_t>("scalars");
-  CHECK(sc.size() >= 9);
-  g.str_mask = sc[0]; g.quote = sc[1]; g.zero = sc[2]; g.dot = sc[3]; g.null_first = sc[4];
-  g.end_tok[0] = sc[5]; g.end_tok[1] = sc[6]; g.end_tok[2] = sc[7]; g.start_pc = sc[8];
+  CHECK(sc.size() >= 8);
+  g.quote = sc[0]; g.zero = sc[1]; g.dot = sc[2]; g.backslash = sc[3]; g.slack = sc[4];
+  g.start_pc = sc[5]; g.ncap = sc[6]; g.cont = sc[7];
+  CHECK(g.fin.size() == g.ops.size() * NPROF);
   return g;
 }
 
@@ -162,7 +173,10 @@ static int grammar_walks(const Grammar& g, const std::vector<uint32_t>& masks, i
   for (int w = 0; w < walks; ++w) {
     std::vector<int32_t> forced;
     int32_t minv = (int32_t)(rng() % 9);
-    State st = g.initial(forced, minv);
+    const int32_t prof = (int32_t)(rng() % 2);
+    // random budgets exercise the close-out; every walk must end inside its budget
+    const int32_t budget = 200 + (int32_t)(rng() % 1001);
+    State st = g.initial(forced, minv, prof, budget);
     int32_t n = (int32_t)forced.size();
     for (int steps = 0;; ++steps) {
       CHECK(steps < 4000);
@@ -177,8 +191,9 @@ static int grammar_walks(const Grammar& g, const std::vector<uint32_t>& masks, i
       CHECK(!allowed.empty());
       int32_t tok = allowed[rng() % allowed.size()];
       forced.clear();
-      CHECK(g.advance(st, tok, forced));
+      CHECK(g.advance(st, tok, forced, budget - n - 1));
       n += 1 + (int32_t)forced.size();
+      CHECK(n <= budget);
     }
     CHECK(g.done(st));
     total += n;
@@ -222,7 +237,8 @@ static void fuzz_engine_core(std::shared_ptr<const Grammar> g, const std::vector
     SeqParams p;
     p.seed = i;
     p.min_items = (int32_t)(rng() % 4);
-    p.max_tokens = 1200;
+    p.profile = (int32_t)(rng() % 2);
+    p.max_tokens = 200 + (int32_t)(rng() % 1001);
     core.add(prompt.data(), (int32_t)prompt.size(), p, 0.0);
   }
   int finished = 0, steps = 0;
@@ -257,7 +273,8 @@ static void fuzz_engine_core(std::shared_ptr<const Grammar> g, const std::vector
     for (int32_t id : done) {
       const Seq& s = core.seq(id);
       CHECK(s.status == S_FINISHED);
-      CHECK(s.finish == F_STOP || s.finish == F_LENGTH);
+      CHECK(s.finish == F_STOP);                     // the close-out always fits the budget
+      CHECK(s.generated() <= s.p.max_tokens);
       core.release(id);
       ++finished;
     }

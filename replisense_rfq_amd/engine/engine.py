@@ -34,7 +34,7 @@ from ..parallel.tp import SINGLE, TPContext
 from ..utils.config import EngineConfig
 from ..utils.faults import FaultInjector
 from ..utils.trace import trace_range
-from .grammar import get_grammar
+from .grammar import PROFILE_REFERENCE, PROFILE_SYNTHETIC, get_grammar
 from .kv_cache import KVCache
 from .runner import EXT_MAX, MAX_GRAPH_TOKENS, TOKEN_MULTS, ModelRunner
 from .sequence import SamplingParams, Sequence, Status
@@ -169,9 +169,7 @@ class LLMEngine:
     # --------------------------------------------------------------- requests
     def add_request(self, prompt_ids: list[int], params: SamplingParams | None = None,
                     callback=None) -> Sequence:
-        params = params or SamplingParams(temperature=self.cfg.temperature,
-                                          max_tokens=self.cfg.max_tokens,
-                                          grammar=self.grammar is not None)
+        params = params or self.default_params()
         if len(prompt_ids) + params.max_tokens > self.cfg.max_model_len:
             params.max_tokens = max(1, self.cfg.max_model_len - len(prompt_ids))
         seq = Sequence(list(prompt_ids), params, callback=callback)
@@ -179,7 +177,7 @@ class LLMEngine:
         seq.core_id = self.core.add(np.asarray(prompt_ids, np.int32), float(params.temperature),
                                     int(params.max_tokens), int(params.seed),
                                     bool(params.grammar and self.grammar is not None),
-                                    int(params.min_items), seq.t_arrival)
+                                    int(params.min_items), int(params.profile), seq.t_arrival)
         self._live[seq.core_id] = seq
         return seq
 
@@ -255,7 +253,7 @@ class LLMEngine:
             if seeds is not None:
                 base = sp or self.default_params()
                 sp = SamplingParams(base.temperature, base.max_tokens, seeds[i], base.grammar,
-                                    base.min_items)
+                                    base.min_items, base.profile)
             seqs.append(self.add_request(p, sp))
         while self.has_work():
             self.step()
@@ -263,7 +261,8 @@ class LLMEngine:
 
     def default_params(self, **kw) -> SamplingParams:
         p = SamplingParams(temperature=self.cfg.temperature, max_tokens=self.cfg.max_tokens,
-                           grammar=self.grammar is not None)
+                           grammar=self.grammar is not None,
+                           profile=PROFILE_SYNTHETIC if self.cfg.decode_hints else PROFILE_REFERENCE)
         for k, v in kw.items():
             setattr(p, k, v)
         return p

@@ -226,12 +226,12 @@ class RouterBackend:
 
     async def acomplete(self, messages):
         from ..service.extract import document_of
-        from ..service.hints import estimate_line_items
+        from ..service.hints import decode_hints_for
 
         ids = self.tokenizer.chat_ids(messages)
         cfg = self.router.cfg
-        params = dict(temperature=cfg.temperature, max_tokens=cfg.max_tokens,
-                      grammar=cfg.grammar, min_items=estimate_line_items(document_of(messages)))
+        params = dict(temperature=cfg.temperature, max_tokens=cfg.max_tokens, grammar=cfg.grammar,
+                      **decode_hints_for(document_of(messages), cfg.decode_hints))
         out = await self.router.generate(ids, params, timeout=cfg.request_timeout_s)
         if out["finish"] in ("engine_error", "grammar_error"):
             raise RuntimeError(f"generation failed: {out['finish']}")

@@ -21,7 +21,9 @@ class SamplingParams:
     max_tokens: int = 1200
     seed: int = 0
     grammar: bool = True
-    min_items: int = 0      # schema hint: minimum line_items the output must contain
+    min_items: int = 0      # bench-only schema hint: minimum line_items the output must contain
+    profile: int = 0        # grammar profile: 0 reference (service default), 1 synthetic
+                            # (bench-only caps for random-init weights; grammar/compiler.py)
 
 
 @dataclass

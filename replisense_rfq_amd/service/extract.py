@@ -253,8 +253,9 @@ def document_of(messages: list[dict]) -> str:
 class EngineBackend:
     """On-node engine backend: chat template -> tokens -> AsyncEngine -> text.
 
-    The document's estimated line-item count (service/hints.py) is passed to the
-    grammar as ``min_items`` so every requested part gets a line_items entry.
+    Requests decode with the grammar's REFERENCE profile (everything the
+    reference's model emits, bounded only by max_tokens).  ``RFQ_DECODE_HINTS=1``
+    switches to the bench-only hints of service/hints.py (random-init weights).
     """
 
     def __init__(self, engine, async_engine=None, timeout_s: float | None = None):
@@ -277,9 +278,10 @@ class EngineBackend:
         return self.tokenizer.decode(seq.output_ids)
 
     def _params(self, messages):
-        from .hints import estimate_line_items
+        from .hints import decode_hints_for
 
-        return self.engine.default_params(min_items=estimate_line_items(document_of(messages)))
+        return self.engine.default_params(
+            **decode_hints_for(document_of(messages), self.engine.cfg.decode_hints))
 
     def complete(self, messages):
         ids = self.tokenizer.chat_ids(messages)

@@ -51,6 +51,8 @@ class EngineConfig:
     gemm_split: bool = True              # + hipBLASLt row-chunk plan for large steps
     custom_allreduce: bool = True        # TP>1 on GPU: xGMI one-/two-shot kernels (self-tested)
     trace: bool = False                  # per-request JSON spans
+    decode_hints: bool = False           # bench-only: SYNTHETIC grammar profile + min_items for
+                                         # random-init weights (service/hints.py); off = reference
 
     @classmethod
     def from_env(cls, **overrides) -> "EngineConfig":
@@ -75,6 +77,7 @@ class EngineConfig:
             decode_tiles=_env("RFQ_DECODE_TILES", cls.decode_tiles, int),
             moe_parallel=_env("RFQ_MOE_PARALLEL", cls.moe_parallel),
             trace=_env("RFQ_TRACE", cls.trace, bool),
+            decode_hints=_env("RFQ_DECODE_HINTS", cls.decode_hints, bool),
         )
         gb = os.environ.get("RFQ_GRAPH_BUCKETS")
         if gb:

@@ -186,9 +186,11 @@ def decode_hints(doc: RFQDoc) -> dict:
     """Bench-only decoding hints for a synthetic document (SamplingParams keywords).
 
     Random-init weights carry no knowledge of when an extraction is complete, so the
-    benchmark shapes each constrained decode like the document's extraction: one
-    ``line_items`` object per part the document mentions (the regex estimate the
-    service used to apply)."""
+    benchmark shapes each constrained decode like the document's extraction: the
+    grammar's SYNTHETIC profile (string / array caps, schema-typed values only) and
+    one ``line_items`` object per part the document mentions.  The service never
+    applies these (it decodes with the REFERENCE profile)."""
+    from ..engine.grammar import PROFILE_SYNTHETIC
     from ..service.hints import estimate_line_items
 
-    return {"min_items": estimate_line_items(doc.text)}
+    return {"min_items": estimate_line_items(doc.text), "profile": PROFILE_SYNTHETIC}

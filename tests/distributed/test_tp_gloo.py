@@ -69,7 +69,8 @@ def _engine_worker(rank, world, port, q, control="shm"):
     from replisense_rfq_amd.utils.config import EngineConfig
 
     tp = init_distributed("gloo")
-    eng = LLMEngine(EngineConfig(model="tiny-llama-tp", device="cpu", max_num_seqs=4), tp=tp)
+    eng = LLMEngine(EngineConfig(model="tiny-llama-tp", device="cpu", max_num_seqs=4,
+                                 decode_hints=True), tp=tp)
     assert (eng.runner.ring is not None) == (control == "shm")
     if tp.rank == 0:
         prompts = [eng.tokenizer.chat_ids(build_messages(synth.make_rfq(i).text)) for i in range(2)]

@@ -55,7 +55,7 @@ def test_engine_serves_from_checkpoint_dir(tmp_path):
     with gzip.open(_DIR / "llama3_synth.json.gz", "rb") as f:
         (tmp_path / "tokenizer.json").write_bytes(f.read())
     eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=2,
-                                 weights_path=str(tmp_path)))
+                                 weights_path=str(tmp_path), decode_hints=True))
     assert torch.equal(eng.model.w["layers"][1]["down"], full["layers"][1]["down"])
     ids = eng.tokenizer.chat_ids(build_messages(synth.make_rfq(5).text))
     s, = eng.generate([ids])

@@ -20,7 +20,7 @@ from replisense_rfq_amd.utils.config import EngineConfig
 @pytest.fixture(scope="module")
 def engine():
     return LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4,
-                                  max_batched_tokens=2048))
+                                  max_batched_tokens=2048, decode_hints=True))
 
 
 def _prompts(eng, n, base=0):
@@ -82,7 +82,7 @@ def test_min_items_hint(engine):
 
 def test_chunked_prefill_and_preemption():
     cfg = EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4, max_batched_tokens=96,
-                       max_kv_blocks=60, prefix_cache=False)
+                       max_kv_blocks=60, prefix_cache=False, decode_hints=True)
     eng = LLMEngine(cfg)
     seqs = eng.generate(_prompts(eng, 4, base=40))
     for s in seqs:
@@ -119,8 +119,8 @@ def test_core_sections_and_layout():
     core = _core()
     h = np.zeros(HEADER, np.int32)
     buf = np.zeros(core.payload_bound(), np.int32)
-    a = core.add(np.arange(100, 400, dtype=np.int32), 0.5, 50, 11, False, 0, 0.0)
-    b = core.add(np.arange(1, 11, dtype=np.int32), 0.5, 50, 12, False, 0, 0.0)
+    a = core.add(np.arange(100, 400, dtype=np.int32), 0.5, 50, 11, False, 0, 0, 0.0)
+    b = core.add(np.arange(1, 11, dtype=np.int32), 0.5, 50, 12, False, 0, 0, 0.0)
     n = core.schedule_and_pack(h, buf, 0.0)
     assert n == h[H_PAYLOAD] > 0
     assert (h[H_T], h[H_TA], h[H_NA], h[H_NB], h[H_S]) == (310, 10, 1, 1, 2)
@@ -153,10 +153,10 @@ def test_core_prefix_cache_and_preemption():
     h = np.zeros(16, np.int32)
     buf = np.zeros(core.payload_bound(), np.int32)
     prompt = np.arange(1, 300, dtype=np.int32)
-    a = core.add(prompt, 0.1, 600, 1, False, 0, 0.0)
+    a = core.add(prompt, 0.1, 600, 1, False, 0, 0, 0.0)
     core.schedule_and_pack(h, buf, 0.0)
     core.post(np.array([9], np.int32), 0.0)
-    b = core.add(prompt, 0.1, 600, 2, False, 0, 0.0)          # shares 9 full prompt blocks
+    b = core.add(prompt, 0.1, 600, 2, False, 0, 0, 0.0)          # shares 9 full prompt blocks
     core.schedule_and_pack(h, buf, 0.0)
     core.post(np.array([9, 9], np.int32), 0.0)
     assert core.info(b)["prefix_hit"] == 9 * 32 and core.prefix_hits >= 1
@@ -187,3 +187,19 @@ def test_async_engine_and_extract_service(engine):
         aeng.shutdown()
     for o in outs:
         assert o["success"] is True and o["message"] == "RFQ processed from mail"
+
+
+def test_reference_profile_closes_inside_budget(engine):
+    """The service default (REFERENCE profile, no hints): random weights never close
+    a string by themselves, so the token-budget close-out must end every output as
+    parseable JSON within max_tokens -- finish 'stop', never 'length'."""
+    from replisense_rfq_amd.engine.grammar import PROFILE_REFERENCE
+    from replisense_rfq_amd.service.extract import parse_and_validate_response
+
+    p = _prompts(engine, 2, base=50)
+    seqs = engine.generate(p, engine.default_params(profile=PROFILE_REFERENCE, max_tokens=300))
+    for s in seqs:
+        assert s.finish_reason == "stop" and len(s.output_ids) <= 300
+        text = engine.decode_text(s)
+        json.loads(text)
+        assert parse_and_validate_response(text, "direct_text_input")["success"] is True

@@ -75,7 +75,7 @@ def test_sequence_parallel_layout_matches_forward(gpu, name):
 
 def _engine(graphs: bool, model="tiny-llama"):
     cfg = EngineConfig(model=model, max_num_seqs=16, use_graphs=graphs, max_kv_blocks=4096,
-                       graph_buckets=(1, 2, 4, 8, 16))
+                       graph_buckets=(1, 2, 4, 8, 16), decode_hints=True)
     return LLMEngine(cfg)
 
 

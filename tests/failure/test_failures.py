@@ -18,7 +18,8 @@ from replisense_rfq_amd.utils.faults import FaultInjector
 
 
 def _cfg(**kw):
-    base = dict(model="tiny-llama", device="cpu", max_num_seqs=4, max_batched_tokens=2048)
+    base = dict(model="tiny-llama", device="cpu", max_num_seqs=4, max_batched_tokens=2048,
+                decode_hints=True)
     base.update(kw)
     return EngineConfig(**base)
 
@@ -82,7 +83,7 @@ def test_router_replica_crash_is_restarted(monkeypatch):
     try:
         eng_tok = router.backend().tokenizer
         ids = eng_tok.chat_ids(build_messages(synth.make_rfq(1).text))
-        params = dict(temperature=0.1, max_tokens=1200, grammar=True, min_items=0)
+        params = dict(temperature=0.1, max_tokens=1200, grammar=True, min_items=0, profile=1)
         out = asyncio.run(router.generate(ids, params, timeout=300))
         assert out["finish"] == "stop"
         RFQResponse(**json.loads(out["text"]))

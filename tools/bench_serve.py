@@ -149,7 +149,9 @@ def main():
     url = f"http://127.0.0.1:{a.port}"
     env = dict(os.environ, RFQ_BACKEND="engine", RFQ_MODEL=a.model, ENVIRONMENT="production",
                RFQ_PARSER_PROCS=str(a.parser_procs),
-               RFQ_MAX_BATCH=str(a.max_batch), LOG_LEVEL="warning", PYTHONUNBUFFERED="1")
+               RFQ_MAX_BATCH=str(a.max_batch), LOG_LEVEL="warning", PYTHONUNBUFFERED="1",
+               # random-init weights: the bench-only decoding hints (service/hints.py)
+               RFQ_DECODE_HINTS=os.environ.get("RFQ_DECODE_HINTS", "1"))
     log = open(os.path.join(ROOT, "gpurun_out", "bench_serve_server.log")
                if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else os.devnull, "w")
     proc = subprocess.Popen([sys.executable, "-m", "replisense_rfq_amd.api.serve", "--host",
