@@ -1,13 +1,20 @@
-"""Data-parallel router: one engine replica per GPU (or TP group) in its own process.
+"""Data-parallel router: engine replicas (each a TP group of processes) behind
+one dispatcher.
 
-SURVEY.md §2.3 DP row: whole-node docs/s with Llama-3-8B TP=1 = 8 independent
-replicas behind a router.  Each worker process is pinned to its devices through
-``HIP_VISIBLE_DEVICES`` *before* torch initialises HIP (spawned, never forked
-from a GPU-initialised parent), builds an ``LLMEngine`` and serves requests from
-a multiprocessing queue; the API process keeps one dispatcher thread that
-resolves asyncio futures.  Routing is least-outstanding-tokens.  If a worker
-dies, its in-flight requests fail (-> HTTP 500 "RFQ processing failed", the
-reference semantics for exceptions escaping the generator) and the replica is
+SURVEY.md §2.3: whole-node docs/s with Llama-3-8B TP=1 = 8 independent replicas
+(DP=8); Llama-3-70B = one replica of TP=8 over RCCL/xGMI (the reference's own
+model, ``llama3-70b-8192``, rfq_agent.py:62).  ``RFQ_DP`` x ``RFQ_TP`` processes
+are spawned (never forked from a GPU-initialised parent), one per GPU.  Every
+process of replica r sees the replica's devices through ``HIP_VISIBLE_DEVICES``
+(set before torch initialises HIP) and joins the replica's own process group
+(``init_process_group``: RCCL on GPUs, gloo on CPU; 127.0.0.1 rendezvous on a
+per-replica port).  TP rank 0 builds the ``LLMEngine`` scheduler and serves
+requests from a multiprocessing queue; TP ranks > 0 mirror its steps
+(``LLMEngine.worker_loop``, shared-memory control plane).  The API process keeps
+one dispatcher thread that resolves asyncio futures.  Routing is
+least-outstanding-tokens.  If any process of a replica dies, the replica's
+in-flight requests fail (-> HTTP 500 "RFQ processing failed", the reference
+semantics for exceptions escaping the generator) and the whole TP group is
 restarted.
 """
 from __future__ import annotations
@@ -24,16 +31,51 @@ import time
 log = logging.getLogger("replisense_rfq_amd.router")
 
 
-def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _join_group(devices: str, tp_rank: int, tp: int, port: int):
+    """Pin this process to the replica's devices and (TP > 1) join the replica's
+    process group.  Runs before anything touches HIP."""
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices
+    if tp <= 1:
+        from ..parallel.tp import SINGLE
+
+        return SINGLE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(tp_rank),
+                      WORLD_SIZE=str(tp), LOCAL_RANK=str(tp_rank))
+    from ..parallel.tp import init_distributed
+
+    return init_distributed()
+
+
+def _follower(idx: int, devices: str, tp_rank: int, tp: int, port: int, cfg_dict: dict):
+    """TP rank > 0 of replica `idx`: mirror rank 0's steps until it stops."""
+    ctx = _join_group(devices, tp_rank, tp, port)
+    from ..utils.config import EngineConfig
+    from .engine import LLMEngine
+
+    eng = LLMEngine(EngineConfig(**cfg_dict), tp=ctx)
+    eng.worker_loop()
+
+
+def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port: int = 0):
+    ctx = _join_group(devices, 0, tp, port)
     from ..utils.config import EngineConfig
     from ..utils.faults import FaultInjector
     from .engine import LLMEngine
     from .sequence import SamplingParams
 
     cfg = EngineConfig(**cfg_dict)
-    eng = LLMEngine(cfg)
+    eng = LLMEngine(cfg, tp=ctx)
     exit_after = FaultInjector().replica_exit_after()
     outq.put(("ready", idx, None))
     pending = {}
@@ -43,6 +85,7 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq):
             while True:
                 msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
                 if msg is None:
+                    eng.shutdown()                 # release the TP followers
                     return
                 if msg[0] == "abort":               # the client's deadline expired
                     for sid, (r, s) in list(pending.items()):
@@ -80,11 +123,15 @@ class DPRouter:
         self.cfg = cfg
         self.n = n_replicas
         self.dpr = devices_per_replica
+        self.tp = max(1, int(cfg.tp))
+        if self.tp > 1 and self.dpr != self.tp:
+            raise ValueError(f"TP={self.tp} replicas need {self.tp} devices each")
         self.restart = restart
         self.ctx = mp.get_context("spawn")
         self.outq = self.ctx.Queue()
         self.inqs = [None] * n_replicas
-        self.procs = [None] * n_replicas
+        self.procs = [None] * n_replicas          # TP rank 0 (the engine loop)
+        self.followers: list[list] = [[] for _ in range(n_replicas)]
         self.ready = [False] * n_replicas
         self.load = [0] * n_replicas
         self.where: dict[int, int] = {}
@@ -106,14 +153,39 @@ class DPRouter:
         self._thread = threading.Thread(target=self._dispatch, daemon=True)
         self._thread.start()
 
+    def _devices(self, i: int) -> str:
+        """HIP_VISIBLE_DEVICES of replica i (``RFQ_DEVICES`` remaps physical ids)."""
+        if self.cfg.device == "cpu":
+            return ""
+        phys = os.environ.get("RFQ_DEVICES")
+        ids = [int(x) for x in phys.split(",")] if phys else None
+        devs = [i * self.dpr + j for j in range(self.dpr)]
+        return ",".join(str(ids[d] if ids else d) for d in devs)
+
     def _spawn(self, i: int) -> None:
-        devs = ",".join(str(i * self.dpr + j) for j in range(self.dpr)) \
-            if self.cfg.device != "cpu" else ""
+        devs = self._devices(i)
+        port = _free_port() if self.tp > 1 else 0
         q = self.ctx.Queue()
-        p = self.ctx.Process(target=_worker, args=(i, devs, self._cfg_dict, q, self.outq),
+        p = self.ctx.Process(target=_worker,
+                             args=(i, devs, self._cfg_dict, q, self.outq, self.tp, port),
                              daemon=True)
         p.start()
+        fol = []
+        for r in range(1, self.tp):
+            f = self.ctx.Process(target=_follower,
+                                 args=(i, devs, r, self.tp, port, self._cfg_dict), daemon=True)
+            f.start()
+            fol.append(f)
         self.inqs[i], self.procs[i], self.ready[i] = q, p, False
+        self.followers[i] = fol
+
+    def _kill_replica(self, i: int) -> None:
+        for f in [self.procs[i], *self.followers[i]]:
+            if f is not None and f.is_alive():
+                f.kill()
+        for f in [self.procs[i], *self.followers[i]]:
+            if f is not None:
+                f.join(timeout=10)
 
     def _dispatch(self):
         while not self._stop:
@@ -138,9 +210,14 @@ class DPRouter:
 
     def _check_workers(self):
         for i, p in enumerate(self.procs):
-            if p is None or p.is_alive() or self._stop:
+            if p is None or self._stop:
                 continue
-            log.error("replica %d died (exit %s); failing its requests", i, p.exitcode)
+            dead = [x for x in [p, *self.followers[i]] if not x.is_alive()]
+            if not dead:
+                continue
+            log.error("replica %d: process %s died (exit %s); failing its requests", i,
+                      dead[0].pid, dead[0].exitcode)
+            self._kill_replica(i)                  # a TP group cannot run with a rank missing
             with self._lock:
                 self.ready[i] = False
                 dead = [rid for rid, r in self.where.items() if r == i]
@@ -190,7 +267,8 @@ class DPRouter:
         return RouterBackend(self)
 
     def stats(self) -> dict:
-        return {"replicas": self.n, "ready": sum(self.ready), "restarts": self.restarts,
+        return {"replicas": self.n, "tp": self.tp, "ready": sum(self.ready),
+                "restarts": self.restarts,
                 "outstanding": len(self.where), "load": list(self.load),
                 "completed": self.completed}
 
@@ -199,9 +277,13 @@ class DPRouter:
         for q, p in zip(self.inqs, self.procs):
             if p is not None and p.is_alive():
                 q.put(None)
-        for p in self.procs:
+        for i, p in enumerate(self.procs):
             if p is not None:
-                p.join(timeout=10)
+                p.join(timeout=30)
+            for f in self.followers[i]:
+                f.join(timeout=30)
+                if f.is_alive():
+                    f.kill()
 
 
 class RouterBackend:
@@ -239,10 +321,11 @@ class RouterBackend:
 
 
 def maybe_router(cfg):
-    """A DPRouter when RFQ_DP > 1 (replicas of cfg.tp devices each) or when the
-    single engine should live in its own process (RFQ_ENGINE_PROCESS=1: the API
-    process then only parses HTTP, tokenises and validates), else None."""
+    """A DPRouter when RFQ_DP > 1 or RFQ_TP > 1 (replicas of cfg.tp processes/devices
+    each) or when the single engine should live in its own process
+    (RFQ_ENGINE_PROCESS=1: the API process then only parses HTTP, tokenises and
+    validates), else None."""
     own_process = os.environ.get("RFQ_ENGINE_PROCESS", "0").lower() in ("1", "true", "on")
-    if cfg.dp <= 1 and not own_process:
+    if cfg.dp <= 1 and cfg.tp <= 1 and not own_process:
         return None
     return DPRouter(cfg, max(1, cfg.dp), max(1, cfg.tp))

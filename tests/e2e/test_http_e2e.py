@@ -54,7 +54,7 @@ def _stop(proc):
         os.killpg(proc.pid, signal.SIGKILL)
 
 
-def _exercise(url, n=16):
+def _exercise(url, n=16, validate=True):
     import httpx
 
     from replisense_rfq_amd.service.schema import RFQResponse
@@ -67,7 +67,8 @@ def _exercise(url, n=16):
         assert body["success"] is True and body["message"] == "Successfully processed text input"
         data = body["data"]
         assert data["parsing_info"]["input_type"] == "direct_text"
-        RFQResponse(**{k: v for k, v in data.items() if k != "parsing_info"})
+        if validate:
+            RFQResponse(**{k: v for k, v in data.items() if k != "parsing_info"})
         return data
 
     with cf.ThreadPoolExecutor(8) as ex:
@@ -94,10 +95,46 @@ def test_http_mock_backend():
 
 @pytest.mark.gpu
 def test_http_engine_backend(gpu):
+    """The service default: REFERENCE grammar profile, no decoding hints (random
+    weights then fill strings until the token-budget close-out): every response is
+    the reference's success envelope (validated or fallback dict)."""
     proc, url = _serve({"RFQ_BACKEND": "engine", "RFQ_MODEL": "tiny-llama", "RFQ_MAX_BATCH": "16",
                         "RFQ_KV_FRACTION": "0.05"})
     try:
-        outs = _exercise(url, n=12)
+        outs = _exercise(url, n=12, validate=False)
         assert all(o["success"] for o in outs)
+    finally:
+        _stop(proc)
+
+
+@pytest.mark.gpu
+def test_http_engine_process_router(gpu):
+    """The router spawn path on the GPU: the engine in its own process
+    (RFQ_ENGINE_PROCESS=1), pinned through HIP_VISIBLE_DEVICES."""
+    proc, url = _serve({"RFQ_BACKEND": "engine", "RFQ_MODEL": "tiny-llama", "RFQ_MAX_BATCH": "16",
+                        "RFQ_KV_FRACTION": "0.05", "RFQ_ENGINE_PROCESS": "1",
+                        "RFQ_DECODE_HINTS": "1"})
+    try:
+        outs = _exercise(url, n=8)
+        assert all(o["success"] for o in outs)
+    finally:
+        _stop(proc)
+
+
+def test_http_tensor_parallel_replica_cpu():
+    """RFQ_TP=2 through the served API: the router spawns one TP group (rank 0 = the
+    engine loop, rank 1 = follower) joined over gloo; /parse-text/ and /upload/
+    return the reference envelopes.  (On GPUs the same path uses RCCL; SURVEY.md
+    §2.3, BASELINE config 4.)"""
+    proc, url = _serve({"RFQ_BACKEND": "engine", "RFQ_MODEL": "tiny-llama-tp", "RFQ_TP": "2",
+                        "RFQ_DEVICE": "cpu", "RFQ_MAX_BATCH": "4", "RFQ_DECODE_HINTS": "1",
+                        "RFQ_GRAPHS": "0", "OMP_NUM_THREADS": "2"})
+    try:
+        import httpx
+
+        outs = _exercise(url, n=3)
+        assert all(o["success"] for o in outs)
+        m = httpx.get(url + "/metrics", timeout=10).json()
+        assert m["data"]["router"]["tp"] == 2 and m["data"]["router"]["ready"] == 1
     finally:
         _stop(proc)
