@@ -218,6 +218,11 @@ class DPRouter:
             log.error("replica %d: process %s died (exit %s); failing its requests", i,
                       dead[0].pid, dead[0].exitcode)
             self._kill_replica(i)                  # a TP group cannot run with a rank missing
+            if self.tp > 1 and self._cfg_dict.get("custom_allreduce"):
+                # a TP replica failed: restart it on RCCL all-reduces only (the custom
+                # xGMI kernel fails a step on a flag timeout, see runner.py)
+                log.error("replica %d restarts with custom all-reduce disabled", i)
+                self._cfg_dict = dict(self._cfg_dict, custom_allreduce=False)
             with self._lock:
                 self.ready[i] = False
                 dead = [rid for rid, r in self.where.items() if r == i]

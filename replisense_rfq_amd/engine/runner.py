@@ -252,6 +252,14 @@ class ModelRunner:
             logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
+        car = self.tp.car
+        if car is not None and car.errors():
+            # a peer's flag never arrived inside the kernel's bounded spin: the sums of
+            # this step may be stale.  Fail the step (its requests get engine_error);
+            # on a TP follower this ends the process and the router restarts the
+            # replica with RCCL all-reduces (router.py).
+            raise RuntimeError(f"custom all-reduce: {car.errors()} flag timeouts on TP rank "
+                               f"{self.tp.rank}; results of this step are unreliable")
         self.stats["steps"] += 1
         self.stats["graph_steps"] += bool(key[0])
         self.stats["tokens"] += int(header[H_T])

@@ -61,11 +61,16 @@ TINY_LLAMA = ModelConfig("tiny-llama", hidden=512, n_layers=2, n_heads=4, n_kv_h
                          ffn=1024, max_position=8192)
 TINY_LLAMA_TP = ModelConfig("tiny-llama-tp", hidden=512, n_layers=2, n_heads=8, n_kv_heads=2,
                             ffn=1024, max_position=8192)
+# Llama-3-70B's per-rank attention shape at TP=8 (Hq=64, Hkv=8 -> 8 q heads and ONE kv
+# head per rank, GQA group 8) on a 2-layer, 512-wide body: the CPU/gloo rehearsal of
+# BASELINE config 4 (tests/distributed/test_tp_gloo.py, test_bench_cli.py).
+TINY_LLAMA70 = ModelConfig("tiny-llama70", hidden=512, n_layers=2, n_heads=64, n_kv_heads=8,
+                           ffn=1024, max_position=8192)
 TINY_MIXTRAL = replace(MIXTRAL_8X7B, name="tiny-mixtral", hidden=512, n_layers=2, n_heads=4,
                        n_kv_heads=1, ffn=512, vocab_size=32000)
 
 CONFIGS = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_LLAMA, TINY_LLAMA_TP,
-                                TINY_MIXTRAL)}
+                                TINY_LLAMA70, TINY_MIXTRAL)}
 ALIASES = {"llama3-70b-8192": "llama3-70b", "8b": "llama3-8b", "70b": "llama3-70b",
            "mixtral": "mixtral-8x7b"}
 

@@ -12,6 +12,9 @@ memory.  Messages above the staging capacity go to RCCL.
 
 The kernel's spins are bounded; :meth:`CustomAllReduce.errors` reads the
 timeout counter so a broken peer path is detected instead of hanging the GPU.
+The model runner reads it after every step (one 4-byte copy behind the step's
+existing sync) and fails the step on a non-zero count (engine/runner.py); the
+router then restarts the TP replica on RCCL (engine/router.py).
 """
 from __future__ import annotations
 

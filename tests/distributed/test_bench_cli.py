@@ -25,8 +25,8 @@ def _port():
     return p
 
 
-def _run(cmd, timeout=600):
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+def _run(cmd, timeout=600, threads=2):
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
     env.pop("WORLD_SIZE", None)
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -45,6 +45,18 @@ def test_bench_torchrun_gloo(tp, par):
                 str(_port()), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
                 "--model", model, "--tp", str(tp)] + SMALL)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == par
+    assert out["per_doc"]["valid"] == 1.0 and out["p50_parse_text_latency_s"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_bench_tp8_gloo():
+    """`bench.py --gpus 8 --tp 8` -- the driver's 70B layout (one TP=8 replica) -- on 8
+    gloo ranks with the 70B-shaped tiny model (per-rank Hq=8, Hkv=1)."""
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                str(_port()), "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama70", "--tp", "8"] + SMALL, timeout=800, threads=1)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp1-tp8"
     assert out["per_doc"]["valid"] == 1.0 and out["p50_parse_text_latency_s"] > 0
 
 

@@ -87,7 +87,7 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e), -1))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_multiprocess(gpu, world):
     import torch.multiprocessing as mp
 
@@ -97,7 +97,7 @@ def test_custom_allreduce_multiprocess(gpu, world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=300) for _ in range(world)]
+    results = [q.get(timeout=600) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     for rank, errs, nerr in results:

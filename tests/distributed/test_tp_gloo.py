@@ -1,6 +1,7 @@
-"""Tensor parallelism on CPU over gloo (world_size 2): sharded forward == TP=1
-forward, and the TP engine (rank-0 scheduler + metadata broadcast + vocab-parallel
-sampler) produces valid RFQ JSON."""
+"""Tensor parallelism on CPU over gloo: sharded forward == TP=1 forward, and the TP
+engine (rank-0 scheduler + metadata broadcast + vocab-parallel sampler) produces
+valid RFQ JSON.  World sizes 2, 4 and 8; ``tiny-llama70`` has Llama-3-70B's per-rank
+attention shape at TP=8 (8 q heads, one kv head, GQA group 8)."""
 import json
 import os
 import socket
@@ -19,22 +20,24 @@ def _port():
     return p
 
 
-def _forward_worker(rank, world, port, q, sp=False):
+def _forward_worker(rank, world, port, q, sp=False, model=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
+    torch.set_num_threads(max(1, 8 // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from replisense_rfq_amd.models.config import get_config
     from replisense_rfq_amd.models.llama import DecoderLM, ForwardMeta
     from replisense_rfq_amd.models.weights import init_weights, shard_weights
     from replisense_rfq_amd.parallel.tp import SINGLE, TPContext
 
-    cfg = get_config("tiny-llama").__class__(**{**get_config("tiny-llama").to_dict(),
-                                                "n_kv_heads": 2, "name": "tiny-tp"})
+    cfg = get_config(model) if model else \
+        get_config("tiny-llama").__class__(**{**get_config("tiny-llama").to_dict(),
+                                              "n_kv_heads": 2, "name": "tiny-tp"})
     full = init_weights(cfg, SINGLE, "cpu", seed=11)
     tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
     m = DecoderLM(cfg, "cpu", tp=tp, weights=shard_weights(full, cfg, tp))
     m.sp_min_tokens = 1 if sp else 0
-    T, nb = (39 if sp else 40), 4  # 39: SP pads the last rank's row shard
+    T, nb = (39 if sp else 40), 4  # 39: SP pads the last rank's row shard (any world)
     shape = (cfg.n_layers, nb, m.hkv, 32, 128)
     m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16), torch.zeros(shape, dtype=torch.bfloat16))
     g = torch.Generator().manual_seed(0)
@@ -59,9 +62,10 @@ def _forward_worker(rank, world, port, q, sp=False):
     dist.destroy_process_group()
 
 
-def _engine_worker(rank, world, port, q, control="shm"):
+def _engine_worker(rank, world, port, q, control="shm", model="tiny-llama-tp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), RFQ_TP_CONTROL=control)
+    torch.set_num_threads(max(1, 8 // world))
     from replisense_rfq_amd.engine.engine import LLMEngine
     from replisense_rfq_amd.parallel.tp import init_distributed
     from replisense_rfq_amd.service.prompt import build_messages
@@ -69,7 +73,7 @@ def _engine_worker(rank, world, port, q, control="shm"):
     from replisense_rfq_amd.utils.config import EngineConfig
 
     tp = init_distributed("gloo")
-    eng = LLMEngine(EngineConfig(model="tiny-llama-tp", device="cpu", max_num_seqs=4,
+    eng = LLMEngine(EngineConfig(model=model, device="cpu", max_num_seqs=4,
                                  decode_hints=True), tp=tp)
     assert (eng.runner.ring is not None) == (control == "shm")
     if tp.rank == 0:
@@ -163,4 +167,35 @@ def test_tp2_engine_valid_json(control):
     from replisense_rfq_amd.service.schema import RFQResponse
 
     for text in q.get(timeout=10):
+        RFQResponse(**json.loads(text))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,sp", [(4, False), (8, False), (8, True)])
+def test_tp_70b_shape_forward_matches_tp1(world, sp):
+    """Llama-3-70B's TP=8 per-rank layout (Hq_local=8, Hkv_local=1, G=8) and TP=4
+    (Hkv_local=2): sharded logits == single-device logits, also with the
+    sequence-parallel residual stream split 8 ways (odd T padded)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    mp.start_processes(_forward_worker, args=(world, port, q, sp, "tiny-llama70"), nprocs=world,
+                       start_method="spawn")
+    assert q.get(timeout=10) < 0.02
+
+
+@pytest.mark.timeout(900)
+def test_tp8_engine_vocab_parallel_sampler():
+    """The 8-rank TP engine on the 70B-shaped model: rank-0 scheduler, shared-memory
+    control plane to 7 followers, vocab sharded 8 ways (each rank samples its 16,032-
+    token shard; the (value, index) partials are all-gathered) -> valid RFQ JSON."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    mp.start_processes(_engine_worker, args=(8, port, q, "shm", "tiny-llama70"), nprocs=8,
+                       start_method="spawn")
+    from replisense_rfq_amd.service.schema import RFQResponse
+
+    texts = q.get(timeout=10)
+    for text in texts:
         RFQResponse(**json.loads(text))
