@@ -250,6 +250,20 @@ int32_t EngineCore::decode_splits(int32_t na, int32_t max_ctx, bool graph) const
   return s;
 }
 
+int32_t EngineCore::pin_prefix(const int32_t* tokens, int32_t n) {
+  const int32_t bs = cfg_.block_size, nfull = n / bs;
+  std::vector<uint64_t> hashes(nfull);
+  uint64_t h = 0;
+  for (int32_t i = 0; i < nfull; ++i) {
+    h = BlockManager::hash_block(h, tokens + (int64_t)i * bs, bs);
+    hashes[i] = h;
+  }
+  std::vector<int32_t> got;
+  bm_.match_prefix(hashes.data(), nfull, got);   // +1 reference each, never released
+  pinned_.insert(pinned_.end(), got.begin(), got.end());
+  return (int32_t)got.size();
+}
+
 void EngineCore::set_graph_keys(const std::vector<std::pair<int32_t, int32_t>>& keys) {
   graph_keys_ = keys;
   std::sort(graph_keys_.begin(), graph_keys_.end());

@@ -118,6 +118,12 @@ class EngineCore {
   std::vector<int32_t> drain_finished();
 
   void set_graph_keys(const std::vector<std::pair<int32_t, int32_t>>& keys);
+  // Pin the cached full blocks of `tokens` (a prompt prefix whose KV is already
+  // published, e.g. by a warm-up prefill): they hold a reference for the engine's
+  // lifetime, so the shared prompt template is never evicted.  Returns the number
+  // of blocks pinned.
+  int32_t pin_prefix(const int32_t* tokens, int32_t n);
+  int32_t num_pinned() const { return (int32_t)pinned_.size(); }
 
   // --- inspection
   const Seq& seq(int32_t id) const { return seqs_[id]; }
@@ -157,6 +163,7 @@ class EngineCore {
   std::vector<std::pair<int32_t, bool>> rows_;             // (seq, samples) per logits row
   std::vector<int32_t> scratch_;
   std::vector<int32_t> finished_;
+  std::vector<int32_t> pinned_;
 };
 
 }  // namespace rfqrt

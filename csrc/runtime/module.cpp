@@ -225,6 +225,10 @@ PYBIND11_MODULE(_runtime, m) {
       })
       .def("release", &EngineCore::release)
       .def("set_graph_keys", &EngineCore::set_graph_keys)
+      .def("pin_prefix", [](EngineCore& e, arr<int32_t> tokens) {
+        return e.pin_prefix(tokens.data(), (int32_t)tokens.size());
+      })
+      .def_property_readonly("num_pinned", &EngineCore::num_pinned)
       .def("payload_bound", &EngineCore::payload_bound)
       .def("tokens", [](const EngineCore& e, int32_t id) {
         const Seq& s = e.seq(id);

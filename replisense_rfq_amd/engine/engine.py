@@ -109,6 +109,26 @@ class LLMEngine:
         self.step_times: list[float] = []
         self.timers = {"execute_s": 0.0, "post_s": 0.0}
         self.faults = FaultInjector()
+        self.pinned_blocks = 0
+        if self.cfg.prefix_cache and self.cfg.warm_prefix and tp.rank == 0:
+            self.warm_prefix()
+
+    def warm_prefix(self, ids: list[int] | None = None) -> int:
+        """prefill the shared system + template prefix once
+        at start-up and pin its KV blocks, so the first wave of requests already
+        hits the prefix cache and the template can never be evicted under load.
+        TP followers mirror the warm-up step like any other."""
+        if ids is None:
+            from ..service.prompt import shared_prefix_ids
+
+            ids = shared_prefix_ids(self.tokenizer)
+        if len(ids) < 2 * self.kv.block_size:
+            return 0
+        # prompt = prefix + 1 token so every full prefix block is computed and published
+        params = SamplingParams(temperature=0.0, max_tokens=1, grammar=False)
+        self.generate([list(ids) + [ids[-1]]], params)
+        self.pinned_blocks = int(self.core.pin_prefix(np.asarray(ids, np.int32)))
+        return self.pinned_blocks
 
     # ------------------------------------------------------------------ setup
     def _tokenizer_path(self) -> str | None:
@@ -284,6 +304,7 @@ class LLMEngine:
         st.update({k: round(v, 3) for k, v in self.timers.items()})
         st.update(self.kv.stats(self.core))
         st["preempted"] = self.core.num_preempted
+        st["pinned_blocks"] = self.core.num_pinned
         st["running"] = self.core.num_running
         st["waiting"] = self.core.num_waiting
         return st

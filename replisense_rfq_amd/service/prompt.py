@@ -86,3 +86,15 @@ def build_user_message(raw_text: str) -> str:
 def build_messages(raw_text: str) -> list[dict]:
     return [{"role": "system", "content": SYSTEM_MESSAGE},
             {"role": "user", "content": build_user_message(truncate(raw_text))}]
+
+
+def shared_prefix_ids(tokenizer) -> list[int]:
+    """Token ids every extraction prompt starts with (system message + chat
+    template + EXTRACTION_PROMPT_TEMPLATE up to the document): the longest common
+    prefix of two prompts that differ only in their document."""
+    a = tokenizer.chat_ids(build_messages("A"))
+    b = tokenizer.chat_ids(build_messages("Z"))
+    n = 0
+    while n < min(len(a), len(b)) and a[n] == b[n]:
+        n += 1
+    return a[:n]

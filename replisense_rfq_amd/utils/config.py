@@ -51,6 +51,7 @@ class EngineConfig:
     gemm_split: bool = True              # + hipBLASLt row-chunk plan for large steps
     custom_allreduce: bool = True        # TP>1 on GPU: xGMI one-/two-shot kernels (self-tested)
     trace: bool = False                  # per-request JSON spans
+    warm_prefix: bool = True             # prefill + pin the shared prompt template at start-up
     decode_hints: bool = False           # bench-only: SYNTHETIC grammar profile + min_items for
                                          # random-init weights (service/hints.py); off = reference
 
@@ -77,6 +78,7 @@ class EngineConfig:
             decode_tiles=_env("RFQ_DECODE_TILES", cls.decode_tiles, int),
             moe_parallel=_env("RFQ_MOE_PARALLEL", cls.moe_parallel),
             trace=_env("RFQ_TRACE", cls.trace, bool),
+            warm_prefix=_env("RFQ_WARM_PREFIX", cls.warm_prefix, bool),
             decode_hints=_env("RFQ_DECODE_HINTS", cls.decode_hints, bool),
         )
         gb = os.environ.get("RFQ_GRAPH_BUCKETS")

@@ -203,3 +203,17 @@ def test_reference_profile_closes_inside_budget(engine):
         text = engine.decode_text(s)
         json.loads(text)
         assert parse_and_validate_response(text, "direct_text_input")["success"] is True
+
+
+def test_shared_prefix_warm_and_pinned(engine):
+    """the shared system + template prefix is prefilled at
+    start-up and its blocks pinned; the first request already hits it."""
+    from replisense_rfq_amd.service.prompt import shared_prefix_ids
+
+    n = len(shared_prefix_ids(engine.tokenizer))
+    assert engine.pinned_blocks == n // engine.kv.block_size > 0
+    hits0 = engine.core.prefix_hits
+    s, = engine.generate(_prompts(engine, 1, base=90))
+    assert s.prefix_hit_tokens >= engine.pinned_blocks * engine.kv.block_size
+    assert engine.core.prefix_hits > hits0
+    assert engine.stats()["pinned_blocks"] == engine.pinned_blocks
