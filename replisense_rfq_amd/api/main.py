@@ -41,8 +41,10 @@ from fastapi.responses import JSONResponse
 
 from ..service.extract import ExtractService
 from ..service.parser import FileParser, FileParsingError
-from .multipart import MultipartError, missing_field_detail, parse_form
+from ..utils.dotenv import load_dotenv
+from .multipart import MultipartError, MultipartStream, missing_field_detail
 
+load_dotenv()                              # app/main.py:23 (before the constants below)
 logging.basicConfig(level=logging.INFO,
                     format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
 logger = logging.getLogger("replisense_rfq_amd.api")
@@ -199,11 +201,20 @@ def validate_file_size(file) -> bool:
     return True
 
 
+def _copy_to(src, destination: Path) -> None:
+    src.seek(0)
+    with open(destination, "wb") as f:
+        while chunk := src.read(1 << 20):
+            f.write(chunk)
+
+
 async def save_upload_file(file, destination: Path) -> None:
+    """Write the upload to `destination` off the event loop (the reference streams
+    8 KiB chunks through aiofiles, app/main.py:157-167); a partial file is removed."""
+    import asyncio
+
     try:
-        with open(destination, "wb") as f:
-            while chunk := await file.read(8192):
-                f.write(chunk)
+        await asyncio.get_running_loop().run_in_executor(None, _copy_to, file.file, destination)
     except Exception:
         if destination.exists():
             destination.unlink()
@@ -242,8 +253,16 @@ async def health_check():
 
 
 async def _upload_file_param(request: Request):
+    """Stream the request body through the incremental multipart parser: the body
+    is never buffered whole and a file part is stored only up to the size limit
+    (the 400/413 checks in upload_file still run in the reference's order)."""
+    form = {}
     try:
-        form = parse_form(await request.body(), request.headers.get("content-type", ""))
+        mp = MultipartStream(request.headers.get("content-type", ""),
+                             max_file_bytes=MAX_FILE_SIZE_MB * 1024 * 1024)
+        async for chunk in request.stream():
+            mp.feed(chunk)
+        form = mp.close()
     except MultipartError:
         form = {}
     files = form.get("file")

@@ -32,7 +32,10 @@ from typing import Any, Protocol
 
 from pydantic import ValidationError
 
+from ..utils.dotenv import load_dotenv
 from .prompt import SYSTEM_MESSAGE, build_user_message, register_prompt_prefix, truncate
+
+load_dotenv()                              # rfq_agent.py:13
 from .schema import RFQResponse
 
 log = logging.getLogger("replisense_rfq_amd.service.extract")

@@ -52,6 +52,25 @@ def _parse_in_process(kind: str, path: str, max_excel_rows: int) -> str:
     return fn(Path(path))
 
 
+
+def _read1(path: Path) -> bytes:
+    with open(path, "rb") as f:
+        return f.read(1)
+
+
+def _md5_file(path: Path) -> str:
+    """md5 over 8 KiB chunks (file_parser.py:122-130)."""
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(8192), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _read_text(path: Path, errors: str) -> str:
+    with open(path, "r", encoding="utf-8", errors=errors) as f:
+        return f.read()
+
 class FileParser:
     def __init__(self, max_file_size_mb: int = 10, max_excel_rows: int = 1000,
                  workers: int = 4, processes: int = 0):
@@ -134,17 +153,17 @@ class FileParser:
         if file_path.suffix.lower() not in self.supported_extensions:
             raise FileParsingError(f"Unsupported file type: {file_path.suffix}")
         try:
-            with open(file_path, "rb") as f:
-                f.read(1)
+            await self._io(_read1, file_path)
         except PermissionError:
             raise FileParsingError(f"Permission denied reading file: {file_path}")
 
+    async def _io(self, fn, *args):
+        """Blocking file I/O off the event loop (the reference awaits aiofiles; the
+        HTTP loop here also shares its GIL slices with the engine thread)."""
+        return await asyncio.get_running_loop().run_in_executor(self.thread_pool, fn, *args)
+
     async def _get_file_hash_async(self, file_path: Path) -> str:
-        h = hashlib.md5()
-        with open(file_path, "rb") as f:
-            for chunk in iter(lambda: f.read(8192), b""):
-                h.update(chunk)
-        return h.hexdigest()
+        return await self._io(_md5_file, file_path)
 
     def _get_cached_result(self, file_hash: str) -> Optional[dict[str, Any]]:
         return None
@@ -154,8 +173,7 @@ class FileParser:
 
     # ----------------------------------------------------------------- formats
     async def _parse_txt_async(self, file_path: Path) -> str:
-        with open(file_path, "r", encoding="utf-8", errors="ignore") as f:
-            return f.read().strip()
+        return (await self._io(_read_text, file_path, "ignore")).strip()
 
     def _parse_pdf_sync(self, file_path: Path) -> str:
         parts = []
@@ -220,8 +238,7 @@ class FileParser:
 
     async def _parse_json_async(self, file_path: Path) -> str:
         try:
-            with open(file_path, "r", encoding="utf-8") as f:
-                content = f.read()
+            content = await self._io(_read_text, file_path, "strict")
             data = json.loads(content)
             return f"=== JSON Data ===\n{json.dumps(data, indent=2, ensure_ascii=False)}"
         except json.JSONDecodeError as e:

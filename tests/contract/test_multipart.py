@@ -1,0 +1,80 @@
+"""Streaming multipart parser (api/multipart.py): chunk-boundary independence,
+bounded storage of oversized file parts, and the reference's 400-before-413 order
+through the API."""
+import random
+
+import pytest
+from fastapi.testclient import TestClient
+
+from replisense_rfq_amd.api.multipart import MultipartStream, parse_form
+
+CT = "multipart/form-data; boundary=XyZ123"
+
+
+def _body(parts, eol=b"\r\n"):
+    out = b"preamble" + eol
+    for name, filename, data in parts:
+        out += b"--XyZ123" + eol
+        disp = f'Content-Disposition: form-data; name="{name}"'
+        if filename is not None:
+            disp += f'; filename="{filename}"'
+        out += disp.encode() + eol
+        if filename is not None:
+            out += b"Content-Type: application/octet-stream" + eol
+        out += eol + data + eol
+    return out + b"--XyZ123--" + eol
+
+
+def _dump(form):
+    out = {}
+    for k, vs in form.items():
+        out[k] = []
+        for v in vs:
+            if isinstance(v, str):
+                out[k].append(v)
+            else:
+                v.file.seek(0)
+                out[k].append((v.filename, v.size, v.file.read()))
+    return out
+
+
+@pytest.mark.parametrize("eol", [b"\r\n", b"\n"])
+def test_chunking_does_not_change_the_result(eol):
+    rng = random.Random(0)
+    blob = bytes(rng.randrange(256) for _ in range(50_000)) + b"\r\n--XyZ12 not a delimiter"
+    body = _body([("note", None, b"hello"), ("file", "réq.pdf", blob),
+                  ("file", "b.txt", b"")], eol)
+    whole = _dump(parse_form(body, CT))
+    assert whole["note"] == ["hello"]
+    assert whole["file"][0] == ("réq.pdf", len(blob), blob)
+    assert whole["file"][1] == ("b.txt", 0, b"")
+    for trial in range(20):
+        mp = MultipartStream(CT)
+        i = 0
+        while i < len(body):
+            n = rng.choice([1, 2, 7, 64, 1000, 8192])
+            mp.feed(body[i:i + n])
+            i += n
+        assert _dump(mp.close()) == whole
+
+
+def test_oversized_part_is_counted_not_stored():
+    data = b"x" * 5000
+    form = parse_form(_body([("file", "a.pdf", data)]), CT, max_file_bytes=1000)
+    f = form["file"][0]
+    assert f.size == 5000                       # the 413 check sees the real size
+    f.file.seek(0, 2)
+    assert f.file.tell() == 1001                # but only limit + 1 bytes were kept
+
+
+def test_api_order_400_before_413(monkeypatch):
+    from replisense_rfq_amd.api import main
+
+    monkeypatch.setattr(main, "MAX_FILE_SIZE_MB", 1)
+    client = TestClient(main.app)
+    big = b"a" * (1024 * 1024 + 10)
+    r = client.post("/upload/", files={"file": ("doc.exe", big, "application/octet-stream")})
+    assert r.status_code == 400 and r.json()["error"].startswith("Unsupported file type")
+    r = client.post("/upload/", files={"file": ("doc.txt", big, "text/plain")})
+    assert r.status_code == 413
+    assert r.json()["error"] == "File too large. Maximum size: 1MB"
