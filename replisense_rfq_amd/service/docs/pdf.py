@@ -18,8 +18,9 @@ The reference extracts PDF text with PyMuPDF ``page.get_text()``, table rows wit
     reference's recorded parse of tests/assets/attachment.pdf, cache.db row 13);
   * ``images()``: image XObjects in the page resources (``get_images``).
 
-Ruled-table detection (``find_tables``) is not reproduced: tables are still
-extracted as text lines.  Documented as parity-unpinned.
+  * ``page_tables()``: ruled tables (``find_tables`` "lines" strategy) from the
+    painted path segments and the glyph boxes the interpreter records
+    (:mod:`.pdf_tables`; byte parity with PyMuPDF unpinned).
 """
 from __future__ import annotations
 
@@ -426,6 +427,20 @@ class PdfDocument:
     def page_text(self, i: int) -> str:
         return PageText(self, self.pages[i]).text()
 
+    def page_text_and_tables(self, i: int) -> tuple[str, list]:
+        """(get_text(), find_tables() rows) of page i from one interpreter pass."""
+        from .pdf_tables import extract_tables
+
+        pt = PageText(self, self.pages[i])
+        text = pt.text()
+        h = pt.height()
+        glyphs = [(min(x0, x1), max(x0, x1), h - (y + ASC * s), h - (y - DESC * s), h - y, s, c)
+                  for x0, x1, y, s, c in pt.glyphs]
+        try:               # table failures never fail the page (file_parser.py:194-196)
+            return text, extract_tables(pt.segments, glyphs, h)
+        except (ValueError, TypeError, KeyError, IndexError, ZeroDivisionError):
+            return text, []
+
     def page_images(self, i: int) -> list:
         res = self.resolve(self.pages[i].get("Resources")) or {}
         xo = self.resolve(res.get("XObject")) or {}
@@ -610,6 +625,10 @@ class Font:
 
 # ---------------------------------------------------------- page interpreter
 
+ASC, DESC = 0.8, 0.2                      # glyph box above / below the baseline (x font size)
+PAINT_OPS = {"S", "s", "f", "F", "f*", "B", "B*", "b", "b*"}
+
+
 def _mul(a, b):
     return [a[0] * b[0] + a[1] * b[2], a[0] * b[1] + a[1] * b[3],
             a[2] * b[0] + a[3] * b[2], a[2] * b[1] + a[3] * b[3],
@@ -621,7 +640,16 @@ class PageText:
         self.doc = doc
         self.page = page
         self.lines: list[list] = []      # [[(x0, x1, y, size, text), ...], ...]
+        self.glyphs: list[tuple] = []    # every shown glyph (x0, x1, baseline y, size, ch)
+        self.segments: list[tuple] = []  # painted straight path segments (x0, y0, x1, y1)
         self._fonts: dict[int, Font] = {}
+
+    def height(self) -> float:
+        box = self.doc.resolve(self.page.get("MediaBox")) or [0, 0, 612, 792]
+        try:
+            return float(self.doc.resolve(box[3])) - float(self.doc.resolve(box[1]))
+        except (TypeError, ValueError, IndexError):
+            return 792.0
 
     def _font(self, res: dict, name):
         fonts = self.doc.resolve(res.get("Font")) or {}
@@ -679,6 +707,11 @@ class PageText:
         tc = tw = ts = 0.0
         th = 1.0
         tl = 0.0
+        pending: list = []              # segments of the path under construction
+        cur = start = None
+
+        def T(x, y):
+            return (ctm[0] * x + ctm[2] * y + ctm[4], ctm[1] * x + ctm[3] * y + ctm[5])
 
         def show(s: bytes, adj=0.0):
             nonlocal tm
@@ -694,6 +727,7 @@ class PageText:
                 x1 = x0 + adv * (tm[0] * ctm[0])
                 for c in ch:
                     self._emit(x0, x1, y0, size, c)
+                    self.glyphs.append((x0, x1, y0, size, c))
                 tm = _mul([1, 0, 0, 1, adv, 0], tm)
 
         while True:
@@ -708,7 +742,33 @@ class PageText:
                 continue
             op = t
             try:
-                if op == "BI":                                # inline image: skip data
+                if op == "m":
+                    cur = start = T(float(stack[-2]), float(stack[-1]))
+                elif op == "l":
+                    p = T(float(stack[-2]), float(stack[-1]))
+                    if cur is not None:
+                        pending.append((*cur, *p))
+                    cur = p
+                elif op in ("c", "v", "y"):               # curves never form table edges
+                    cur = T(float(stack[-2]), float(stack[-1]))
+                elif op == "h":
+                    if cur is not None and start is not None and cur != start:
+                        pending.append((*cur, *start))
+                    cur = start
+                elif op == "re":
+                    x, y, w, hh = (float(v) for v in stack[-4:])
+                    c4 = [T(x, y), T(x + w, y), T(x + w, y + hh), T(x, y + hh)]
+                    pending.extend((*c4[k], *c4[(k + 1) % 4]) for k in range(4))
+                    cur = start = c4[0]
+                elif op in PAINT_OPS:
+                    if op in ("s", "b", "b*") and cur is not None and start is not None \
+                            and cur != start:
+                        pending.append((*cur, *start))
+                    self.segments.extend(pending)
+                    pending, cur, start = [], None, None
+                elif op == "n":
+                    pending, cur, start = [], None, None
+                elif op == "BI":                                # inline image: skip data
                     e = data.find(b"EI", lx.p)
                     lx.p = len(data) if e < 0 else e + 2
                 elif op == "q":

@@ -29,6 +29,7 @@ import pandas as pd
 
 from .docs.docx import docx_to_text
 from .docs.pdf import PdfDocument
+from .docs.pdf_tables import format_tables
 from .docs.xls import read_xls_frames
 from .docs.xlsx import read_excel_frames
 
@@ -180,9 +181,10 @@ class FileParser:
         try:
             doc = PdfDocument.open(file_path)
             for i in range(len(doc)):
-                t = doc.page_text(i)
+                t, tables = doc.page_text_and_tables(i)
                 if t.strip():
                     parts.append(f"=== Page {i + 1} ===\n{t.strip()}")
+                parts.extend(format_tables(tables, i + 1))
                 imgs = doc.page_images(i)
                 if imgs:
                     parts.append(f"\n=== Images on Page {i + 1} ===\nFound {len(imgs)} image(s)")

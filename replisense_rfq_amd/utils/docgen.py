@@ -26,17 +26,60 @@ def _pdf_escape(s: str) -> bytes:
 
 def write_pdf(lines: list[str], path=None, lines_per_page: int = 26, font_size: float = 12.0) -> bytes:
     pages = [lines[i:i + lines_per_page] for i in range(0, max(1, len(lines)), lines_per_page)]
-    objs: dict[int, bytes] = {}
-    page_ids = []
-    nxt = 3
+    streams = []
     for pl in pages:
-        pid, cid = nxt, nxt + 1
-        nxt += 2
         ops = [b"2 J", b"0.57 w", b"BT /F1 %.2f Tf ET" % font_size]
         y = 795.17
         for ln in pl:
             ops.append(b"BT 31.19 %.2f Td (%s) Tj ET" % (y, _pdf_escape(ln)))
             y -= 28.35
+        streams.append(ops)
+    return _assemble(streams, path)
+
+
+def write_pdf_table(lines: list[str], rows: list[list[str]], path=None, ruling: str = "lines",
+                    col_widths: list[float] | None = None, font_size: float = 10.0) -> bytes:
+    """One page: text lines, then a ruled table (the layout RFQ line items usually
+    have).  ``ruling``: "lines" (m/l/S grid), "rects" (one stroked ``re`` per cell)
+    or "none" (the same text with no ruling: no table may be detected)."""
+    ncol = max(len(r) for r in rows)
+    col_widths = col_widths or [530.0 / ncol] * ncol
+    ops = [b"0.5 w", b"BT /F1 %.2f Tf ET" % font_size]
+    y = 800.0
+    for ln in lines:
+        ops.append(b"BT 31.19 %.2f Td (%s) Tj ET" % (y, _pdf_escape(ln)))
+        y -= 20.0
+    top, rh, left = y - 10.0, 18.0, 31.19
+    xs = [left]
+    for w in col_widths:
+        xs.append(xs[-1] + w)
+    for r, row in enumerate(rows):
+        base = top - (r + 1) * rh + 5.0
+        for c, cell in enumerate(row):
+            if cell:
+                ops.append(b"BT %.2f %.2f Td (%s) Tj ET" % (xs[c] + 3.0, base, _pdf_escape(cell)))
+    bottom = top - len(rows) * rh
+    if ruling == "lines":
+        for r in range(len(rows) + 1):
+            yy = top - r * rh
+            ops.append(b"%.2f %.2f m %.2f %.2f l S" % (xs[0], yy, xs[-1], yy))
+        for x in xs:
+            ops.append(b"%.2f %.2f m %.2f %.2f l S" % (x, top, x, bottom))
+    elif ruling == "rects":
+        for r in range(len(rows)):
+            for c in range(ncol):
+                ops.append(b"%.2f %.2f %.2f %.2f re S" % (xs[c], top - (r + 1) * rh,
+                                                         col_widths[c], rh))
+    return _assemble([ops], path)
+
+
+def _assemble(page_ops: list[list[bytes]], path=None) -> bytes:
+    objs: dict[int, bytes] = {}
+    page_ids = []
+    nxt = 3
+    for ops in page_ops:
+        pid, cid = nxt, nxt + 1
+        nxt += 2
         raw = zlib.compress(b"\n".join(ops) + b"\n")
         objs[cid] = b"<</Filter /FlateDecode /Length %d>>\nstream\n%s\nendstream" % (len(raw), raw)
         objs[pid] = b"<</Type /Page\n/Parent 1 0 R\n/Resources 2 0 R\n/Contents %d 0 R>>" % cid

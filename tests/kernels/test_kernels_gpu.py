@@ -507,3 +507,43 @@ def test_linear_m_split_plan(gpu):
             _close(ops.linear(xm, w), xm.float() @ w.float().t(), 1e-2, 1e-2, f"lt plan M={M}")
     finally:
         ops.set_split_plan({})
+
+
+@pytest.mark.parametrize("M,cfg", [(1, 12), (4, 15), (16, 13), (1, 12 | 64)])
+def test_skinny_norm_handoff_stress(gpu, M, cfg):
+    """The NormEpi hand-off (sc1 tile stores drained by every wave, relaxed agent
+    ticket, sc1 loads in the last workgroup -- cdna_hip_programming.md §6
+    Guideline 16, "every load sc1" form) over many launches, with a second stream
+    keeping other CUs busy (uneven load): the residual written by the last
+    workgroup must equal bf16(y + residual) of the unfused GEMM bit for bit every
+    time; a stale Y read would break it."""
+    torch.manual_seed(M + cfg)
+    N, K = 4096, 4096
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(BF)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
+    counter = torch.zeros(4, dtype=torch.int32, device=gpu)
+    partials = torch.empty(2 * M * N, device=gpu)
+    load_a = torch.randn(4096, 4096, device=gpu, dtype=BF)
+    side = torch.cuda.Stream()
+    bad = 0
+    for it in range(300):
+        x = torch.randn(M, K, device=gpu, dtype=BF)
+        res = torch.randn(M, N, device=gpu, dtype=BF)
+        res0 = res.clone()
+        y = torch.empty(M, N, device=gpu, dtype=BF)
+        out = torch.empty(M, N, device=gpu, dtype=BF)
+        if it % 3 == 0:
+            with torch.cuda.stream(side):
+                load_a @ load_a                          # concurrent work on other CUs
+        torch.ops.rfq_amd.skinny_gemm_norm(x, w, y, res, nw, 1e-5, out, counter, partials, cfg)
+        y_ref = torch.empty(M, N, device=gpu, dtype=BF)
+        torch.ops.rfq_amd.skinny_gemm(x, w, y_ref, cfg & 63)
+        if cfg & 64:                                      # split-K: fp32 slices summed
+            want = (y_ref.float() + res0.float()).to(BF)
+            bad += int(((res.float() - want.float()).abs() > 0.05 * want.float().abs() + 0.05)
+                       .any())
+        else:
+            bad += int(not torch.equal(res, (y_ref.float() + res0.float()).to(BF)))
+    torch.cuda.synchronize()
+    assert bad == 0, f"{bad} of 300 launches read a stale tile"
+    assert int(counter[0]) == 0
