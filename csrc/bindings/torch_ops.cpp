@@ -24,6 +24,13 @@ void launch_skinny_gemm_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf
                              int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*,
                              int, int, int, hipStream_t);
 void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
+void launch_skinny_gemm_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
+                               int, int, hipStream_t);
+void launch_gemv_splitk_plain(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
+                              int, int, float*, unsigned*, hipStream_t);
+void launch_gemv_splitk_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
+                             int, int, float*, unsigned*, bf16_t*, int64_t, const bf16_t*,
+                             bf16_t*, int64_t, float, unsigned*, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
@@ -159,6 +166,73 @@ void skinny_gemm_norm(const Tensor& x, const Tensor& w, const Tensor& y, const T
                                out.stride(0), (float)eps,
                                reinterpret_cast<unsigned*>(counter.data_ptr()),
                                (cfg & 64) ? partials.data_ptr<float>() : nullptr, cur_stream());
+}
+
+// out[M, F] = silu(x . Wg^T) * (x . Wu^T), w = [Wg; Wu] [2F, K] (M <= 16): the gate|up
+// projection with the SwiGLU in its epilogue (= skinny_gemm then silu_mul).
+void skinny_gemm_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "skinny_gemm_swiglu: w must be contiguous [2F, K]");
+  const int M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny_gemm_swiglu: M must be in [1, 16]");
+  TORCH_CHECK(w.size(0) == 2 * F && w.size(1) == K && K % 128 == 0 && F % 16 == 0,
+              "skinny_gemm_swiglu: w [2F, K] with K % 128 == 0, F % 16 == 0");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == F, "skinny_gemm_swiglu: out [M, F]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && out.stride(0) % 4 == 0, "skinny_gemm_swiglu: alignment");
+  rfq::launch_skinny_gemm_swiglu(bp(x), x.stride(0), bp(w), F, K, bpm(out), out.stride(0), M,
+                                 (int)cfg, cur_stream());
+}
+
+static void check_splitk(const char* what, const Tensor& x, const Tensor& w, const Tensor& y,
+                         const Tensor& part, const Tensor& tile_cnt, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_I32(tile_cnt);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(y);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), what, ": w must be contiguous [N, K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), KS = 2 << (cfg & 3);
+  TORCH_CHECK(M >= 1 && M <= 16, what, ": M must be in [1, 16]");
+  TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N % 16 == 0 && (K / 128) >= KS, what,
+              ": K % 128 == 0, N % 16 == 0 and K / 128 >= KS required");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N, what, ": y [M, N]");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, what, ": alignment");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
+              what, ": fp32 partials workspace of KS*M*N floats");
+  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, what, ": N/16 tile counters");
+}
+
+// y = x . w^T, split-K over (N/16) x KS workgroups with the in-launch per-tile
+// reduction (M <= 16).  tile_cnt: int32 [>= N/16], zero, left at zero.
+void gemv_splitk(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& part,
+                 const Tensor& tile_cnt, int64_t cfg) {
+  check_splitk("gemv_splitk", x, w, y, part, tile_cnt, cfg);
+  rfq::launch_gemv_splitk_plain(bp(x), x.stride(0), bp(w), w.size(0), x.size(1), bpm(y),
+                                y.stride(0), x.size(0), (int)cfg, part.data_ptr<float>(),
+                                reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), cur_stream());
+}
+
+// gemv_splitk followed, in the same launch, by residual <- y + residual and
+// out <- rmsnorm(residual) * norm_w (= fused_add_rms_norm).
+void gemv_splitk_norm(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& residual,
+                      const Tensor& norm_w, double eps, const Tensor& out, const Tensor& counter,
+                      const Tensor& part, const Tensor& tile_cnt, int64_t cfg) {
+  check_splitk("gemv_splitk_norm", x, w, y, part, tile_cnt, cfg);
+  CHECK_BF16(residual); CHECK_BF16(norm_w); CHECK_BF16(out); CHECK_I32(counter);
+  CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
+  const int64_t M = x.size(0), N = w.size(0);
+  const int threads = (cfg & 4) ? 512 : 256;
+  TORCH_CHECK(N % 8 == 0 && N / 8 <= 4 * threads, "gemv_splitk_norm: N <= 32 * threads");
+  TORCH_CHECK(residual.size(0) == M && residual.size(1) == N && out.size(0) == M &&
+                  out.size(1) == N && norm_w.numel() == N,
+              "gemv_splitk_norm: shapes");
+  TORCH_CHECK(y.stride(0) % 8 == 0 && residual.stride(0) % 8 == 0 && out.stride(0) % 8 == 0,
+              "gemv_splitk_norm: alignment");
+  TORCH_CHECK(counter.is_cuda() && counter.numel() >= 1, "gemv_splitk_norm: counter");
+  rfq::launch_gemv_splitk_norm(bp(x), x.stride(0), bp(w), N, x.size(1), bpm(y), y.stride(0), M,
+                               (int)cfg, part.data_ptr<float>(),
+                               reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), bpm(residual),
+                               residual.stride(0), bp(norm_w), bpm(out), out.stride(0),
+                               (float)eps, reinterpret_cast<unsigned*>(counter.data_ptr()),
+                               cur_stream());
 }
 
 // qkv = x . w^T (skinny, M <= 16) with NeoX RoPE on q/k and the paged KV append in the
@@ -569,6 +643,12 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
   m.def("skinny_gemm_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
         "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) partials, int cfg) -> ()");
+  m.def("skinny_gemm_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("gemv_splitk(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) part, Tensor(c!) tile_cnt, "
+        "int cfg) -> ()");
+  m.def("gemv_splitk_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
+        "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) part, Tensor(f!) tile_cnt, "
+        "int cfg) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
@@ -622,6 +702,9 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("skinny_gemm", &skinny_gemm);
   m.impl("skinny_gemm_norm", &skinny_gemm_norm);
   m.impl("skinny_gemm_rope", &skinny_gemm_rope);
+  m.impl("skinny_gemm_swiglu", &skinny_gemm_swiglu);
+  m.impl("gemv_splitk", &gemv_splitk);
+  m.impl("gemv_splitk_norm", &gemv_splitk_norm);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);

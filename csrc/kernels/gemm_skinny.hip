@@ -166,20 +166,27 @@ struct RopeEpi {
 // KS > 1 (NORM only): the KS workgroups of an output tile each stream one K slice and
 // publish fp32 partials; the last workgroup sums them before the add + RMSNorm.  For
 // N = 4096 projections (o, down: 256 tiles) this doubles the workgroups in flight.
+// SWI (MT = 1, NT = 2): tile 0 = gate rows [n0, n0+16), tile 1 = up rows
+// [up_off + n0, ...) of the stacked gate|up weight; the epilogue writes
+// silu(gate) * up rounded exactly like act.hip's silu_mul (gate and up rounded to bf16
+// first), so the gate|up GEMM, the SwiGLU pass and its [M, 2F] intermediate become one
+// kernel whose output is the down projection's [M, F] input.
 template <int MT, int NT, int NW, int U, bool CMAP, bool NTL, bool GX = false, bool NORM = false,
-          bool ROPE = false, int KS = 1>
+          bool ROPE = false, int KS = 1, bool SWI = false>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K, int64_t wstr,
-    bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep, RopeEpi re = RopeEpi{}) {
+    bf16_t* __restrict__ Y, int64_t ldy, int M, NormEpi ep, RopeEpi re = RopeEpi{},
+    int up_off = 0) {
   static_assert(!ROPE || (MT == 1 && NT == 2 && !NORM && !GX), "RoPE epilogue: MT=1, NT=2");
+  static_assert(!SWI || (MT == 1 && NT == 2 && !NORM && !GX && !ROPE), "SwiGLU: MT=1, NT=2");
   static_assert(KS == 1 || (NORM && MT == 1), "split-K only with the norm epilogue");
   __shared__ f32x4 red[NW][NT * MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   // ROPE: block b owns head b/4, rotary pair block b%4 (features n0 and n0 + 64)
   const int bt = KS > 1 ? blockIdx.x / KS : blockIdx.x, slice = KS > 1 ? blockIdx.x % KS : 0;
-  const int n0 = ROPE ? (bt >> 2) * 128 + (bt & 3) * 16 : bt * (16 * NT);
-  constexpr int ASTRIDE = ROPE ? 64 : 16;
+  const int n0 = ROPE ? (bt >> 2) * 128 + (bt & 3) * 16 : (SWI ? bt * 16 : bt * (16 * NT));
+  const int astride = ROPE ? 64 : (SWI ? up_off : 16);
   const int nks_all = K >> 7;
   const int sl0 = slice * nks_all / KS, nks = (slice + 1) * nks_all / KS - sl0;
   const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
@@ -187,7 +194,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   const bf16_t* wp[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a)
-    wp[a] = W + (int64_t)(n0 + a * ASTRIDE + r) * wstr + g * (CMAP ? 8 : 32);
+    wp[a] = W + (int64_t)(n0 + a * astride + r) * wstr + g * (CMAP ? 8 : 32);
   constexpr int JS = CMAP ? 32 : 8;                 // element stride between MFMA chunks
   const bf16_t* xp[MT];
   bool xv[MT];
@@ -260,6 +267,29 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 #pragma unroll
       for (int t = 0; t < MT; ++t) red[wave][a * MT + t][lane] = acc[a][t];
     __syncthreads();
+  }
+  if constexpr (SWI) {
+    if (wave != 0) return;
+    f32x4 s0 = NW == 1 ? acc[0][0] : red[0][0][lane];
+    f32x4 s1 = NW == 1 ? acc[1][0] : red[0][1][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) {
+      s0 += red[w2][0][lane];
+      s1 += red[w2][1][lane];
+    }
+    if (r >= M) return;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float gf = bf2f(f2bf(s0[i]));                // = the gate_up GEMM's bf16 output
+      const float sg = gf / (1.f + __expf(-gf));
+      o[i] = bf2f(f2bf(sg)) * bf2f(f2bf(s1[i]));
+    }
+    uint2 v;
+    v.x = pack_bf16x2(o[0], o[1]);
+    v.y = pack_bf16x2(o[2], o[3]);
+    *reinterpret_cast<uint2*>(Y + (int64_t)r * ldy + n0 + g * 4) = v;
+    return;
   }
   if constexpr (ROPE) {
     if (wave != 0) return;
@@ -464,6 +494,194 @@ void launch_skinny_gemm_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
                    (cfg & 64) ? partials : nullptr, (int64_t)M * N};
   cfg &= 63;
   skinny_dispatch(X, ldx, W, N, K, (int64_t)K, Y, ldy, M, cfg, true, ep, s);
+}
+
+// out[M, F] = silu(x Wg^T) * (x Wu^T) for w = [Wg; Wu] ([2F, K]); M <= 16.
+// cfg bit 1 picks 4 or 8 waves.
+void launch_skinny_gemm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, int F, int K,
+                               bf16_t* Y, int64_t ldy, int M, int cfg, hipStream_t s) {
+  const dim3 grid(F / 16);
+  if (cfg & 2)
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 8, 2, true, false, false, false, false, 1, true>),
+                       grid, dim3(512), 0, s, X, ldx, W, K, (int64_t)K, Y, ldy, M, NormEpi{},
+                       RopeEpi{}, F);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<1, 2, 4, 2, true, false, false, false, false, 1, true>),
+                       grid, dim3(256), 0, s, X, ldx, W, K, (int64_t)K, Y, ldy, M, NormEpi{},
+                       RopeEpi{}, F);
+}
+
+// ---------------------------------------------------------------------------
+// Split-K weight-streaming GEMV (M <= 16) with an in-launch reduction.
+//
+// The o / down projections have only N/16 = 256 output tiles: one workgroup per CU
+// whose waves each stream a long K range as a few dependent load rounds, so the
+// kernel is bound by (rounds x HBM latency), not by bandwidth.  Here the grid is
+// tiles x KS: KS workgroups per 16-feature tile each stream K/KS (more, shorter
+// streams in flight on every CU), publish their fp32 partial tile write-through,
+// and the last of a tile's KS arrivals (per-tile ticket) sums the slices in slice
+// order and writes the bf16 tile.  With NORM, finished tiles take a second ticket
+// and the grid's last one runs the residual-add RMSNorm (last_block_add_norm).
+// Every hand-off is the "every load sc1" form of cdna_hip_programming.md §6
+// Guideline 16: sc1 8-byte stores drained by vmcnt(0) + barrier, relaxed agent
+// tickets, sc1 loads of all handed-off bytes; counters are left at zero.
+template <int NW, int U, bool NORM>
+__global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
+    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
+    bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part,
+    unsigned* __restrict__ tile_cnt, NormEpi ep) {
+  __shared__ f32x4 red[NW][64];
+  __shared__ float nscratch[17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int ntile = gridDim.x / KS, N = ntile * 16;
+  const int bt = blockIdx.x / KS, slice = blockIdx.x - bt * KS;
+  const int n0 = bt * 16;
+  const int nks_all = K >> 7;
+  const int sl0 = slice * nks_all / KS, nks = (slice + 1) * nks_all / KS - sl0;
+  const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
+  const bf16_t* wp = W + (int64_t)(n0 + r) * K + g * 8;
+  const bool xv = r < M;
+  const bf16_t* xp = X + (int64_t)(xv ? r : 0) * ldx + g * 8;
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int ks = ks0;
+  for (; ks + U <= ks1; ks += U) {
+    s16x8 w[U][4], x[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[u][j] = ldw<false>(wp + (int64_t)(ks + u) * 128 + j * 32);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        x[u][j] = xv ? *reinterpret_cast<const s16x8*>(xp + (ks + u) * 128 + j * 32) : zero;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[u][j]), as_bf16x8(x[u][j]), acc,
+                                                      0, 0, 0);
+  }
+  for (; ks < ks1; ++ks) {
+    s16x8 w[4], x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = ldw<false>(wp + (int64_t)ks * 128 + j * 32);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      x[j] = xv ? *reinterpret_cast<const s16x8*>(xp + ks * 128 + j * 32) : zero;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j]), as_bf16x8(x[j]), acc, 0, 0,
+                                                    0);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  // D layout: lane holds output features n0 + g*4 + i for token r.
+  gu64* slab = (gu64*)(part + ((int64_t)slice * M + r) * N + n0 + g * 4);
+  if (wave == 0) {
+    f32x4 s = red[0][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) s += red[w2][lane];
+    if (xv) {
+      __hip_atomic_store(slab, (unsigned long long)__float_as_uint(s[0]) |
+                                   ((unsigned long long)__float_as_uint(s[1]) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(slab + 1, (unsigned long long)__float_as_uint(s[2]) |
+                                       ((unsigned long long)__float_as_uint(s[3]) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev =
+        __hip_atomic_fetch_add(tile_cnt + bt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nscratch[16] = (prev == (unsigned)KS - 1) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (nscratch[16] == 0.f) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
+  if (threadIdx.x == 0)
+    __hip_atomic_store(tile_cnt + bt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0 && xv) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < KS; ++sl) {
+      const gu64* q = (const gu64*)(part + ((int64_t)sl * M + r) * N + n0 + g * 4);
+      const unsigned long long u0 = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long u1 =
+          __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s[0] += __uint_as_float((uint32_t)u0);
+      s[1] += __uint_as_float((uint32_t)(u0 >> 32));
+      s[2] += __uint_as_float((uint32_t)u1);
+      s[3] += __uint_as_float((uint32_t)(u1 >> 32));
+    }
+    uint2 v;
+    v.x = pack_bf16x2(s[0], s[1]);
+    v.y = pack_bf16x2(s[2], s[3]);
+    bf16_t* yp = Y + (int64_t)r * ldy + n0 + g * 4;
+    if constexpr (NORM)
+      __hip_atomic_store((gu64*)yp, (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      *reinterpret_cast<uint2*>(yp) = v;
+  }
+  if constexpr (NORM) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev =
+          __hip_atomic_fetch_add(ep.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nscratch[16] = (prev == (unsigned)ntile - 1) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (nscratch[16] == 0.f) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x == 0)
+      __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_block_add_norm<NW * 64, 1>(Y, ldy, N, M, ep, nscratch);
+  }
+}
+
+// cfg bits: [1:0] KS = 2 << bits (2, 4, 8, 16); bit 2: 8 waves (else 4); bit 3: U = 2 (else 4;
+// U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones).
+// part: fp32 [KS][M][N]; tile_cnt: N/16 zeroed uint32 (left at zero).
+void launch_gemv_splitk(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                        int64_t ldy, int M, int cfg, float* part, unsigned* tile_cnt, bool norm,
+                        const NormEpi& ep, hipStream_t s) {
+  const int KS = 2 << (cfg & 3);
+  const dim3 grid((N / 16) * KS);
+#define GV_LAUNCH(nw, u, nm)                                                                \
+  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, nm>), grid, dim3(nw * 64), 0, s, X, ldx, W, K, \
+                     Y, ldy, M, KS, part, tile_cnt, ep)
+  const int sel = ((cfg >> 2) & 3) | (norm ? 4 : 0);
+  switch (sel) {
+    case 0: GV_LAUNCH(4, 4, false); break;
+    case 1: GV_LAUNCH(8, 4, false); break;
+    case 2: GV_LAUNCH(4, 2, false); break;
+    case 3: GV_LAUNCH(8, 2, false); break;
+    case 4: GV_LAUNCH(4, 4, true); break;
+    case 5: GV_LAUNCH(8, 4, true); break;
+    case 6: GV_LAUNCH(4, 2, true); break;
+    default: GV_LAUNCH(8, 2, true); break;
+  }
+#undef GV_LAUNCH
+}
+
+void launch_gemv_splitk_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                             bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
+                             unsigned* tile_cnt, bf16_t* residual, int64_t res_stride,
+                             const bf16_t* norm_w, bf16_t* out, int64_t out_stride, float eps,
+                             unsigned* counter, hipStream_t s) {
+  const NormEpi ep{residual, res_stride, norm_w, out, out_stride, eps, counter, nullptr, 0};
+  launch_gemv_splitk(X, ldx, W, N, K, Y, ldy, M, cfg, part, tile_cnt, true, ep, s);
+}
+
+void launch_gemv_splitk_plain(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                              bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
+                              unsigned* tile_cnt, hipStream_t s) {
+  launch_gemv_splitk(X, ldx, W, N, K, Y, ldy, M, cfg, part, tile_cnt, false, NormEpi{}, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -10,6 +10,8 @@ MLP).  A forward pass consumes a *mixed* token batch laid out as
      jump-forward extends) + attn_prefill (varlen causal MFMA flash; prompt
      chunks) -> O GEMM -> [all-reduce]
      -> fused_add_rms_norm -> gate|up GEMM -> silu_mul -> down GEMM -> [all-reduce]
+       (TP=1 latency path, when the start-up plan measured it faster: gate|up GEMM with
+        the SwiGLU epilogue, down GEMM with the residual-add RMSNorm in-launch)
         (MoE: router -> top-2 -> align -> grouped MFMA GEMMs -> combine)
   -> final norm on the rows that need logits -> vocab-parallel LM head.
 
@@ -142,11 +144,18 @@ class DecoderLM:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
                              expert_offset=self.expert_offset)
             else:
-                gu = ops.linear(x, lw["gate_up"])
-                if fuse and ops.linear_add_norm(gu, lw["down"], residual, nxt, eps, x,
-                                                gated=True):
-                    continue
-                mo = ops.silu_linear(gu, lw["down"])
+                # latency path: gate|up with the SwiGLU epilogue (one kernel, [M, F] out)
+                act = ops.linear_swiglu(x, lw["gate_up"]) if fuse else None
+                if act is not None:
+                    if ops.linear_add_norm(act, lw["down"], residual, nxt, eps, x):
+                        continue
+                    mo = ops.linear(act, lw["down"])
+                else:
+                    gu = ops.linear(x, lw["gate_up"])
+                    if fuse and ops.linear_add_norm(gu, lw["down"], residual, nxt, eps, x,
+                                                    gated=True):
+                        continue
+                    mo = ops.silu_linear(gu, lw["down"])
             self.tp.all_reduce_(mo)
             ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)

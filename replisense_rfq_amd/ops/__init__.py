@@ -19,7 +19,7 @@ __all__ = [
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
-    "set_rope_plan",
+    "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
 ]
 
@@ -140,6 +140,22 @@ def norm_plan(M: int, N: int, K: int, gated: bool) -> int:
     return -1
 
 
+def splitk_ws(device):
+    """(fp32 partial slabs [16 slices x 16 rows x 16384], zeroed int32 tile tickets
+    [1024]) of the split-K GEMV (gemm_skinny.hip gemv_splitk); allocated before any
+    graph capture so captured graphs bake in stable pointers; tickets left at zero."""
+    d = torch.device(device)
+    key = ("splitk", d)
+    ws = _NORM_COUNTERS.get(key)
+    if ws is None:
+        ws = _NORM_COUNTERS[key] = (torch.empty(16 * 16 * 16384, dtype=torch.float32, device=d),
+                                    torch.zeros(1024, dtype=torch.int32, device=d))
+    return ws
+
+
+SPLITK_BIT = 128          # plan cfg bit: the split-K GEMV kernel (low bits = its cfg)
+
+
 def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bool:
     """Try the fused path for ``y = x w^T`` (``gated``: x = gate|up, y = down(SwiGLU(x)))
     followed by ``fused_add_rms_norm(y, residual, norm_w, eps, out)``.  Returns False
@@ -153,9 +169,43 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     if cfg < 0:
         return False
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if cfg & SPLITK_BIT:
+        part, tiles = splitk_ws(x.device)
+        _native.ops().gemv_splitk_norm(x, w, y, residual, norm_w, eps, out,
+                                       norm_counter(x.device), part, tiles, cfg & 127)
+        return True
     _native.ops().skinny_gemm_norm(x, w, y, residual, norm_w, eps, out,
                                    norm_counter(x.device), norm_partials(x.device), cfg)
     return True
+
+
+# (M, F, K) -> skinny cfg of the gate|up projection with the SwiGLU epilogue
+# (gemm_skinny.hip SWI: out [M, F] = silu(x Wg^T) * (x Wu^T)), or absent = unfused.
+_SWI_PLAN: dict[tuple[int, int, int], int] = {}
+
+
+def set_swiglu_plan(plan: dict) -> None:
+    _SWI_PLAN.clear()
+    _SWI_PLAN.update(plan)
+
+
+def linear_swiglu(x, w):
+    """act[M, F] = silu(x Wg^T) * (x Wu^T) for w = gate|up [2F, K] in one skinny kernel
+    when the start-up plan measured it faster than gate|up GEMM + silu_mul; None
+    otherwise (the caller runs the unfused path)."""
+    if not _SWI_PLAN or not _gpu(x) or x.stride(1) != 1 or x.stride(0) % 8:
+        return None
+    M, K = x.shape
+    F = w.shape[0] // 2
+    for m in _TUNED_MS:
+        if m >= M:
+            cfg = _SWI_PLAN.get((m, F, K), -1)
+            if cfg < 0:
+                return None
+            out = torch.empty((M, F), dtype=x.dtype, device=x.device)
+            _native.ops().skinny_gemm_swiglu(x, w, out, cfg)
+            return out
+    return None
 
 
 # (M, N, K) -> skinny cfg (NT = 2) whose epilogue applies RoPE to q/k and appends k/v

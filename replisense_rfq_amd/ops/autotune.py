@@ -15,7 +15,7 @@ import os
 import torch
 
 from . import (_native, set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan,
-               set_split_plan, silu_linear, silu_mul)
+               set_split_plan, set_swiglu_plan, silu_linear, silu_mul)
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -123,7 +123,8 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
     """o / down projection followed by the residual-add RMSNorm: the planned GEMM path
     (linear or silu_linear) + fused_add_rms_norm vs the skinny kernel that runs the
     norm in its last workgroup (one launch instead of two)."""
-    from . import NORM_FUSE_MAX_M, fused_add_rms_norm, linear, norm_counter, norm_partials
+    from . import (NORM_FUSE_MAX_M, SPLITK_BIT, fused_add_rms_norm, linear, norm_counter,
+                   norm_partials, splitk_ws)
 
     ops = _native.ops()
     N, K = ws[0].shape
@@ -132,6 +133,7 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
         return plan, report
     dev, dt = ws[0].device, ws[0].dtype
     counter, partials = norm_counter(dev), norm_partials(dev)
+    part, tiles = splitk_ws(dev)
     for M in ms:
         if M > NORM_FUSE_MAX_M:
             continue
@@ -154,9 +156,49 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
                                                           counter, partials, c), ws, reps)
             if t < t_best:
                 best, t_best = c, t
+        # the split-K GEMV with the in-launch per-tile reduction + norm (plain x only;
+        # tools/bench_gemv.py: KS 2-4, 4 waves, U 2-4 are its useful corner)
+        for c in ((8, 9, 12, 0) if not gated else ()):
+            if (K // 128) < (2 << (c & 3)):
+                continue
+            t = _time(lambda w, c=c: ops.gemv_splitk_norm(x, w, y, res, norm_w, eps, out,
+                                                          counter, part, tiles, c), ws, reps)
+            if t < t_best:
+                best, t_best = c | SPLITK_BIT, t
         if best >= 0:
             plan[(M, N, K, gated)] = best
         report.append(("down+norm" if gated else "o+norm", M, N, K, round(t_ref, 1), best,
+                       round(min(t_best, t_ref), 1)))
+    return plan, report
+
+
+def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: float = 0.97):
+    """gate|up projection + silu_mul (planned GEMM path) vs the skinny kernel with the
+    SwiGLU epilogue (gemm_skinny.hip SWI; 4 or 8 waves)."""
+    from . import NORM_FUSE_MAX_M, linear
+
+    ops = _native.ops()
+    N2, K = ws[0].shape
+    F = N2 // 2
+    plan, report = {}, []
+    if K % 128 or F % 16:
+        return plan, report
+    dev, dt = ws[0].device, ws[0].dtype
+    for M in ms:
+        if M > NORM_FUSE_MAX_M:
+            continue
+        x = torch.randn(M, K, device=dev, dtype=dt)
+        gu = torch.empty(M, N2, device=dev, dtype=dt)
+        act = torch.empty(M, F, device=dev, dtype=dt)
+        t_ref = _time(lambda w: silu_mul(linear(x, w, out=gu), out=act), ws, reps)
+        best, t_best = -1, t_ref * margin
+        for c in (0, 2):
+            t = _time(lambda w, c=c: ops.skinny_gemm_swiglu(x, w, act, c), ws, reps)
+            if t < t_best:
+                best, t_best = c, t
+        if best >= 0:
+            plan[(M, F, K)] = best
+        report.append(("gate_up+swiglu", M, N2, K, round(t_ref, 1), best,
                        round(min(t_best, t_ref), 1)))
     return plan, report
 
@@ -309,6 +351,14 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
             p2, r2 = tune_norm(groups["down"], ms, nw, gated=True)
             nplan.update(p2)
             nreport += r2
+            # the down projection on the SwiGLU output of the fused gate|up kernel
+            p3, r3 = tune_norm(groups["down"], ms, nw, gated=False)
+            nplan.update(p3)
+            nreport += [("down(act)+norm",) + tuple(r[1:]) for r in r3]
+        if "gate_up" in groups and os.environ.get("RFQ_FUSE_SWIGLU", "1") != "0":
+            wplan, wreport = tune_swiglu(groups["gate_up"], ms)
+            set_swiglu_plan(wplan)
+            nreport += wreport
         set_norm_plan(nplan)
         report += nreport
     if max_tokens > 0:

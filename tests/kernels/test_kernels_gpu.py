@@ -547,3 +547,57 @@ def test_skinny_norm_handoff_stress(gpu, M, cfg):
     torch.cuda.synchronize()
     assert bad == 0, f"{bad} of 300 launches read a stale tile"
     assert int(counter[0]) == 0
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("cfg", [0, 2])
+def test_skinny_gemm_swiglu(gpu, M, cfg):
+    """gate|up GEMM with the SwiGLU epilogue == the same tile's skinny GEMM followed
+    by silu_mul, bit for bit (same wave split: cfg 0 <-> 13, cfg 2 <-> 15)."""
+    torch.manual_seed(M + cfg)
+    F, K = 1024, 2048
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(2 * F, K, device=gpu) * 0.03).to(BF)
+    out = torch.empty(M, F, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm_swiglu(x, w, out, cfg)
+    gu = torch.empty(M, 2 * F, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm(x, w, gu, 13 if cfg == 0 else 15)
+    want = torch.empty(M, F, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.silu_mul(gu, want)
+    assert torch.equal(out, want)
+    # and against the fp32 torch reference of the op
+    g, u = (x.float() @ w.float().t()).split(F, dim=1)
+    _close(out, torch.nn.functional.silu(g) * u, 3e-2, 2e-2, f"swiglu M={M}")
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("cfg", [0, 1, 8, 9, 12, 13])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 14336)])
+def test_gemv_splitk(gpu, M, cfg, N, K):
+    """Split-K GEMV with the in-launch per-tile reduction vs an fp32 torch matmul;
+    the norm variant vs skinny GEMM + fused_add_rms_norm; repeated launches (tile
+    tickets and the norm counter must be left at zero)."""
+    torch.manual_seed(M * 7 + cfg)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(BF)
+    part = torch.empty(16 * 16 * 16384, device=gpu)
+    tiles = torch.zeros(1024, dtype=torch.int32, device=gpu)
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    ref_y = x.float() @ w.float().t()
+    for it in range(3):
+        torch.ops.rfq_amd.gemv_splitk(x, w, y, part, tiles, cfg)
+        _close(y, ref_y, 2e-2, 1e-2, f"gemv_splitk cfg={cfg} it={it}")
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
+    counter = torch.zeros(4, dtype=torch.int32, device=gpu)
+    res = torch.randn(M, N, device=gpu, dtype=BF)
+    for it in range(3):
+        res0 = res.clone()
+        out = torch.empty(M, N, device=gpu, dtype=BF)
+        torch.ops.rfq_amd.gemv_splitk_norm(x, w, y, res, nw, 1e-5, out, counter, part, tiles, cfg)
+        want_res = (y.float() + res0.float()).to(BF)
+        assert torch.equal(res, want_res), f"residual it={it}"
+        r = want_res.float()
+        want = r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+        _close(out, want, 3e-2, 2e-2, f"gemv_splitk_norm cfg={cfg} it={it}")
+    torch.cuda.synchronize()
+    assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
