@@ -45,7 +45,7 @@ void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16
                                bool, hipStream_t);
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                         const int32_t*, int, bf16_t*, int64_t, int, int, float, hipStream_t);
+                         const int32_t*, int, bf16_t*, int64_t, int, int, float, int, hipStream_t);
 void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t*, int,
                            const int32_t*, const float*, const uint64_t*, float*, int32_t*, int,
                            hipStream_t);
@@ -387,7 +387,7 @@ void attn_decode_shared(const Tensor& q, const Tensor& k_cache, const Tensor& v_
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
                   const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_qblk,
-                  const Tensor& out, int64_t Hq, int64_t Hkv, double scale) {
+                  const Tensor& out, int64_t Hq, int64_t Hkv, double scale, int64_t qblk) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
   CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
@@ -397,12 +397,15 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
               "attn_prefill: cache must be [blocks, Hkv, 32, 128]");
   TORCH_CHECK(Hq % Hkv == 0 && (Hq / Hkv) % 4 == 0, "attn_prefill: GQA group must be a multiple of 4");
   TORCH_CHECK(work_seq.numel() == work_qblk.numel(), "work list mismatch");
+  const int64_t nw = qblk * (Hq / Hkv) / 32;
+  TORCH_CHECK((qblk == 32 || qblk == 64) && (nw == 4 || nw == 8),
+              "attn_prefill: qblk * (Hq / Hkv) must be 128 or 256 (4 or 8 waves)");
   rfq::launch_attn_prefill(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
                            block_tables.data_ptr<int32_t>(), block_tables.stride(0),
                            seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
                            seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(),
                            work_qblk.data_ptr<int32_t>(), work_seq.numel(), bpm(out),
-                           out.stride(0), Hq, Hkv, (float)scale, cur_stream());
+                           out.stride(0), Hq, Hkv, (float)scale, (int)qblk, cur_stream());
 }
 
 void sample_partial(const Tensor& logits, int64_t v0, const Tensor& mask_table,
@@ -676,7 +679,7 @@ TORCH_LIBRARY(rfq_amd, m) {
         "int Hq, int Hkv, float scale, int tiles_per_item, bool run_meta) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
-        "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale) -> ()");
+        "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale, int qblk=32) -> ()");
   m.def("sample_partial(Tensor logits, int v0, Tensor mask_table, Tensor mask_idx, Tensor temps, "
         "Tensor seeds, Tensor(a!) part_val, Tensor(b!) part_idx) -> ()");
   m.def("sample_final(Tensor part_val, Tensor part_idx, Tensor(a!) out) -> ()");

@@ -4,9 +4,17 @@
 // prefill / grammar jump-forward extends).
 //
 // Structure (gfx950):
-//   * workgroup = 4 waves = 4 query heads of ONE kv head x one 32-query block, so
-//     the K/V tiles staged in LDS are shared by the whole GQA group;
-//   * 64-key tiles (two 32-token pages) are staged through registers into LDS:
+//   * workgroup = 8 waves = the G query heads of ONE kv head x QB queries
+//     (QB = 256 / G: 64 queries for Llama-3-8B / Mixtral, G = 4; 32 for Llama-3-70B,
+//     G = 8), so every K/V tile staged in LDS feeds 256 (query, head) rows; each
+//     wave owns 32 queries of one head (cdna_hip_programming.md Appendix B "Fused
+//     attention prefill": 8 waves x 32 rows, KVBLK 64);
+//   * 64-key tiles (two 32-token pages), double-buffered in LDS with the
+//     async-STAGE split (T14): a tile's global loads are issued two phases before
+//     they are written to the other buffer; raw s_barrier + lgkmcnt(0) only, so the
+//     loads stay in flight across barriers;
+//   * ping-pong: the two halves of the workgroup run half a tile apart (QK^T +
+//     softmax of one group beside the PV MFMAs of the other on every SIMD);
 //       K image  [64][128] bf16, 16-B chunk ch of row r at ch ^ (r & 15)
 //                (ds_read_b128 row reads conflict-free, T2),
 //       V image  [64][128] bf16, chunk ch of row r at ch ^ ((r & 3) << 2)
@@ -16,7 +24,9 @@
 //     shuffle per row statistic);
 //   * O^T = V^T P^T with the S^T accumulators reused as the bf16 B operand
 //     (accumulator-as-operand, §3) — O keeps the query on the lane, so the
-//     rescale by exp2(m_old - m_new) needs no data movement.
+//     rescale by exp2(m_old - m_new) needs no data movement;
+//   * causal: a wave skips the MFMAs of tiles past its last query; the grid runs
+//     the work list back to front so the heaviest (latest) query blocks start first.
 #include "common.h"
 
 namespace rfq {
@@ -25,25 +35,38 @@ constexpr int kPD = 128;
 constexpr int kPPage = 32;
 constexpr int kKT = 64;  // keys per tile
 constexpr int kQB = 32;  // queries per wave
+constexpr int kStage = 2 * kKT * kPD;   // K + V elements per LDS stage
+constexpr float kRescale = 8.f;         // defer-max threshold (log2 units)
 
-__global__ __launch_bounds__(256) void attn_prefill_kernel(
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_qblk, bf16_t* __restrict__ out, int64_t out_stride, int Hq,
-    int Hkv, float scale_log2) {
+    int Hkv, float scale_log2, int hsplit) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* k_lds = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* v_lds = k_lds + kKT * kPD;
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+  constexpr int NT = NW * 64;
+  constexpr int NCH = kKT * 16 / NT;          // 16-B chunks of K (and of V) per thread per tile
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h2 = lane >> 5;
-  const int seq = work_seq[blockIdx.x];
-  const int qs = work_qblk[blockIdx.x] * kQB;
   const int G = Hq / Hkv;
-  const int head = blockIdx.y * 4 + wid;
-  const int kvh = head / G;
+  const int Gw = G / hsplit;                  // query heads per workgroup
+  const int QB = NW * kQB / Gw;               // queries per work item
+  // 1-D grid of num_work x hsplit x Hkv: consecutive workgroups land on consecutive
+  // XCDs, so kv head = id % Hkv keeps every workgroup of one kv head on one XCD (its
+  // L2 holds that head's K/V; T1), and the work list runs heaviest (latest) blocks
+  // first.  hsplit = 2 halves the heads per workgroup when the grid is small.
+  const int num_work = gridDim.x / (Hkv * hsplit);
+  const int kvh = blockIdx.x % Hkv;
+  const int rest = blockIdx.x / Hkv;
+  const int wi = num_work - 1 - rest / hsplit;
+  const int seq = work_seq[wi];
+  const int head = kvh * G + (rest % hsplit) * Gw + wid % Gw;
+  const int qs = work_qblk[wi] * QB + (wid / Gw) * kQB;   // this wave's first query
   const int q_len = seq_q_len[seq], kv_len = seq_kv_len[seq];
   const int ctx0 = kv_len - q_len;  // absolute position of query 0
   const int tok0 = seq_q_start[seq];
@@ -59,109 +82,197 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
     for (int ks = 0; ks < 8; ++ks) qf[ks] = reinterpret_cast<const s16x8*>(qrow + 16 * ks + 8 * h2)[0];
   }
   const int qpos = ctx0 + qi;
-  const int last_q = min(qs + kQB, q_len) - 1;
-  const int kv_end = min(kv_len, ctx0 + last_q + 1);  // keys this workgroup needs
+  // keys the workgroup needs (its last query) and this wave needs
+  const int wg_last_q = min(work_qblk[wi] * QB + QB, q_len) - 1;
+  const int kv_end = min(kv_len, ctx0 + wg_last_q + 1);
+  const int w_last_q = min(qs + kQB, q_len) - 1;
+  const int w_kv_end = w_last_q < qs ? 0 : min(kv_len, ctx0 + w_last_q + 1);
 
+  auto load = [&](int kt, s16x8* kr, s16x8* vr) {
+    // the tile's two pages: wave-uniform block-table reads (scalar loads)
+    const int pg0 = kt / kPPage;
+    const int64_t page_a = bt[pg0];
+    const int64_t page_b = kt + kPPage < kv_end ? bt[pg0 + 1] : page_a;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = threadIdx.x + NT * i, row = idx >> 4, ch = idx & 15;
+      const int key = kt + row;
+      kr[i] = vr[i] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+      if (key < kv_end) {
+        const int64_t page = row < kPPage ? page_a : page_b;
+        const int64_t off = ((page * Hkv + kvh) * kPPage + (key % kPPage)) * kPD;
+        kr[i] = reinterpret_cast<const s16x8*>(k_cache + off)[ch];
+        vr[i] = reinterpret_cast<const s16x8*>(v_cache + off)[ch];
+      }
+    }
+  };
+  auto store = [&](int buf, const s16x8* kr, const s16x8* vr) {
+    bf16_t* kl = lds + buf * kStage;
+    bf16_t* vl = kl + kKT * kPD;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int idx = threadIdx.x + NT * i, row = idx >> 4, ch = idx & 15;
+      reinterpret_cast<s16x8*>(kl + row * kPD)[ch ^ (row & 15)] = kr[i];
+      reinterpret_cast<s16x8*>(vl + row * kPD)[ch ^ ((row & 3) << 2)] = vr[i];
+    }
+  };
+
+  // online softmax state in raw score units (scale applied inside the exp2's FMA)
   float m_run = -INFINITY, l_run = 0.f;
+  const float rescale_raw = kRescale / scale_log2;
   f32x16 o[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[m][i] = 0.f;
+  f32x16 s[2];                                 // S^T, then P^T, of the current tile
 
-  for (int kt = 0; kt < kv_end; kt += kKT) {
-    // ---- stage K/V tile (64 rows x 16 chunks each) : thread -> 4 chunks of K and V
+  // Ping-pong phases: the waves of group 1 run half a tile behind group 0, so in
+  // every barrier interval one group's QK^T + softmax (VALU / transcendental) runs
+  // beside the other group's PV MFMAs on the same SIMD instead of both groups
+  // queueing for the same unit.  Phase p: group g works on half-tile p - g (stage 0 =
+  // QK^T + softmax, stage 1 = PV).  Tile T+1 is loaded at phase 2T and written to the
+  // other LDS buffer at the end of phase 2T+1, after both groups left tile T-1.
+  const int grp = wid >= NW / 2 ? 1 : 0;
+  const int ntiles = (kv_end + kKT - 1) / kKT;
+  s16x8 kr[NCH], vr[NCH];
+  // the second-dispatched half loses every VALU arbitration at equal priority: one
+  // static s_setprio for it, no per-phase flips (MI355X_MICROARCH "Two waves per SIMD" 4)
+  if (grp) __builtin_amdgcn_s_setprio(1);
+  load(0, kr, vr);
+  store(0, kr, vr);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int p = 0; p <= 2 * ntiles; ++p) {
+    const int T = p >> 1;
+    if (!(p & 1) && T + 1 < ntiles) load((T + 1) * kKT, kr, vr);   // in flight 2 phases
+    const int tp = p - grp;
+    const int t = tp >> 1, kt = t * kKT;
+    if (tp >= 0 && t < ntiles && kt < w_kv_end) {
+      const bf16_t* k_lds = lds + (t & 1) * kStage;
+      const bf16_t* v_lds = k_lds + kKT * kPD;
+      if (!(tp & 1)) {
+        // ---- S^T for two 32-key subtiles ----
+        // K fragments are read a whole subtile ahead of the MFMAs that use them: the
+        // 8 reads of subtile 1 issue between subtile 0's MFMAs (each waits only for its
+        // own fragment), so no MFMA waits out a full LDS round trip
+        const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                               0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        auto kfrag = [&](int st, int ks) {
+          const int row = 32 * st + r, ch = 2 * ks + h2;
+          return reinterpret_cast<const s16x8*>(k_lds + row * kPD)[ch ^ (row & 15)];
+        };
+        s16x8 ka[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (threadIdx.x >> 4) + 16 * i, ch = threadIdx.x & 15;
-      const int key = kt + row;
-      s16x8 kv = (s16x8){0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
-      if (key < kv_end) {
-        const int64_t page = bt[key / kPPage];
-        const int64_t off = ((page * Hkv + kvh) * kPPage + (key % kPPage)) * kPD;
-        kv = reinterpret_cast<const s16x8*>(k_cache + off)[ch];
-        vv = reinterpret_cast<const s16x8*>(v_cache + off)[ch];
-      }
-      reinterpret_cast<s16x8*>(k_lds + row * kPD)[ch ^ (row & 15)] = kv;
-      reinterpret_cast<s16x8*>(v_lds + row * kPD)[ch ^ ((row & 3) << 2)] = vv;
-    }
-    __syncthreads();
-
-    // ---- S^T for two 32-key subtiles ----
-    f32x16 s[2];
+        for (int ks = 0; ks < 8; ++ks) ka[ks] = kfrag(0, ks);
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+        for (int ks = 0; ks < 8; ++ks) {
+          s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[ks]), as_bf16x8(qf[ks]),
+                                                         ks == 0 ? zero16 : s[0], 0, 0, 0);
+          ka[ks] = kfrag(1, ks);
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[st][i] = 0.f;
-      const int row = 32 * st + r;
+        for (int ks = 0; ks < 8; ++ks)
+          s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[ks]), as_bf16x8(qf[ks]),
+                                                         ks == 0 ? zero16 : s[1], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // 8 DS reads
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const int ch = 2 * ks + h2;
-        const s16x8 a = reinterpret_cast<const s16x8*>(k_lds + row * kPD)[ch ^ (row & 15)];
-        s[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(qf[ks]), s[st], 0, 0, 0);
-      }
-    }
-    // lane: S^T[key 32st + (i&3) + 8(i>>2) + 4h2][query r]
-    float mx = -INFINITY;
+        for (int ks = 0; ks < 8; ++ks) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA ks of subtile 0
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // read ks of subtile 1
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // subtile 1
+        // lane: S^T[key 32st + (i&3) + 8(i>>2) + 4h2][query r]
+        if (kt + kKT > ctx0 + qs || kt + kKT > kv_end) {
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+          for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h2;
-        float v = s[st][i] * scale_log2;
-        if (key > qpos || key >= kv_end) v = -INFINITY;
-        s[st][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = fast_exp2(m_run - m_use);
-    float psum = 0.f;
+            for (int i = 0; i < 16; ++i) {
+              const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h2;
+              if (key > qpos || key >= kv_end) s[st][i] = -INFINITY;
+            }
+        }
+        float mx = -INFINITY;
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fast_exp2(s[st][i] - m_use);
-        s[st][i] = p;
-        psum += p;
-      }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[st][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        // defer-max (T13): keep the running max -- and skip rescaling O -- unless a
+        // row's max grew by more than kRescale (log2 units); p <= 2^kRescale meanwhile
+        if (__any(mx > m_run + rescale_raw)) {
+          const float m_new = fmaxf(m_run, mx);
+          const float alpha = m_new == -INFINITY ? 1.f : fast_exp2((m_run - m_new) * scale_log2);
+          l_run *= alpha;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) o[m] *= alpha;
-
-    // ---- O^T += V^T P^T ----
-    const int gi = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+          for (int m = 0; m < 4; ++m) o[m] *= alpha;
+          m_run = m_new;
+        }
+        const float nb = m_run == -INFINITY ? 0.f : -m_run * scale_log2;
+        float psum = 0.f;
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int ksub = 0; ksub < 2; ++ksub) {
-        float pv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pv[j] = s[st][8 * ksub + j];
-        const s16x8 pb = pack8(pv);
-        const int r0 = 32 * st + 16 * ksub + 4 * h2 + qq;
-        const int r1 = r0 + 8;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
+          for (int i = 0; i < 16; ++i) {
+            const float pr = fast_exp2(fmaf(s[st][i], scale_log2, nb));
+            s[st][i] = pr;
+            psum += pr;
+          }
+        l_run += psum;
+      } else {
+        // ---- O^T += V^T P^T ----
+        // 4 key chunks x 4 dh tiles; the V^T fragments of chunk c + 1 (8 transposing
+        // reads) are in flight while chunk c's 4 MFMAs run
+        const int gi = lane >> 4, ii = lane & 15, qq = ii >> 2, pp = ii & 3;
+        auto vfrag = [&](int c, int m) {
+          const int r0 = 16 * c + 4 * h2 + qq, r1 = r0 + 8;
           const int col = 32 * m + 16 * (gi & 1) + 4 * pp;
           const int ch = col >> 3, sub = col & 7;
           const s16x4 a0 = ds_read_tr16(v_lds + r0 * kPD + ((ch ^ ((r0 & 3) << 2)) << 3) + sub);
           const s16x4 a1 = ds_read_tr16(v_lds + r1 * kPD + ((ch ^ ((r1 & 3) << 2)) << 3) + sub);
-          const s16x8 a = (s16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-          o[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(pb), o[m], 0, 0, 0);
+          return (s16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        };
+        s16x8 va[2][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) va[0][m] = vfrag(0, m);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c < 3) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) va[(c + 1) & 1][m] = vfrag(c + 1, m);
+          }
+          float pv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pv[j] = s[c >> 1][8 * (c & 1) + j];
+          const s16x8 pb = pack8(pv);
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            o[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(va[c & 1][m]), as_bf16x8(pb),
+                                                           o[m], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // chunks 0 and 1
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // chunk c
+          if (c < 2) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // chunk c + 2
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
     }
-    __syncthreads();
+    if ((p & 1) && T + 1 < ntiles) store((T + 1) & 1, kr, vr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS stores done; loads stay in flight
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 
   float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  if (!qvalid) return;
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16_t* orow = out + (int64_t)(tok0 + qi) * out_stride + (int64_t)head * kPD;
-  // O^T lane: dh rows (i&3) + 8(i>>2) + 4h2 of each 32-row tile m
+  // Epilogue (T21): the loop's last barrier has retired every K/V read, so each wave
+  // stages its 32 x 128 O tile in its own 8 KB of LDS (16-B chunks XOR-swizzled by
+  // row) and stores whole rows, 16 B per lane -- 8 dwordx4 row stores instead of 16
+  // dwordx2 stores that each touch 32 rows.
+  bf16_t* ol = lds + wid * (kQB * kPD);
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -169,24 +280,47 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(
       uint2 w;
       w.x = pack_bf16x2(o[m][4 * k + 0] * inv, o[m][4 * k + 1] * inv);
       w.y = pack_bf16x2(o[m][4 * k + 2] * inv, o[m][4 * k + 3] * inv);
-      *reinterpret_cast<uint2*>(orow + 32 * m + 8 * k + 4 * h2) = w;
+      *reinterpret_cast<uint2*>(ol + r * kPD + (((4 * m + k) ^ (r & 15)) << 3) + 4 * h2) = w;
     }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int cc = lane & 15;
+#pragma unroll
+  for (int j = 0; j < kQB / 4; ++j) {
+    const int row = (lane >> 4) + 4 * j;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ol + row * kPD + ((cc ^ (row & 15)) << 3));
+    if (qs + row < q_len)
+      *reinterpret_cast<u32x4*>(out + (int64_t)(tok0 + qs + row) * out_stride +
+                                (int64_t)head * kPD + 8 * cc) = v;
+  }
 }
 
+// qblk: queries per work item (the packer's prefill block): NW = qblk * G / 32 waves.
 void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                          const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
                          const int32_t* seq_q_start, const int32_t* seq_q_len,
                          const int32_t* seq_kv_len, const int32_t* work_seq,
                          const int32_t* work_qblk, int num_work, bf16_t* out, int64_t out_stride,
-                         int Hq, int Hkv, float scale, hipStream_t s) {
+                         int Hq, int Hkv, float scale, int qblk, hipStream_t s) {
   if (num_work == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_work, Hq / 4);
-  const size_t lds = 2 * kKT * kPD * sizeof(bf16_t);
-  attn_prefill_kernel<<<grid, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
-                                             bt_stride, seq_q_start, seq_q_len, seq_kv_len,
-                                             work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                             scale_log2);
+  const int G = Hq / Hkv;
+  // hsplit = 2 (half the query heads per workgroup, twice the workgroups) measured
+  // slower at B = 1 (S 2048: 104 vs 89 us; profiles/r2_prefill_attention.md): a small
+  // grid here is bound by its heaviest causal block's latency, not by idle CUs
+  const int hsplit = 1;
+  const int nw = qblk * G / (kQB * hsplit);
+  dim3 grid(num_work * Hkv * hsplit);
+  const size_t lds = 2 * kStage * sizeof(bf16_t);
+  if (nw == 8)
+    attn_prefill_kernel<8><<<grid, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                  bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                  work_seq, work_qblk, out, out_stride, Hq, Hkv,
+                                                  scale_log2, hsplit);
+  else
+    attn_prefill_kernel<4><<<grid, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                  bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                  work_seq, work_qblk, out, out_stride, Hq, Hkv,
+                                                  scale_log2, hsplit);
 }
 
 }  // namespace rfq

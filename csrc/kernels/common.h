@@ -33,7 +33,10 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  // fptrunc <2 x float> -> <2 x bfloat>: a single v_cvt_pk_bf16_f32 (RNE)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }
 
 __device__ __forceinline__ void unpack8(const s16x8& v, float* f) {
@@ -42,10 +45,10 @@ __device__ __forceinline__ void unpack8(const s16x8& v, float* f) {
 }
 
 __device__ __forceinline__ s16x8 pack8(const float* f) {
-  s16x8 v;
+  u32x4 w;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(f[i]);
-  return v;
+  for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
+  return __builtin_bit_cast(s16x8, w);
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(const s16x8& v) {

@@ -322,7 +322,7 @@ int64_t EngineCore::schedule_and_pack(int32_t* header, int32_t* payload, int64_t
   int32_t S = (int32_t)A.size();
   for (auto& r : B) {
     TB += r.q;
-    WB += (r.q + 31) / 32;
+    WB += (r.q + cfg_.prefill_qblk - 1) / cfg_.prefill_qblk;
     maxb = std::max(maxb, (int32_t)seqs_[r.id].blocks.size());
     const Seq& s = seqs_[r.id];
     S += (s.num_cached + r.q == (int32_t)s.tokens.size());
@@ -410,7 +410,7 @@ int64_t EngineCore::schedule_and_pack(int32_t* header, int32_t* payload, int64_t
     b_qs[j] = t - TA;
     b_ql[j] = r.q;
     b_kvl[j] = p0 + r.q;
-    const int32_t nqb = (r.q + 31) / 32;
+    const int32_t nqb = (r.q + cfg_.prefill_qblk - 1) / cfg_.prefill_qblk;
     for (int32_t c = 0; c < nqb; ++c, ++w) {
       b_ws[w] = j;
       b_wq[w] = c;

@@ -79,6 +79,7 @@ struct CoreConfig {
   int32_t group = 4;                     // q heads per kv head (decode work-item tiling)
   int32_t hkv = 8;                       // local kv heads (decode split heuristic)
   int32_t decode_tiles = 1;              // 16-column tiles per decode attention work item
+  int32_t prefill_qblk = 32;             // queries per prefill attention work item (32 | 64)
   bool jump_forward = true;
   bool prefix_cache = true;
   bool is_cuda = true;

@@ -184,6 +184,9 @@ PYBIND11_MODULE(_runtime, m) {
              geti("group", cfg.group);
              geti("hkv", cfg.hkv);
              geti("decode_tiles", cfg.decode_tiles);
+             geti("prefill_qblk", cfg.prefill_qblk);
+             if (cfg.prefill_qblk != 32 && cfg.prefill_qblk != 64)
+               throw py::value_error("prefill_qblk must be 32 or 64");
              getb("jump_forward", cfg.jump_forward);
              getb("prefix_cache", cfg.prefix_cache);
              getb("is_cuda", cfg.is_cuda);

@@ -150,7 +150,7 @@ class LLMEngine:
                     jump_forward=c.jump_forward, prefix_cache=c.prefix_cache,
                     is_cuda=self.device.type == "cuda", use_graphs=c.use_graphs,
                     token_mults=list(TOKEN_MULTS), eos_ids=list(self.tokenizer.eos_ids),
-                    decode_tiles=c.decode_tiles)
+                    decode_tiles=c.decode_tiles, prefill_qblk=self.runner.prefill_qblk)
         g = self.grammar.native if self.grammar is not None else None
         if self.grammar is not None and g is None:
             raise RuntimeError("the native grammar automaton failed to build")

@@ -78,6 +78,7 @@ class ModelRunner:
         self._stage = None                   # its numpy view
         self._header = np.zeros(HEADER, np.int32)
         self.decode_tiles = int(getattr(cfg, "decode_tiles", 1))
+        self.prefill_qblk = ops.prefill_qblk(model.hq, model.hkv) if self.is_cuda else 32
         self.ring = None
         if tp.enabled:
             self._setup_control_plane()
@@ -120,7 +121,7 @@ class ModelRunner:
             num_prefill_tokens=T - TA, pf_block_tables=v["b_bt"], pf_q_start=v["b_qs"],
             pf_q_len=v["b_ql"], pf_kv_len=v["b_kvl"], work_seq=v["b_ws"], work_qblk=v["b_wq"],
             logits_idx=v["lidx"], decode_splits=int(h[H_SPLITS]),
-            decode_tiles=max(1, int(h[H_TILES])))
+            decode_tiles=max(1, int(h[H_TILES])), prefill_qblk=self.prefill_qblk)
 
     def _staging(self, words: int) -> np.ndarray:
         if self._stage is None or self._stage.size < words:

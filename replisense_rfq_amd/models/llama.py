@@ -57,6 +57,7 @@ class ForwardMeta:
     pf_kv_len: torch.Tensor | None = None          # [P]
     work_seq: torch.Tensor | None = None           # [W]
     work_qblk: torch.Tensor | None = None          # [W]
+    prefill_qblk: int = 32                         # queries per prefill work item
     logits_idx: torch.Tensor | None = None         # [S] int64 rows needing logits
     decode_splits: int = 1
     decode_tiles: int = 1          # column tiles per decode work item (attn_decode.hip)
@@ -247,7 +248,7 @@ class DecoderLM:
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
-                             self.scale)
+                             self.scale, m.prefill_qblk)
 
     # ------------------------------------------------------------- conveniences
     def weight_bytes(self) -> int:

@@ -406,11 +406,19 @@ def attn_decode_shared(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len
                          out, Hq, Hkv, scale)
 
 
+def prefill_qblk(Hq: int, Hkv: int) -> int:
+    """Queries per prefill work item: 256 (query, head) rows per workgroup (8 waves)
+    -> 64 queries at GQA group 4 (Llama-3-8B, Mixtral), 32 at group 8 (Llama-3-70B)."""
+    return 64 if Hq // Hkv == 4 else 32
+
+
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
-                 work_seq, work_qblk, out, Hq, Hkv, scale):
+                 work_seq, work_qblk, out, Hq, Hkv, scale, qblk: int = 32):
+    """Causal paged prefill attention; the work list holds (sequence, query block of
+    ``qblk`` queries) items (qblk * Hq / Hkv must be 128 or 256)."""
     if _gpu(q):
         _native.ops().attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len,
-                                   seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale)
+                                   seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale, qblk)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
                          work_seq, work_qblk, out, Hq, Hkv, scale)

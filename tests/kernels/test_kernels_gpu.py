@@ -211,32 +211,38 @@ def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
     torch.testing.assert_close(out2[:T - 1], out[:T - 1], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])
-def test_attn_prefill(gpu, Hq, Hkv):
+@pytest.mark.parametrize("Hq,Hkv,qblk,spike", [(32, 8, 32, False), (32, 8, 64, False),
+                                               (8, 1, 32, False), (64, 8, 32, False),
+                                               (32, 8, 64, True)])
+def test_attn_prefill(gpu, Hq, Hkv, qblk, spike):
+    """spike: a few late keys get a large norm so a row's running max jumps past the
+    defer-max threshold mid-stream (forces the rescale branch, guide rule 26)."""
     torch.manual_seed(6)
     # (q_len, kv_len): fresh prompt, prefix-cache hit, 1-token extend, chunk
     cases = [(300, 300), (77, 542), (1, 65), (64, 64), (33, 1000)]
     qlens = [c[0] for c in cases]
     kvlens = [c[1] for c in cases]
     k, v = _paged_cache(512, Hkv, gpu, seed=7)
+    if spike:
+        k[::7, :, 5] *= 40.0                   # every 7th page: one key row 40x larger
     bt = _block_tables(kvlens, 512, gpu, seed=1)
     T = sum(qlens)
     starts = torch.tensor([sum(qlens[:i]) for i in range(len(qlens))], dtype=torch.int32)
     q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
     ws, wq = [], []
     for s, ql in enumerate(qlens):
-        for j in range((ql + 31) // 32):
+        for j in range((ql + qblk - 1) // qblk):
             ws.append(s)
             wq.append(j)
     args = [torch.tensor(a, dtype=torch.int32, device=gpu) for a in (qlens, kvlens, ws, wq)]
     out = torch.zeros(T, Hq * 128, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(128)
     ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out, Hq,
-                     Hkv, scale)
+                     Hkv, scale, qblk)
     exp = torch.zeros(T, Hq * 128, dtype=BF)
     ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), starts, args[0].cpu(), args[1].cpu(),
                      None, None, exp, Hq, Hkv, scale)
-    _close(out, exp, 2e-2, 0, f"attn_prefill Hq={Hq}")
+    _close(out, exp, 2e-2, 0, f"attn_prefill Hq={Hq} qblk={qblk}")
 
 
 def test_sampler_masks_and_gumbel(gpu):
