@@ -45,7 +45,7 @@ def run(B, S, Hq, Hkv, iters=10):
     us = e0.elapsed_time(e1) / iters * 1e3
     flops = B * 2.0 * S * S * 128 * Hq
     # numerics spot check of the first sequence against an fp32 torch reference
-    if B <= 4 and not os.environ.get("RFQ_PREFILL_DBG"):
+    if B <= 4:
         from replisense_rfq_amd.ops import reference as ref
 
         exp = torch.zeros(S, Hq * 128, dtype=torch.bfloat16)
