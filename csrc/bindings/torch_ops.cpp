@@ -56,6 +56,8 @@ void launch_moe_route(const bf16_t*, int64_t, const bf16_t*, int, int, int, int,
 void launch_moe_align(const int32_t*, int, int, int, int32_t*, int32_t*, int32_t*, int32_t*,
                       int32_t*, int, int, hipStream_t);
 void launch_moe_gather(const bf16_t*, int64_t, const int32_t*, int, int, int, bf16_t*, hipStream_t);
+void launch_moe_gemm8(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, const int32_t*,
+                      const int32_t*, int, int, int, int, int64_t, int, bool, hipStream_t);
 void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, const int32_t*,
                              int, int, int, int, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
@@ -627,6 +629,28 @@ void moe_grouped_gemm(const Tensor& x, const Tensor& w, const Tensor& out,
                                cur_stream());
 }
 
+// 8-wave 128x256 grouped GEMM (moe.hip moe_gemm8_kernel).  swiglu: w = [E, 2F, K]
+// (gate | up), out = [rows, F] = silu(x Wg^T) * (x Wu^T); else out = [rows, N] = x W^T.
+void moe_gemm8(const Tensor& x, const Tensor& w, const Tensor& out,
+               const Tensor& expert_of_block, const Tensor& num_blocks,
+               const Tensor& expert_offsets, bool swiglu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
+  const int E = w.size(0), N = w.size(1), K = w.size(2);
+  const int n_out = swiglu ? N / 2 : N;
+  TORCH_CHECK(x.size(1) == K && out.size(1) == n_out && out.size(0) == x.size(0),
+              "moe gemm8 shape");
+  TORCH_CHECK(K % 64 == 0 && (swiglu ? (N % 2 == 0 && n_out % 128 == 0) : N % 256 == 0),
+              "moe gemm8: K % 64, N % 256 (F % 128 with swiglu)");
+  TORCH_CHECK(x.size(0) % 128 == 0, "moe gemm8: rows must be padded to 128");
+  TORCH_CHECK(expert_of_block.numel() >= x.size(0) / 128, "expert_of_block too short");
+  TORCH_CHECK(expert_offsets.numel() >= E + 1, "expert_offsets too short");
+  rfq::launch_moe_gemm8(bp(x), bp(w), bpm(out), expert_of_block.data_ptr<int32_t>(),
+                        num_blocks.data_ptr<int32_t>(), expert_offsets.data_ptr<int32_t>(),
+                        x.size(0) / 128, n_out, K, E, N, n_out, swiglu, cur_stream());
+}
+
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
 void moe_combine(const Tensor& y, const Tensor& inv_pos, const Tensor& weights, int64_t topk,
                  const Tensor& out) {
@@ -689,6 +713,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("moe_align(Tensor topk_ids, int E, int block_m, Tensor(a!) sorted_ids, Tensor(b!) inv_pos, "
         "Tensor(c!) expert_of_block, Tensor(d!) expert_offsets, Tensor(e!) num_blocks) -> ()");
   m.def("moe_gather(Tensor x, Tensor sorted_ids, int topk, Tensor(a!) out) -> ()");
+  m.def("moe_gemm8(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
+        "Tensor num_blocks, Tensor expert_offsets, bool swiglu) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
         "Tensor num_blocks) -> ()");
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
@@ -722,6 +748,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gather", &moe_gather);
   m.impl("moe_grouped_gemm", &moe_grouped_gemm);
+  m.impl("moe_gemm8", &moe_gemm8);
   m.impl("moe_combine", &moe_combine);
   m.impl("moe_skinny_splitk", &moe_skinny_splitk);
   m.impl("moe_combine_splitk", &moe_combine_splitk);

@@ -495,6 +495,201 @@ void launch_moe_gather(const bf16_t* x, int64_t x_stride, const int32_t* sorted_
                                                                           P, d, topk, out);
 }
 
+// ------------------------------------------------------ grouped GEMM, 8 waves
+// out[r, n] = sum_k x[r, k] * w[e(r), n, k] on a 128 (rows) x 256 (weight rows) tile,
+// K-step 64, 512 threads = 8 waves as 2 (64 rows) x 4 (64 weight rows).
+//  * operands swapped (C^T = W X^T): the weight tile is the MFMA A operand, so a
+//    lane ends up holding 4 consecutive output columns of one row (8-byte stores)
+//    and, with SWI, the gate and up values of the same (row, column) -- the wave's
+//    64 weight rows are 32 gate rows + the 32 matching up rows (up_off apart in w),
+//    so the SwiGLU epilogue writes act directly (no h13 round trip, no silu_mul);
+//  * LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring (3 x 48 KB): stage k+2
+//    is issued while stage k is multiplied and waited with a counted vmcnt, one raw
+//    barrier per K-step (the in-flight stage survives it);
+//  * images [rows][64 k] with chunk ch of row r at ch ^ ((r >> 1) & 7) (T2), the
+//    swizzle applied on the DMA source address (lane-linear destination).
+// Block order (weight-tile reuse): the ~2 GB of Mixtral w13 is far larger than L2
+// and the MALL, so every (expert, weight tile) must be consumed by all of that
+// expert's row blocks while it is resident.  The live blocks (< num_blocks x ntn)
+// are renumbered expert-major, then weight tile, then row block, and that order is
+// laid out contiguously per XCD (bijective T1 remap over the live count, so
+// padding capacity does not unbalance the XCDs): the few row blocks of one expert
+// that share a weight tile run back to back on one XCD and hit its L2.
+constexpr int kM8 = 128, kN8 = 256, kK8 = 64;
+constexpr int kStage8 = (kM8 + kN8) * kK8;        // bf16 elements per stage
+constexpr int kRing8 = 3;
+
+template <bool SWI>
+__global__ __launch_bounds__(512) void moe_gemm8_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+    const int32_t* __restrict__ expert_of_block, const int32_t* __restrict__ num_blocks,
+    const int32_t* __restrict__ expert_offsets, int n_out, int K, int E, int64_t w_rows,
+    int up_off) {
+  extern __shared__ __attribute__((aligned(16))) char smem8[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem8);
+  const int ntn = SWI ? n_out / 128 : n_out / kN8;
+  const int nlive = *num_blocks * ntn;
+  const int bid = blockIdx.x;
+  if (bid >= nlive) return;
+  const int q8 = nlive >> 3, r8 = nlive & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int e = expert_of_block[wg / ntn];
+  if (e < 0 || e >= E) return;      // padding block, or a remote expert's segment (EP)
+  const int s0 = expert_offsets[e] / kM8, nbe = expert_offsets[e + 1] / kM8 - s0;
+  const int local = wg - s0 * ntn;
+  const int cn = local / nbe, rb = s0 + local % nbe;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h2 = lane >> 5;
+  const int wm = wid & 1, wn = wid >> 1;
+  const bf16_t* xa = x + (int64_t)rb * kM8 * K;
+  const bf16_t* we = w + (int64_t)e * w_rows * K;
+
+  // DMA: per stage 16 (A) + 32 (B) wave-instructions of 1 KiB (8 rows of 128 B);
+  // wave w issues A pieces 2w, 2w+1 and B pieces 4w..4w+3
+  const int prow = lane >> 3, pch = lane & 7;
+  const bf16_t* asrc[2];
+  const bf16_t* bsrc[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * wid + i) + prow;
+    asrc[i] = xa + (int64_t)row * K + 8 * (pch ^ ((row >> 1) & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 8 * (4 * wid + i) + prow;     // tile row
+    int64_t wr;
+    if constexpr (SWI) {
+      // tile rows [64v, 64v + 32) = gate rows cn*128 + 32v + c, [64v + 32, 64v + 64) = up
+      const int v = j >> 6, h = (j >> 5) & 1, c = j & 31;
+      wr = (h ? up_off : 0) + cn * 128 + 32 * v + c;
+    } else {
+      wr = (int64_t)cn * kN8 + j;
+    }
+    bsrc[i] = we + wr * K + 8 * (pch ^ ((j >> 1) & 7));
+  }
+  auto issue = [&](int kt) {
+    bf16_t* st = lds + (kt % kRing8) * kStage8;
+    const int k0 = kt * kK8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(asrc[i] + k0, (lds_void_t*)(st + (2 * wid + i) * 512), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(bsrc[i] + k0,
+                                       (lds_void_t*)(st + kM8 * kK8 + (4 * wid + i) * 512), 16, 0, 0);
+  };
+
+  f32x16 acc[2][2];                 // [weight subtile i][row subtile j]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = K / kK8;
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) issue(kt + 2);            // into the stage kt-1 vacated
+    const bf16_t* a_lds = lds + (kt % kRing8) * kStage8;   // x rows
+    const bf16_t* b_lds = a_lds + kM8 * kK8;               // weight rows
+    s16x8 wf[4][2], xf[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wn * 64 + i * 32 + r;
+        wf[ks][i] = reinterpret_cast<const s16x8*>(b_lds + row * kK8)[swz64(row, 2 * ks + h2)];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wm * 64 + j * 32 + r;
+        xf[ks][j] = reinterpret_cast<const s16x8*>(a_lds + row * kK8)[swz64(row, 2 * ks + h2)];
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wf[ks][i]),
+                                                              as_bf16x8(xf[ks][j]), acc[i][j],
+                                                              0, 0, 0);
+    // fragments two k-slices ahead of their MFMAs (the compiler otherwise issues each
+    // slice's reads right before its MFMAs and waits out the LDS latency 4x per step)
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      if (ks < 2) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    }
+    // stage kt+1 landed (kt+2 may stay in flight); every wave done with stage kt
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // C^T lane layout: weight row (q&3) + 8(q>>2) + 4h2 of subtile i, x row r of subtile j
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t row = (int64_t)rb * kM8 + wm * 64 + j * 32 + r;
+    if constexpr (SWI) {
+      bf16_t* orow = out + row * n_out + cn * 128 + wn * 32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float gf = bf2f(f2bf(acc[0][j][4 * g + u]));   // = the h13 GEMM's bf16
+          const float sg = gf / (1.f + __expf(-gf));
+          o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[1][j][4 * g + u]));
+        }
+        uint2 v;
+        v.x = pack_bf16x2(o[0], o[1]);
+        v.y = pack_bf16x2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(orow + 8 * g + 4 * h2) = v;
+      }
+    } else {
+      bf16_t* orow = out + row * n_out + cn * kN8 + wn * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint2 v;
+          v.x = pack_bf16x2(acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]);
+          v.y = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+          *reinterpret_cast<uint2*>(orow + 32 * i + 8 * g + 4 * h2) = v;
+        }
+    }
+  }
+}
+
+// out = x W_e^T per 128-row expert block (SWI: out = silu(x Wg^T) * (x Wu^T), n_out = F,
+// w = [Wg; Wu] with up rows at up_off).  Shapes: n_out % 256 == 0 (128 with SWI),
+// K % 64 == 0.
+void launch_moe_gemm8(const bf16_t* x, const bf16_t* w, bf16_t* out,
+                      const int32_t* expert_of_block, const int32_t* num_blocks,
+                      const int32_t* expert_offsets, int max_blocks, int n_out, int K, int E,
+                      int64_t w_rows, int up_off, bool swiglu, hipStream_t s) {
+  if (max_blocks == 0) return;
+  const size_t lds = kRing8 * kStage8 * sizeof(bf16_t);
+  if (swiglu)
+    moe_gemm8_kernel<true><<<max_blocks * (n_out / 128), 512, lds, s>>>(
+        x, w, out, expert_of_block, num_blocks, expert_offsets, n_out, K, E, w_rows, up_off);
+  else
+    moe_gemm8_kernel<false><<<max_blocks * (n_out / kN8), 512, lds, s>>>(
+        x, w, out, expert_of_block, num_blocks, expert_offsets, n_out, K, E, w_rows, up_off);
+}
+
 void launch_moe_grouped_gemm(const bf16_t* x, const bf16_t* w, bf16_t* out,
                              const int32_t* expert_of_block, const int32_t* num_blocks,
                              int max_blocks, int N, int K, int E, hipStream_t s) {

@@ -24,6 +24,14 @@ BLOCK_S = 16            # expert segment padding on the small-batch path
 SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
 # K slices of the latency-path w2 (gemm_skinny.hip moe_skinny_kernel SPLIT): 0/1 = off
 W2_SPLITS = int(os.environ.get("RFQ_MOE_W2_SPLITS", "2"))
+# Eager steps above this many tokens run one hipBLASLt GEMM per expert (one host sync
+# per layer for the segment offsets); at or below it, and in every captured step, the
+# hand-written grouped GEMMs.  Measured (profiles/r2_moe_grouped_gemm.md): the fused
+# gemm8 w13+SwiGLU beats hipBLASLt + silu_mul at ~192 rows per expert, ties at ~384 and
+# loses 10-13 % at >= 768, where end-to-end Mixtral serving ran 77.6 docs/s on the
+# per-expert path vs 61.4 with gemm8 for every eager step.  RFQ_MOE_BLT_MIN_TOKENS=0
+# sends all eager steps to hipBLASLt, a huge value none.
+BLT_MIN_TOKENS = int(os.environ.get("RFQ_MOE_BLT_MIN_TOKENS", "1025"))
 
 
 @dataclass
@@ -119,7 +127,7 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
         return out
     logits = x @ router_w.t()
-    if not torch.cuda.is_current_stream_capturing():
+    if T >= BLT_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
         return _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset, E)
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
     nb = cap // BLOCK_M
@@ -131,9 +139,14 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
                   bufs.num_blocks)
     xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
     ops.moe_gather(x, sorted_ids, topk, xs)
-    ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks)
-    ops.silu_mul(h13, act)
-    ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks)
+    if ops.moe_gemm8_ok(w13, True) and ops.moe_gemm8_ok(w2, False):
+        # 8-wave 128x256 grouped GEMMs; w13's epilogue applies SwiGLU (no h13 pass)
+        ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True)
+        ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False)
+    else:
+        ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks)
+        ops.silu_mul(h13, act)
+        ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks)
     ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
     return out
 
@@ -150,8 +163,9 @@ def _localize(ids: torch.Tensor, w: torch.Tensor, e0: int, e_local: int) -> None
 def _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset=0, E_align=None):
     """Large eager steps: expert segments padded to 16 rows, one hipBLASLt GEMM per
     routed expert.  Reading the 9 segment offsets costs one host sync per layer,
-    which only eager (non-graph) steps can afford; it buys ~1.0 PF/s GEMMs instead
-    of the grouped kernel's ~0.65 (tools/bench_moe.py) and 1/8 of its row padding."""
+    which only eager (non-graph) steps can afford; at >= 768 rows per expert it buys
+    ~1.05 PF/s GEMMs vs the grouped gemm8's ~0.85 (tools/bench_moe.py) and 1/8 of
+    its row padding."""
     T = x.shape[0]
     E = E_align or w13.shape[0]
     n = T * topk

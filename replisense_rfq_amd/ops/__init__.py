@@ -15,7 +15,7 @@ from . import reference as ref
 
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
-    "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm",
+    "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm", "moe_gemm8",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
@@ -472,6 +472,18 @@ def moe_gather(x, sorted_ids, topk, out):
 
 def moe_grouped_gemm(x, w, out, expert_of_block, num_blocks):
     _native.ops().moe_grouped_gemm(x, w, out, expert_of_block, num_blocks)
+
+
+def moe_gemm8_ok(w, swiglu: bool) -> bool:
+    """Shapes the 8-wave 128x256 grouped GEMM (moe.hip moe_gemm8_kernel) takes."""
+    return w.shape[2] % 64 == 0 and w.shape[1] % 256 == 0   # swiglu: F % 128
+
+
+def moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu: bool = False):
+    """Grouped GEMM over 128-row expert blocks (moe_align's segments: expert_offsets
+    [E+1] padded row offsets); swiglu: w = [E, 2F, K] gate|up and out = silu(x Wg^T) *
+    (x Wu^T) ([rows, F]), rounded like GEMM -> bf16 -> silu_mul."""
+    _native.ops().moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu)
 
 
 def moe_route(x, router_w, topk, renorm, weights, ids):

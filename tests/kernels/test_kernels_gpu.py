@@ -287,6 +287,38 @@ def test_moe_pipeline(gpu, T):
     _close(out, exp, 3e-2, 2e-2, f"moe T={T}")
 
 
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("N,K", [(512, 512), (768, 384), (1024, 1024)])
+def test_moe_gemm8(gpu, swiglu, N, K):
+    """8-wave grouped GEMM over 128-row expert blocks (padding blocks -1 and blocks
+    past num_blocks untouched) == per-block fp32 GEMM; swiglu == GEMM -> bf16 ->
+    silu_mul (act.hip rounding)."""
+    torch.manual_seed(N + K + swiglu)
+    E, nb = 4, 7
+    x = torch.randn(nb * 128, K, device=gpu, dtype=BF)
+    w = (torch.randn(E, N, K, device=gpu) / math.sqrt(K)).to(BF)
+    # segments as moe_align lays them out: expert-sorted, padded rows at the end
+    eob = torch.tensor([0, 0, 1, 2, 2, 3, -1], dtype=torch.int32, device=gpu)
+    offs = torch.tensor([0, 256, 384, 640, 768], dtype=torch.int32, device=gpu)
+    num = torch.tensor([6], dtype=torch.int32, device=gpu)       # block 6 not computed
+    n_out = N // 2 if swiglu else N
+    out = torch.full((nb * 128, n_out), float("nan"), device=gpu, dtype=BF)
+    ops.moe_gemm8(x, w, out, eob, num, offs, swiglu)
+    for b in range(nb):
+        rows = slice(128 * b, 128 * b + 128)
+        e = int(eob[b])
+        if b >= 6 or e < 0:
+            assert torch.isnan(out[rows].float()).all(), f"block {b} written"
+            continue
+        h = (x[rows].float() @ w[e].float().t())
+        if swiglu:
+            act = torch.empty(128, n_out, dtype=BF)
+            ref.silu_mul(h.to(BF).cpu(), act)
+            _close(out[rows], act.float(), 3e-2, 2e-2, f"gemm8 swiglu block {b}")
+        else:
+            _close(out[rows], h, 2e-2, 1e-2, f"gemm8 block {b}")
+
+
 @pytest.mark.parametrize("M", [1, 5, 16, 17, 40, 64])
 @pytest.mark.parametrize("N,K", [(512, 4096), (256, 14336), (1024, 3584)])
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])
@@ -462,16 +494,20 @@ def test_skinny_gemm_rope_kv(gpu, M, cfg):
 
 
 @pytest.mark.parametrize("T", [3, 40, 100, 200])
-@pytest.mark.parametrize("grouped", [False, True])
-def test_moe_expert_parallel_partial(gpu, T, grouped, monkeypatch):
+@pytest.mark.parametrize("mode", ["eager", "captured", "blt"])
+def test_moe_expert_parallel_partial(gpu, T, mode, monkeypatch):
     """Expert parallelism: a rank holding experts [2, 6) of 8 computes exactly the
     partial sum of its experts (remote pairs -> dummy segment, weight 0) on every
-    path: skinny (T <= 64), per-expert hipBLASLt (eager) and the grouped kernel
-    (the graph-capture path, forced here)."""
+    path: skinny (T <= 64), the grouped gemm8 kernels (eager below
+    BLT_MIN_TOKENS, and the graph-capture path, forced here) and per-expert
+    hipBLASLt (eager above the threshold, forced with BLT_MIN_TOKENS = 0)."""
     from replisense_rfq_amd.models import moe as M
 
-    if grouped:
+    if mode == "captured":
         monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    if mode == "blt":
+        monkeypatch.setattr(M, "BLT_MIN_TOKENS", 0)
+    grouped = mode
     torch.manual_seed(40 + T)
     d, F, E, k, e0, el = 512, 384, 8, 2, 2, 4
     x = (torch.randn(T, d, device=gpu) * 0.5).to(BF)

@@ -1,6 +1,8 @@
 """Grouped-GEMM throughput for the Mixtral MoE at throughput-step token counts:
-the hand-written 128x128 MFMA grouped GEMM vs hipBLASLt called once per expert
-(with the host reading the expert counts)."""
+the hand-written grouped GEMMs (8-wave 128x256 with the fused SwiGLU epilogue, and
+the older 4-wave 128x128) vs hipBLASLt called once per expert (with the host
+reading the expert counts).  TF/s count the routed pairs only (2 * pairs * N * K),
+not the block padding."""
 import json
 import os
 import sys
@@ -49,6 +51,9 @@ def main():
         eob = bufs.expert_of_block[:nb]
         t13 = timeit(lambda: ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks))
         t2 = timeit(lambda: ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks))
+        tsm = timeit(lambda: ops.silu_mul(h13, act))
+        g13 = timeit(lambda: ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True))
+        g2 = timeit(lambda: ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False))
         off = bufs.expert_offsets.cpu().tolist()
         cnt = torch.bincount(ids.flatten().long(), minlength=E).cpu().tolist()
 
@@ -68,7 +73,12 @@ def main():
         b2 = timeit(per_expert2)
         fl13 = 2 * n * 2 * F * d
         fl2 = 2 * n * F * d
-        print(json.dumps({"T": T, "pairs": n, "grouped_w13_us": round(t13, 1),
+        print(json.dumps({"T": T, "pairs": n, "rows_padded": int(bufs.num_blocks.item()) * BLOCK_M,
+                          "gemm8_w13_swiglu_us": round(g13, 1),
+                          "gemm8_w13_TF": round(fl13 / g13 / 1e6, 1),
+                          "gemm8_w2_us": round(g2, 1), "gemm8_w2_TF": round(fl2 / g2 / 1e6, 1),
+                          "silu_mul_us": round(tsm, 1),
+                          "grouped_w13_us": round(t13, 1),
                           "grouped_w13_TF": round(fl13 / t13 / 1e6, 1),
                           "blt_w13_us": round(b13, 1), "blt_w13_TF": round(fl13 / b13 / 1e6, 1),
                           "grouped_w2_us": round(t2, 1), "grouped_w2_TF": round(fl2 / t2 / 1e6, 1),

@@ -2,6 +2,7 @@
 the counters of such a pass.
 
   python tools/prof_one_kernel.py run prefill B S Hq Hkv      # the profiled program
+  python tools/prof_one_kernel.py run moe T                    # Mixtral w13+SwiGLU gemm8
   python tools/prof_one_kernel.py sum <prof dir> <kernel substring>
 """
 import csv
@@ -21,6 +22,27 @@ def run(kind, *a):
     if kind == "prefill":
         B, S, Hq, Hkv = (int(x) for x in a)
         bench_prefill.run(B, S, Hq, Hkv, iters=5)
+    elif kind == "moe":
+        from replisense_rfq_amd import ops
+        from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
+
+        T = int(a[0])
+        d, F, E, k = 4096, 14336, 8, 2
+        dev = torch.device("cuda:0")
+        w13 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02
+        x = torch.randn(T, d, device=dev, dtype=torch.bfloat16)
+        logits = torch.randn(T, E, device=dev, dtype=torch.bfloat16)
+        bufs = MoEBuffers.allocate(T, k, E, d, F, dev)
+        n = T * k
+        cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+        nb = cap // BLOCK_M
+        ops.moe_topk(logits, k, True, bufs.weights[:T], bufs.ids[:T])
+        ops.moe_align(bufs.ids[:T], E, BLOCK_M, bufs.sorted_ids[:cap], bufs.inv_pos[:n],
+                      bufs.expert_of_block[:nb], bufs.expert_offsets, bufs.num_blocks)
+        ops.moe_gather(x, bufs.sorted_ids[:cap], k, bufs.xs[:cap])
+        for _ in range(5):
+            ops.moe_gemm8(bufs.xs[:cap], w13, bufs.act[:cap], bufs.expert_of_block[:nb],
+                          bufs.num_blocks, bufs.expert_offsets, True)
     torch.cuda.synchronize()
 
 
