@@ -70,7 +70,15 @@ def test_oversized_part_is_counted_not_stored():
 def test_api_order_400_before_413(monkeypatch):
     from replisense_rfq_amd.api import main
 
+    from replisense_rfq_amd.service.extract import ExtractService, MockBackend
+    from replisense_rfq_amd.service.parser import FileParser
+
     monkeypatch.setattr(main, "MAX_FILE_SIZE_MB", 1)
+    # the services without running the app's startup (as test_api.py does); neither
+    # is reached before the 400 / 413 checks
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_parser, lambda: FileParser())
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_field_generator,
+                        lambda: ExtractService(MockBackend()))
     client = TestClient(main.app)
     big = b"a" * (1024 * 1024 + 10)
     r = client.post("/upload/", files={"file": ("doc.exe", big, "application/octet-stream")})

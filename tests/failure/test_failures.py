@@ -64,7 +64,8 @@ def test_step_fault_fails_inflight_and_frees_kv():
 
 def test_watchdog_marks_stalled_engine_unhealthy():
     eng = LLMEngine(_cfg(step_timeout_s=0.2))
-    eng.faults = FaultInjector("step_sleep:0:1500")
+    # the next step (start-up prefix warm-up steps already counted)
+    eng.faults = FaultInjector(f"step_sleep:{eng.num_steps}:1500")
     aeng = AsyncEngine(eng)
     s = asyncio.run(asyncio.wait_for(aeng.generate(_prompt(eng, 3)), 120))
     assert s.finish_reason == "stop"
