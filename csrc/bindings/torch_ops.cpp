@@ -37,7 +37,7 @@ void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
-                        float, int, int, hipStream_t);
+                        float, int, int, int32_t*, hipStream_t);
 void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16_t*,
                                const int32_t*, int, const int32_t*, const int32_t*,
                                const int32_t*, int, const int32_t*, const int32_t*, int, int,
@@ -314,7 +314,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
                  const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
-                 int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item) {
+                 int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item,
+                 const std::optional<Tensor>& tickets) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode: tiles_per_item in {1, 2}");
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
@@ -338,6 +339,13 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                     part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
                 "attn_decode: partial buffers too small");
   }
+  int32_t* tk = nullptr;
+  if (tickets.has_value() && num_splits > 1) {
+    // zero-initialised once by the caller; the merging wave resets its entry
+    CHECK_DEV(*tickets); CHECK_I32(*tickets);
+    TORCH_CHECK(tickets->numel() >= work_seq.numel() * Hkv, "attn_decode: ticket buffer too small");
+    tk = tickets->data_ptr<int32_t>();
+  }
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
                           block_tables.data_ptr<int32_t>(), block_tables.stride(0),
                           seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
@@ -345,7 +353,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
-                          (float)scale, num_splits, tiles_per_item, cur_stream());
+                          (float)scale, num_splits, tiles_per_item, tk, cur_stream());
 }
 
 // Shared-prefix (cascade) decode attention, num_splits == 1; see attn_decode.hip.
@@ -696,7 +704,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
-        "int num_splits, int tiles_per_item=1) -> ()");
+        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None) -> ()");
   m.def("attn_decode_shared(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_ct, Tensor(a!) out, Tensor(b!) ws_i32, Tensor(c!) pre_o, Tensor(d!) pre_ml, "

@@ -45,6 +45,12 @@ constexpr int kD = 128;
 constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
 constexpr int kMinPrefixPages = 4;
 
+typedef __attribute__((address_space(1))) unsigned long long gu64;   // global, sc1 access
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ unsigned long long pack_f2(float lo, float hi) {
+  return (unsigned long long)__float_as_uint(lo) | ((unsigned long long)__float_as_uint(hi) << 32);
+}
+
 struct PrefixArgs {
   const int32_t* meta;     // [0] shared prefix length in tokens (P * kPage), [1] row count
   const int32_t* pflag;    // per sequence: 1 = keys [0, P*32) come from the prefix pass
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
-    int num_splits, PrefixArgs px = PrefixArgs{}) {
+    int num_splits, PrefixArgs px = PrefixArgs{}, int32_t* __restrict__ tickets = nullptr) {
   __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
   const int split = blockIdx.x, kvh = blockIdx.y, w = blockIdx.z;
   const int lane = threadIdx.x;
@@ -308,14 +314,99 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
         *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
       }
     } else {
+      // partials write-through (8-byte agent-scope atomic stores = sc1): the in-kernel
+      // merge below reads them without a release / acquire pair
       const int64_t pidx = ((int64_t)qrow[t] * Hq + h[t]) * num_splits + split;
       float* po = part_o + pidx * kD;
 #pragma unroll
-      for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[t][m];
-      if (g == 0) {
-        part_ml[pidx * 2 + 0] = m_run[t];
-        part_ml[pidx * 2 + 1] = l_tot;
+      for (int m = 0; m < 8; ++m) {
+        gu64* d = (gu64*)(po + 16 * m + 4 * g);
+        __hip_atomic_store(d, pack_f2(o[t][m][0], o[t][m][1]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, pack_f2(o[t][m][2], o[t][m][3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (g == 0)
+        __hip_atomic_store((gu64*)(part_ml + pidx * 2), pack_f2(m_run[t], l_tot),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (MODE != 0 || num_splits == 1 || tickets == nullptr) return;
+
+  // Single pass (cdna_hip_programming.md §6 Guideline 16, R1 counter form): the
+  // partials above are sc1 stores, drained by this wave's vmcnt(0) before its relaxed
+  // agent-scope ticket add; the last of the num_splits waves of this (work item, kv
+  // head) reads every partial with sc1 loads (no L1 copy can be stale, so no acquire
+  // fence), merges them and writes the bf16 output -- no second reduce launch -- then
+  // zeroes the ticket for the next launch on the stream.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  gu32* tk = (gu32*)(tickets + (int64_t)w * Hkv + kvh);
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0, 64);
+  if (prev != (unsigned)num_splits - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
+  if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (!act[t] || !cvalid[t]) continue;
+    const int64_t pbase = ((int64_t)qrow[t] * Hq + h[t]) * num_splits;
+    // every split's (max, sum) in flight at once (num_splits <= 16), then the partial
+    // rows 2 splits at a time: the merge is a few memory round trips, not 16 chained
+    float ms[16], ls[16];
+#pragma unroll
+    for (int sp = 0; sp < 16; ++sp) {
+      ms[sp] = -INFINITY;
+      ls[sp] = 0.f;
+      if (sp < num_splits) {
+        const unsigned long long x = __hip_atomic_load((const gu64*)(part_ml + (pbase + sp) * 2),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ms[sp] = __uint_as_float((unsigned)x);
+        ls[sp] = __uint_as_float((unsigned)(x >> 32));
+      }
+    }
+    float gm = -INFINITY;
+#pragma unroll
+    for (int sp = 0; sp < 16; ++sp) gm = fmaxf(gm, ms[sp]);
+    f32x4 num[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) num[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float den = 0.f;
+    if (gm != -INFINITY) {
+#pragma unroll
+      for (int s0 = 0; s0 < 16; s0 += 2) {
+        if (s0 >= num_splits) break;
+        f32x4 pv[2][8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float* po = part_o + (pbase + min(s0 + u, num_splits - 1)) * kD;
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const gu64* d = (const gu64*)(po + 16 * m + 4 * g);
+            const unsigned long long x0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pv[u][m] = (f32x4){__uint_as_float((unsigned)x0), __uint_as_float((unsigned)(x0 >> 32)),
+                               __uint_as_float((unsigned)x1), __uint_as_float((unsigned)(x1 >> 32))};
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int sp = s0 + u;
+          const float wgt = (sp < num_splits && ms[sp] != -INFINITY) ? fast_exp2(ms[sp] - gm) : 0.f;
+          den += wgt * ls[sp];
+#pragma unroll
+          for (int m = 0; m < 8; ++m) num[m] += wgt * pv[u][m];
+        }
+      }
+    }
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      uint2 wv;
+      wv.x = pack_bf16x2(num[m][0] * inv, num[m][1] * inv);
+      wv.y = pack_bf16x2(num[m][2] * inv, num[m][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
     }
   }
 }
@@ -360,21 +451,23 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
                         const int32_t* seq_kv_len, const int32_t* work_seq,
                         const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
                         float* part_o, float* part_ml, int Hq, int Hkv, float scale,
-                        int num_splits, int tiles_per_item, hipStream_t s) {
+                        int num_splits, int tiles_per_item, int32_t* tickets, hipStream_t s) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_splits, Hkv, W);
+  int32_t* tk = num_splits > 1 ? tickets : nullptr;
   if (tiles_per_item == 2)
     attn_decode_kernel<2><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                               bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                               work_seq, work_ct, out, out_stride, part_o, part_ml,
-                                              Hq, Hkv, scale_log2, num_splits);
+                                              Hq, Hkv, scale_log2, num_splits, PrefixArgs{}, tk);
   else
     attn_decode_kernel<1><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                               bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                               work_seq, work_ct, out, out_stride, part_o, part_ml,
-                                              Hq, Hkv, scale_log2, num_splits);
-  if (num_splits > 1)
+                                              Hq, Hkv, scale_log2, num_splits, PrefixArgs{}, tk);
+  // without a ticket buffer the split partials are merged by a second launch
+  if (num_splits > 1 && tk == nullptr)
     attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                         num_splits);
 }

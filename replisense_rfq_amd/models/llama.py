@@ -36,6 +36,13 @@ from .config import ModelConfig
 from .moe import MoEBuffers, moe_mlp
 from .weights import init_weights
 
+# RFQ_SINGLE_PASS_DECODE=1: split-K decode attention merges its partials in-kernel (the
+# last split wave of each work item, Guideline-16 sc1 hand-off) instead of a second
+# reduce launch.  Off by default: measured 19.1 us per layer vs 8.5 + 4.8 us for the
+# two launches at batch 1 (profiles/r2_decode_attention_single_pass.md) -- one wave
+# merging 16 splits x 16 columns is slower than the 32-workgroup reduce kernel.
+SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "0") == "1"
+
 
 @dataclass
 class ForwardMeta:
@@ -91,6 +98,7 @@ class DecoderLM:
         self.kv_k = None
         self.kv_v = None
         self._moe_bufs: dict[int, MoEBuffers] = {}
+        self._tickets: torch.Tensor | None = None     # single-pass split decode attention
         # Megatron sequence parallelism for steps of >= sp_min_tokens tokens (TP > 1):
         # the residual stream lives sharded by token rows; each all-reduce becomes a
         # reduce-scatter (then the residual-add RMSNorm runs on 1/W of the rows) and an
@@ -207,6 +215,17 @@ class DecoderLM:
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
 
+    def _dec_tickets(self, work_items: int):
+        """Zeroed int32 tickets for single-pass split decode attention (the kernel resets
+        each entry it uses, so one persistent buffer serves every layer and graph replay).
+        Sized once, before any capture: split decode only runs below 1024 (work item, kv
+        head) waves (engine/runner.py _decode_splits), extend rows at most 4x that."""
+        if self.device.type != "cuda" or not SINGLE_PASS_DECODE:
+            return None
+        if self._tickets is None:
+            self._tickets = torch.zeros(4096 * self.hkv, dtype=torch.int32, device=self.device)
+        return self._tickets if work_items * self.hkv <= self._tickets.numel() else None
+
     def _attn_scratch(self, m: ForwardMeta, x: torch.Tensor):
         """Split-K partials for decode attention and cascade-attention scratch."""
         D, hq = m.num_decode, self.hq
@@ -244,7 +263,7 @@ class DecoderLM:
                             m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
                             hq, hkv, self.scale,
                             m.decode_splits if dec_parts is not None else 1,
-                            m.decode_tiles)
+                            m.decode_tiles, self._dec_tickets(m.dec_work_seq.numel()))
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,

@@ -371,14 +371,17 @@ def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq, work_ct,
-                out, part_o, part_ml, Hq, Hkv, scale, num_splits=1, tiles_per_item=1):
+                out, part_o, part_ml, Hq, Hkv, scale, num_splits=1, tiles_per_item=1,
+                tickets=None):
     """Paged attention for decode / short-extend rows (see csrc/kernels/attn_decode.hip).
     A work item (work_seq[w], work_ct[w]) covers column tiles
-    [work_ct*tiles_per_item, +tiles_per_item) of its sequence's q_len*G (query, head) pairs."""
+    [work_ct*tiles_per_item, +tiles_per_item) of its sequence's q_len*G (query, head) pairs.
+    With num_splits > 1, ``tickets`` (int32 zeros, >= work items * Hkv, reset by the kernel)
+    makes it single-pass: the last split to finish merges the partials in-kernel."""
     if _gpu(q):
         _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
                                   work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
-                                  num_splits, tiles_per_item)
+                                  num_splits, tiles_per_item, tickets)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
                          out, Hq, Hkv, scale)

@@ -108,11 +108,13 @@ def _block_tables(lens, nblocks, device, seed=0):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
-@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("splits,single", [(1, False), (4, False), (4, True), (16, True)])
 @pytest.mark.parametrize("tiles", [1, 2])
-def test_attn_decode(gpu, Hq, Hkv, splits, tiles):
+def test_attn_decode(gpu, Hq, Hkv, splits, single, tiles):
     """Decode rows (q=1) and short extend rows (q>1, causal inside the extend); a work
-    item covers `tiles` 16-column tiles of a sequence."""
+    item covers `tiles` 16-column tiles of a sequence.  single: split partials merged
+    in-kernel by the last split wave (ticket buffer), three launches in a row so the
+    tickets must have been reset, compared bit-for-bit with the two-launch merge."""
     torch.manual_seed(4)
     G = Hq // Hkv
     cases = [(1, 1), (1, 31), (1, 32), (1, 33), (1, 700), (5, 129), (9, 2049), (3, 3), (1, 64)]
@@ -137,6 +139,16 @@ def test_attn_decode(gpu, Hq, Hkv, splits, tiles):
     scale = 1 / math.sqrt(128)
     ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct), out, po,
                     pm, Hq, Hkv, scale, splits, tiles)
+    if single:
+        tickets = torch.zeros(len(ws) * Hkv, dtype=torch.int32, device=gpu)
+        for it in range(3):
+            out1 = torch.full_like(out, float("nan"))
+            ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct),
+                            out1, po, pm, Hq, Hkv, scale, splits, tiles, tickets)
+            torch.cuda.synchronize()
+            assert int(tickets.abs().sum()) == 0, "tickets not reset"
+            # same partials, same merge order and arithmetic up to f32 rounding of the weights
+            _close(out1, out, 8e-3, 0, f"single-pass it={it}")
     exp = torch.zeros(T, Hq * 128, dtype=BF)
     ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
                      torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
