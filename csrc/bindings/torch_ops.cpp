@@ -24,6 +24,7 @@ void launch_skinny_gemm_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf
                              int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*,
                              int, int, int, hipStream_t);
 void launch_silu_mul(const bf16_t*, int64_t, bf16_t*, int64_t, int, int, hipStream_t);
+void launch_count_nonfinite(const bf16_t*, int64_t, int, int, int32_t*, hipStream_t);
 void launch_skinny_gemm_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
                                int, int, hipStream_t);
 void launch_gemv_splitk_plain(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
@@ -266,6 +267,14 @@ void skinny_gemm_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const
                                (int)cfg, positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
                                slot_mapping.data_ptr<int32_t>(), bpm(k_cache), bpm(v_cache),
                                (int)Hq, (int)Hkv, k_cache.size(2), cur_stream());
+}
+
+// counter[0] += number of Inf / NaN entries of the bf16 matrix x (rows x cols, row stride)
+void count_nonfinite(const Tensor& x, const Tensor& counter) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_ROWMAJOR(x); CHECK_I32(counter);
+  TORCH_CHECK(x.dim() == 2 && x.stride(0) % 8 == 0, "count_nonfinite: 2-D, 16-byte aligned rows");
+  rfq::launch_count_nonfinite(bp(x), x.stride(0), x.size(0), x.size(1),
+                              counter.data_ptr<int32_t>(), cur_stream());
 }
 
 void silu_mul(const Tensor& gate_up, const Tensor& out) {
@@ -721,6 +730,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("moe_align(Tensor topk_ids, int E, int block_m, Tensor(a!) sorted_ids, Tensor(b!) inv_pos, "
         "Tensor(c!) expert_of_block, Tensor(d!) expert_offsets, Tensor(e!) num_blocks) -> ()");
   m.def("moe_gather(Tensor x, Tensor sorted_ids, int topk, Tensor(a!) out) -> ()");
+  m.def("count_nonfinite(Tensor x, Tensor(a!) counter) -> ()");
   m.def("moe_gemm8(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
         "Tensor num_blocks, Tensor expert_offsets, bool swiglu) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
@@ -757,6 +767,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("moe_gather", &moe_gather);
   m.impl("moe_grouped_gemm", &moe_grouped_gemm);
   m.impl("moe_gemm8", &moe_gemm8);
+  m.impl("count_nonfinite", &count_nonfinite);
   m.impl("moe_combine", &moe_combine);
   m.impl("moe_skinny_splitk", &moe_skinny_splitk);
   m.impl("moe_combine_splitk", &moe_combine_splitk);

@@ -80,6 +80,10 @@ class ModelRunner:
         self.decode_tiles = int(getattr(cfg, "decode_tiles", 1))
         self.prefill_qblk = ops.prefill_qblk(model.hq, model.hkv) if self.is_cuda else 32
         self.ring = None
+        # SURVEY.md §5.2 debug check: Inf/NaN logits are counted on device inside the step
+        # (captured into the decode graphs too) and read back with the sampled tokens
+        self.check_finite = bool(getattr(cfg, "check_finite", False))
+        self._nonfinite = torch.zeros(1, dtype=torch.int32, device=self.device)
         if tp.enabled:
             self._setup_control_plane()
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
@@ -253,6 +257,12 @@ class ModelRunner:
             logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
+        if self.check_finite:
+            bad = int(self._nonfinite[0])
+            if bad:
+                self._nonfinite.zero_()
+                raise RuntimeError(f"non-finite logits: {bad} Inf/NaN entries in step "
+                                   f"{self.stats['steps']} (TP rank {self.tp.rank})")
         car = self.tp.car
         if car is not None and car.errors():
             # a peer's flag never arrived inside the kernel's bounded spin: the sums of
@@ -269,6 +279,8 @@ class ModelRunner:
 
     def _sample(self, logits, midx, temps, seeds, out=None):
         S = logits.shape[0]
+        if self.check_finite:
+            ops.count_nonfinite(logits, self._nonfinite)
         if not logits.is_cuda:
             mt = self.mask_table.cpu()
             vals, idx = ops.reference.sample(logits, mt, midx, temps, seeds, self.model.vocab_start)

@@ -15,7 +15,7 @@ from . import reference as ref
 
 __all__ = [
     "rms_norm", "fused_add_rms_norm", "silu_mul", "embed", "rope_kv", "attn_decode",
-    "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm", "moe_gemm8",
+    "attn_prefill", "sample", "moe_topk", "moe_align", "moe_gather", "moe_grouped_gemm", "moe_gemm8", "count_nonfinite",
     "moe_combine", "moe_skinny", "native_available", "linear", "linear_plan",
     "set_linear_plan", "silu_linear", "set_silu_plan", "set_split_plan", "split_chunks",
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
@@ -475,6 +475,15 @@ def moe_gather(x, sorted_ids, topk, out):
 
 def moe_grouped_gemm(x, w, out, expert_of_block, num_blocks):
     _native.ops().moe_grouped_gemm(x, w, out, expert_of_block, num_blocks)
+
+
+def count_nonfinite(x, counter):
+    """counter[0] += number of Inf / NaN entries of the 2-D bf16 ``x`` (no host sync;
+    graph-capturable).  CPU: the same count with torch."""
+    if _gpu(x):
+        _native.ops().count_nonfinite(x, counter)
+    else:
+        counter[0] += int((~torch.isfinite(x.float())).sum())
 
 
 def moe_gemm8_ok(w, swiglu: bool) -> bool:

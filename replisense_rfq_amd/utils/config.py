@@ -52,6 +52,7 @@ class EngineConfig:
     custom_allreduce: bool = True        # TP>1 on GPU: xGMI one-/two-shot kernels (self-tested)
     trace: bool = False                  # per-request JSON spans
     warm_prefix: bool = True             # prefill + pin the shared prompt template at start-up
+    check_finite: bool = False           # debug: count Inf/NaN logits every step, fail the step
     decode_hints: bool = False           # bench-only: SYNTHETIC grammar profile + min_items for
                                          # random-init weights (service/hints.py); off = reference
 
@@ -79,6 +80,7 @@ class EngineConfig:
             moe_parallel=_env("RFQ_MOE_PARALLEL", cls.moe_parallel),
             trace=_env("RFQ_TRACE", cls.trace, bool),
             warm_prefix=_env("RFQ_WARM_PREFIX", cls.warm_prefix, bool),
+            check_finite=_env("RFQ_CHECK_FINITE", cls.check_finite, bool),
             decode_hints=_env("RFQ_DECODE_HINTS", cls.decode_hints, bool),
         )
         gb = os.environ.get("RFQ_GRAPH_BUCKETS")

@@ -62,6 +62,25 @@ def test_step_fault_fails_inflight_and_frees_kv():
     aeng.shutdown()
 
 
+def test_nonfinite_logits_fail_the_step():
+    """RFQ_CHECK_FINITE: a NaN in the lm_head makes the step's logits
+    non-finite; the runner's device-side count fails exactly that step's requests
+    (engine_error), and the engine serves again once the weights are repaired."""
+    eng = LLMEngine(_cfg(check_finite=True))
+    assert eng.runner.check_finite
+    lm = eng.model.w["lm_head"]
+    saved = lm[5].clone()
+    lm[5, 3] = float("nan")
+    aeng = AsyncEngine(eng)
+    s = asyncio.run(asyncio.wait_for(aeng.generate(_prompt(eng, 1), timeout=120), 120))
+    assert s.finish_reason == "engine_error"
+    assert "non-finite logits" in str(aeng.error)
+    lm[5].copy_(saved)
+    s = asyncio.run(asyncio.wait_for(aeng.generate(_prompt(eng, 2)), 120))
+    assert s.finish_reason == "stop"
+    aeng.shutdown()
+
+
 def test_watchdog_marks_stalled_engine_unhealthy():
     eng = LLMEngine(_cfg(step_timeout_s=0.2))
     # the next step (start-up prefix warm-up steps already counted)

@@ -299,6 +299,22 @@ def test_moe_pipeline(gpu, T):
     _close(out, exp, 3e-2, 2e-2, f"moe T={T}")
 
 
+@pytest.mark.parametrize("rows,cols", [(1, 128256), (37, 16032), (5, 1003)])
+def test_count_nonfinite(gpu, rows, cols):
+    """check.hip: Inf / NaN entries counted (tail columns included), finite extremes not;
+    the counter accumulates across launches."""
+    x = (torch.randn(rows, cols, device=gpu) * 1e4).to(BF)
+    x[0, 0] = float("inf")
+    x[rows - 1, cols - 1] = float("nan")
+    x[rows // 2, cols // 2] = float("-inf")
+    x[0, 1] = torch.finfo(torch.bfloat16).max
+    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ops.count_nonfinite(x, cnt)
+    ops.count_nonfinite(x, cnt)
+    exp = int((~torch.isfinite(x.float())).sum())
+    assert exp == 3 and int(cnt[0]) == 2 * exp
+
+
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("N,K", [(512, 512), (768, 384), (1024, 1024)])
 def test_moe_gemm8(gpu, swiglu, N, K):
