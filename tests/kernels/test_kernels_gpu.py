@@ -303,7 +303,11 @@ def test_moe_pipeline(gpu, T):
 def test_count_nonfinite(gpu, rows, cols):
     """check.hip: Inf / NaN entries counted (tail columns included), finite extremes not;
     the counter accumulates across launches."""
-    x = (torch.randn(rows, cols, device=gpu) * 1e4).to(BF)
+    # rows 16-byte aligned (the kernel's vector loads); cols need not be a multiple of 8
+    stride = (cols + 7) // 8 * 8
+    x = (torch.randn(rows, stride, device=gpu) * 1e4).to(BF)
+    x[:, cols:] = float("nan")                    # outside the view: must not be counted
+    x = x[:, :cols]
     x[0, 0] = float("inf")
     x[rows - 1, cols - 1] = float("nan")
     x[rows // 2, cols // 2] = float("-inf")
