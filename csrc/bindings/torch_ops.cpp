@@ -58,7 +58,7 @@ void launch_moe_align(const int32_t*, int, int, int, int32_t*, int32_t*, int32_t
                       int32_t*, int, int, hipStream_t);
 void launch_moe_gather(const bf16_t*, int64_t, const int32_t*, int, int, int, bf16_t*, hipStream_t);
 void launch_moe_gemm8(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, const int32_t*,
-                      const int32_t*, int, int, int, int, int64_t, int, bool, hipStream_t);
+                      const int32_t*, int, int, int, int, int64_t, int, bool, int, hipStream_t);
 void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, const int32_t*,
                              int, int, int, int, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
@@ -650,7 +650,7 @@ void moe_grouped_gemm(const Tensor& x, const Tensor& w, const Tensor& out,
 // (gate | up), out = [rows, F] = silu(x Wg^T) * (x Wu^T); else out = [rows, N] = x W^T.
 void moe_gemm8(const Tensor& x, const Tensor& w, const Tensor& out,
                const Tensor& expert_of_block, const Tensor& num_blocks,
-               const Tensor& expert_offsets, bool swiglu) {
+               const Tensor& expert_offsets, bool swiglu, int64_t tile) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && out.is_contiguous(), "contiguous");
   TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
@@ -663,9 +663,10 @@ void moe_gemm8(const Tensor& x, const Tensor& w, const Tensor& out,
   TORCH_CHECK(x.size(0) % 128 == 0, "moe gemm8: rows must be padded to 128");
   TORCH_CHECK(expert_of_block.numel() >= x.size(0) / 128, "expert_of_block too short");
   TORCH_CHECK(expert_offsets.numel() >= E + 1, "expert_offsets too short");
+  TORCH_CHECK(tile == 128 || tile == 256, "moe gemm8: tile rows 128 or 256");
   rfq::launch_moe_gemm8(bp(x), bp(w), bpm(out), expert_of_block.data_ptr<int32_t>(),
                         num_blocks.data_ptr<int32_t>(), expert_offsets.data_ptr<int32_t>(),
-                        x.size(0) / 128, n_out, K, E, N, n_out, swiglu, cur_stream());
+                        x.size(0) / 128, n_out, K, E, N, n_out, swiglu, (int)tile, cur_stream());
 }
 
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
@@ -732,7 +733,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("moe_gather(Tensor x, Tensor sorted_ids, int topk, Tensor(a!) out) -> ()");
   m.def("count_nonfinite(Tensor x, Tensor(a!) counter) -> ()");
   m.def("moe_gemm8(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
-        "Tensor num_blocks, Tensor expert_offsets, bool swiglu) -> ()");
+        "Tensor num_blocks, Tensor expert_offsets, bool swiglu, int tile=256) -> ()");
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
         "Tensor num_blocks) -> ()");
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");

@@ -676,11 +676,190 @@ __global__ __launch_bounds__(512) void moe_gemm8_kernel(
 // out = x W_e^T per 128-row expert block (SWI: out = silu(x Wg^T) * (x Wu^T), n_out = F,
 // w = [Wg; Wu] with up rows at up_off).  Shapes: n_out % 256 == 0 (128 with SWI),
 // K % 64 == 0.
+// ---------------------------------------------------- grouped GEMM, 256 x 256 tile
+// Same contract as moe_gemm8 on a 256-row x 256-weight-row tile: a third fewer
+// staged bytes per FLOP (the 128 x 256 tile is bound by the per-CU vector-memory
+// path, profiles/r2_moe_grouped_gemm.md).  A tile covers two consecutive 128-row
+// blocks of ONE expert; when an expert has an odd block count its last tile holds
+// one block, and the waves of the empty half skip their DMA pieces and MFMAs (the
+// SIMD then runs one wave instead of two, so the half tile costs about half).
+// 8 waves = 2 (128 rows) x 4 (64 weight rows), 8 accumulators of 32 x 32 per wave,
+// K-step 64, two 64-KB LDS stages by LDS-DMA, one barrier per K-step.
+constexpr int kM16 = 256, kN16 = 256, kK16 = 64;
+constexpr int kStage16 = (kM16 + kN16) * kK16;     // bf16 elements per stage
+
+template <bool SWI>
+__global__ __launch_bounds__(512) void moe_gemm16_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ out,
+    const int32_t* __restrict__ num_blocks, const int32_t* __restrict__ expert_offsets,
+    int n_out, int K, int E, int64_t w_rows, int up_off) {
+  extern __shared__ __attribute__((aligned(16))) char smem16[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem16);
+  const int ntn = SWI ? n_out / 128 : n_out / kN16;
+  // live tiles: sum over experts of ceil(blocks / 2) per weight tile
+  int nchunks = 0;
+  for (int e = 0; e < E; ++e) {
+    const int nb = expert_offsets[e + 1] / kM8 - expert_offsets[e] / kM8;
+    nchunks += (nb + 1) >> 1;
+  }
+  const int nlive = nchunks * ntn;
+  const int bid = blockIdx.x;
+  if (bid >= nlive || *num_blocks == 0) return;
+  const int q8 = nlive >> 3, r8 = nlive & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // expert-major, then weight tile, then 256-row chunk (T1 remap above keeps the
+  // chunks that share a weight tile back to back on one XCD)
+  int e = 0, p0 = 0, s0 = 0, nbe = 0, che = 0;
+  for (; e < E; ++e) {
+    s0 = expert_offsets[e] / kM8;
+    nbe = expert_offsets[e + 1] / kM8 - s0;
+    che = (nbe + 1) >> 1;
+    if (wg < (p0 + che) * ntn) break;
+    p0 += che;
+  }
+  if (e >= E) return;
+  const int local = wg - p0 * ntn;
+  const int cn = local / che, chunk = local % che;
+  const int rb = s0 + 2 * chunk;                   // first 128-row block of the tile
+  const bool two = 2 * chunk + 1 < nbe;            // second block present
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h2 = lane >> 5;
+  const int wm = wid >> 2, wn = wid & 3;           // waves 4-7 own rows 128-255
+  const bool active = two || wm == 0;              // wave-uniform
+  const bf16_t* xa = x + (int64_t)rb * kM8 * K;
+  const bf16_t* we = w + (int64_t)e * w_rows * K;
+
+  // DMA: 32 A pieces (8 rows each) + 32 B pieces per stage; wave w issues A pieces
+  // 4w..4w+3 (rows 32w.. -> waves 4-7 fill the second block) and B pieces 4w..4w+3
+  const int prow = lane >> 3, pch = lane & 7;
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wid + i) + prow;
+    asrc[i] = xa + (int64_t)row * K + 8 * (pch ^ ((row >> 1) & 7));
+    const int j = row;                             // weight tile row
+    int64_t wr;
+    if constexpr (SWI) {
+      const int v = j >> 6, h = (j >> 5) & 1, c = j & 31;
+      wr = (h ? up_off : 0) + cn * 128 + 32 * v + c;
+    } else {
+      wr = (int64_t)cn * kN16 + j;
+    }
+    bsrc[i] = we + wr * K + 8 * (pch ^ ((j >> 1) & 7));
+  }
+  auto issue = [&](int kt) {
+    bf16_t* st = lds + (kt & 1) * kStage16;
+    const int k0 = kt * kK16;
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(asrc[i] + k0, (lds_void_t*)(st + (4 * wid + i) * 512), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(bsrc[i] + k0,
+                                       (lds_void_t*)(st + kM16 * kK16 + (4 * wid + i) * 512), 16, 0, 0);
+  };
+
+  f32x16 acc[2][4];                 // [weight subtile i][row subtile j]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = K / kK16;
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue(kt + 1);                // into the stage kt-1 vacated
+    if (active) {
+      const bf16_t* a_lds = lds + (kt & 1) * kStage16;    // x rows
+      const bf16_t* b_lds = a_lds + kM16 * kK16;           // weight rows
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s16x8 wf[2], xf[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wn * 64 + i * 32 + r;
+          wf[i] = reinterpret_cast<const s16x8*>(b_lds + row * kK16)[swz64(row, 2 * ks + h2)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wm * 128 + j * 32 + r;
+          xf[j] = reinterpret_cast<const s16x8*>(a_lds + row * kK16)[swz64(row, 2 * ks + h2)];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wf[i]), as_bf16x8(xf[j]),
+                                                                acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // stage kt+1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every wave done with stage kt
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (!active) return;
+
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t row = (int64_t)rb * kM8 + wm * 128 + j * 32 + r;
+    if constexpr (SWI) {
+      bf16_t* orow = out + row * n_out + cn * 128 + wn * 32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float gf = bf2f(f2bf(acc[0][j][4 * g + u]));   // = the h13 GEMM's bf16
+          const float sg = gf / (1.f + __expf(-gf));
+          o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[1][j][4 * g + u]));
+        }
+        uint2 v;
+        v.x = pack_bf16x2(o[0], o[1]);
+        v.y = pack_bf16x2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(orow + 8 * g + 4 * h2) = v;
+      }
+    } else {
+      bf16_t* orow = out + row * n_out + cn * kN16 + wn * 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint2 v;
+          v.x = pack_bf16x2(acc[i][j][4 * g + 0], acc[i][j][4 * g + 1]);
+          v.y = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+          *reinterpret_cast<uint2*>(orow + 32 * i + 8 * g + 4 * h2) = v;
+        }
+    }
+  }
+}
+
 void launch_moe_gemm8(const bf16_t* x, const bf16_t* w, bf16_t* out,
                       const int32_t* expert_of_block, const int32_t* num_blocks,
                       const int32_t* expert_offsets, int max_blocks, int n_out, int K, int E,
-                      int64_t w_rows, int up_off, bool swiglu, hipStream_t s) {
+                      int64_t w_rows, int up_off, bool swiglu, int tile, hipStream_t s) {
   if (max_blocks == 0) return;
+  if (tile == 256) {
+    // live 256-row tiles <= (blocks + experts) / 2 per weight tile
+    const int chunks = (max_blocks + E) / 2 + 1;
+    const size_t lds16 = 2 * kStage16 * sizeof(bf16_t);
+    if (swiglu)
+      moe_gemm16_kernel<true><<<chunks * (n_out / 128), 512, lds16, s>>>(
+          x, w, out, num_blocks, expert_offsets, n_out, K, E, w_rows, up_off);
+    else
+      moe_gemm16_kernel<false><<<chunks * (n_out / kN16), 512, lds16, s>>>(
+          x, w, out, num_blocks, expert_offsets, n_out, K, E, w_rows, up_off);
+    return;
+  }
   const size_t lds = kRing8 * kStage8 * sizeof(bf16_t);
   if (swiglu)
     moe_gemm8_kernel<true><<<max_blocks * (n_out / 128), 512, lds, s>>>(

@@ -24,14 +24,15 @@ BLOCK_S = 16            # expert segment padding on the small-batch path
 SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
 # K slices of the latency-path w2 (gemm_skinny.hip moe_skinny_kernel SPLIT): 0/1 = off
 W2_SPLITS = int(os.environ.get("RFQ_MOE_W2_SPLITS", "2"))
-# Eager steps above this many tokens run one hipBLASLt GEMM per expert (one host sync
-# per layer for the segment offsets); at or below it, and in every captured step, the
-# hand-written grouped GEMMs.  Measured (profiles/r2_moe_grouped_gemm.md): the fused
-# gemm8 w13+SwiGLU beats hipBLASLt + silu_mul at ~192 rows per expert, ties at ~384 and
-# loses 10-13 % at >= 768, where end-to-end Mixtral serving ran 77.6 docs/s on the
-# per-expert path vs 61.4 with gemm8 for every eager step.  RFQ_MOE_BLT_MIN_TOKENS=0
-# sends all eager steps to hipBLASLt, a huge value none.
-BLT_MIN_TOKENS = int(os.environ.get("RFQ_MOE_BLT_MIN_TOKENS", "1025"))
+# Eager steps of at least this many tokens run one hipBLASLt GEMM per expert (one host
+# sync per layer for the segment offsets) instead of the hand-written grouped GEMMs.
+# Measured (profiles/r2_moe_grouped_gemm.md): the grouped w13+SwiGLU (256x256) + w2
+# pair beats hipBLASLt w13 + silu_mul + w2 from 192 to 1536 rows per expert (top-2 of
+# 8: T = 768-6144 tokens); the large prefill-chunk steps (up to 16K tokens, 4K rows
+# per expert) stay on hipBLASLt.  End to end (bench.py --model mixtral): threshold
+# 4096: 77.9 docs/s, 8192: 77.0, 1025: 75.7-77.6, grouped everywhere: 68.3.
+# RFQ_MOE_BLT_MIN_TOKENS=0 sends all eager steps to hipBLASLt.
+BLT_MIN_TOKENS = int(os.environ.get("RFQ_MOE_BLT_MIN_TOKENS", "4096"))
 
 
 @dataclass
@@ -140,9 +141,12 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
     xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
     ops.moe_gather(x, sorted_ids, topk, xs)
     if ops.moe_gemm8_ok(w13, True) and ops.moe_gemm8_ok(w2, False):
-        # 8-wave 128x256 grouped GEMMs; w13's epilogue applies SwiGLU (no h13 pass)
-        ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True)
-        ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False)
+        # grouped MFMA GEMMs; w13's epilogue applies SwiGLU (no h13 pass).  w13 always
+        # on the 256x256 tile; w2 (N = d, 16x fewer weight tiles) on 128x256 below
+        # ~320 rows per expert, where the 256-row tile leaves CUs idle
+        w2_tile = 256 if n >= 320 * w13.shape[0] else 128
+        ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True, 256)
+        ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False, w2_tile)
     else:
         ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks)
         ops.silu_mul(h13, act)

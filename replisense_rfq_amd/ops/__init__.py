@@ -491,11 +491,17 @@ def moe_gemm8_ok(w, swiglu: bool) -> bool:
     return w.shape[2] % 64 == 0 and w.shape[1] % 256 == 0   # swiglu: F % 128
 
 
-def moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu: bool = False):
+MOE_TILE_ROWS = int(os.environ.get("RFQ_MOE_TILE", "256"))
+
+
+def moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu: bool = False,
+              tile: int | None = None):
     """Grouped GEMM over 128-row expert blocks (moe_align's segments: expert_offsets
     [E+1] padded row offsets); swiglu: w = [E, 2F, K] gate|up and out = silu(x Wg^T) *
-    (x Wu^T) ([rows, F]), rounded like GEMM -> bf16 -> silu_mul."""
-    _native.ops().moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu)
+    (x Wu^T) ([rows, F]), rounded like GEMM -> bf16 -> silu_mul.  tile: 256 = the
+    256x256 kernel (pairs of an expert's blocks, half tiles skipped), 128 = 128x256."""
+    _native.ops().moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu,
+                            tile or MOE_TILE_ROWS)
 
 
 def moe_route(x, router_w, topk, renorm, weights, ids):

@@ -319,27 +319,29 @@ def test_count_nonfinite(gpu, rows, cols):
     assert exp == 3 and int(cnt[0]) == 2 * exp
 
 
+@pytest.mark.parametrize("tile", [128, 256])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("N,K", [(512, 512), (768, 384), (1024, 1024)])
-def test_moe_gemm8(gpu, swiglu, N, K):
+def test_moe_gemm8(gpu, swiglu, N, K, tile):
     """8-wave grouped GEMM over 128-row expert blocks (padding blocks -1 and blocks
     past num_blocks untouched) == per-block fp32 GEMM; swiglu == GEMM -> bf16 ->
     silu_mul (act.hip rounding)."""
     torch.manual_seed(N + K + swiglu)
-    E, nb = 4, 7
+    # segments as moe_align lays them out: expert-sorted, padded rows at the end; expert 1
+    # has one block, expert 3 three (a full and a half 256-row tile)
+    E, nb = 4, 9
     x = torch.randn(nb * 128, K, device=gpu, dtype=BF)
     w = (torch.randn(E, N, K, device=gpu) / math.sqrt(K)).to(BF)
-    # segments as moe_align lays them out: expert-sorted, padded rows at the end
-    eob = torch.tensor([0, 0, 1, 2, 2, 3, -1], dtype=torch.int32, device=gpu)
-    offs = torch.tensor([0, 256, 384, 640, 768], dtype=torch.int32, device=gpu)
-    num = torch.tensor([6], dtype=torch.int32, device=gpu)       # block 6 not computed
+    eob = torch.tensor([0, 0, 1, 2, 2, 3, 3, 3, -1], dtype=torch.int32, device=gpu)
+    offs = torch.tensor([0, 256, 384, 640, 1024], dtype=torch.int32, device=gpu)
+    num = torch.tensor([8], dtype=torch.int32, device=gpu)       # block 8 not computed
     n_out = N // 2 if swiglu else N
     out = torch.full((nb * 128, n_out), float("nan"), device=gpu, dtype=BF)
-    ops.moe_gemm8(x, w, out, eob, num, offs, swiglu)
+    ops.moe_gemm8(x, w, out, eob, num, offs, swiglu, tile)
     for b in range(nb):
         rows = slice(128 * b, 128 * b + 128)
         e = int(eob[b])
-        if b >= 6 or e < 0:
+        if b >= 8 or e < 0:
             assert torch.isnan(out[rows].float()).all(), f"block {b} written"
             continue
         h = (x[rows].float() @ w[e].float().t())

@@ -52,8 +52,14 @@ def main():
         t13 = timeit(lambda: ops.moe_grouped_gemm(xs, w13, h13, eob, bufs.num_blocks))
         t2 = timeit(lambda: ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks))
         tsm = timeit(lambda: ops.silu_mul(h13, act))
-        g13 = timeit(lambda: ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True))
-        g2 = timeit(lambda: ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False))
+        g13 = timeit(lambda: ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets,
+                                           True, 128))
+        g2 = timeit(lambda: ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets,
+                                          False, 128))
+        q13 = timeit(lambda: ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets,
+                                           True, 256))
+        q2 = timeit(lambda: ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets,
+                                          False, 256))
         off = bufs.expert_offsets.cpu().tolist()
         cnt = torch.bincount(ids.flatten().long(), minlength=E).cpu().tolist()
 
@@ -77,6 +83,9 @@ def main():
                           "gemm8_w13_swiglu_us": round(g13, 1),
                           "gemm8_w13_TF": round(fl13 / g13 / 1e6, 1),
                           "gemm8_w2_us": round(g2, 1), "gemm8_w2_TF": round(fl2 / g2 / 1e6, 1),
+                          "gemm256_w13_swiglu_us": round(q13, 1),
+                          "gemm256_w13_TF": round(fl13 / q13 / 1e6, 1),
+                          "gemm256_w2_us": round(q2, 1), "gemm256_w2_TF": round(fl2 / q2 / 1e6, 1),
                           "silu_mul_us": round(tsm, 1),
                           "grouped_w13_us": round(t13, 1),
                           "grouped_w13_TF": round(fl13 / t13 / 1e6, 1),
