@@ -111,9 +111,22 @@ def build_kernels(jobs: int | None = None, verbose: bool = False) -> Path:
             f"-Wl,-rpath,{tdir / 'lib'}", f"-L{ROCM / 'lib'}", "-lhipblaslt",
             f"-Wl,-rpath,{ROCM / 'lib'}"]
     _link(C_SO, objs, libs, "C" + ARCH)
+    _check_stubs(C_SO)
     if verbose:
         print(f"[rfq build] {C_SO}")
     return C_SO
+
+
+def _check_stubs(so: Path) -> None:
+    """Fail the build when a kernel's host launch stub is undefined: clang can drop a
+    kernel template's stub without an error (e.g. a device-only builtin called with
+    template-dependent arguments), and the library then fails to load only on the
+    GPU box (`torch.ops.load_library`: undefined symbol)."""
+    nm = shutil.which("nm") or str(ROCM / "lib" / "llvm" / "bin" / "llvm-nm")
+    out = _run([nm, "-D", "--undefined-only", str(so)], "nm")
+    missing = [ln.split()[-1] for ln in out.splitlines() if "__device_stub__" in ln]
+    if missing:
+        raise RuntimeError(f"[rfq build] {so.name}: undefined kernel launch stubs {missing}")
 
 
 def build_runtime(verbose: bool = False) -> Path:

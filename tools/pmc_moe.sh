@@ -3,6 +3,7 @@
 set -u
 OUT=${1:-gpurun_out/pmc_moe}; shift || true
 T=${PMC_T:-3072}
+TILE=${PMC_TILE:-256}
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p "$OUT"
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES"
@@ -12,7 +13,7 @@ rc=0
 for i in 1 2 3; do
   eval C=\$P$i
   timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 tools/prof_one_kernel.py run moe $T > "$OUT/p$i.log" 2>&1 || { rc=$?; echo "pass $i rc=$rc"; tail -3 "$OUT/p$i.log"; continue; }
-  python3 tools/prof_one_kernel.py sum "$OUT/p$i" moe_gemm8
+    python3 tools/prof_one_kernel.py run moe $T $TILE > "$OUT/p$i.log" 2>&1 || { rc=$?; echo "pass $i rc=$rc"; tail -3 "$OUT/p$i.log"; continue; }
+  python3 tools/prof_one_kernel.py sum "$OUT/p$i" moe_gemm
 done
 exit $rc

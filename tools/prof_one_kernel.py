@@ -2,7 +2,7 @@
 the counters of such a pass.
 
   python tools/prof_one_kernel.py run prefill B S Hq Hkv      # the profiled program
-  python tools/prof_one_kernel.py run moe T                    # Mixtral w13+SwiGLU gemm8
+  python tools/prof_one_kernel.py run moe T [tile]             # Mixtral w13+SwiGLU grouped GEMM
   python tools/prof_one_kernel.py sum <prof dir> <kernel substring>
 """
 import csv
@@ -27,6 +27,7 @@ def run(kind, *a):
         from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
 
         T = int(a[0])
+        tile = int(a[1]) if len(a) > 1 else 256
         d, F, E, k = 4096, 14336, 8, 2
         dev = torch.device("cuda:0")
         w13 = torch.randn(E, 2 * F, d, device=dev, dtype=torch.bfloat16) * 0.02
@@ -42,7 +43,7 @@ def run(kind, *a):
         ops.moe_gather(x, bufs.sorted_ids[:cap], k, bufs.xs[:cap])
         for _ in range(5):
             ops.moe_gemm8(bufs.xs[:cap], w13, bufs.act[:cap], bufs.expert_of_block[:nb],
-                          bufs.num_blocks, bufs.expert_offsets, True)
+                          bufs.num_blocks, bufs.expert_offsets, True, tile)
     torch.cuda.synchronize()
 
 
