@@ -1,6 +1,6 @@
 """Does a weight prefetch into the MALL (Infinity Cache, 256 MB) speed up a latency-path
 GEMV that follows it?  For each projection shape: the skinny GEMV at M = 1 on weights
-evicted from L2/MALL (1 GiB of other traffic first) vs the same GEMV right after a
+evicted from L2/MALL (1 GiB of other reads first) vs the same GEMV right after a
 strided read of its weights (one element per 64-B line).  Times the GEMV alone (events).
 A large gap would make overlapping next-kernel weight prefetch with the
 latency-bound attention / norm kernels of a decode step worth building."""
@@ -31,9 +31,9 @@ def main():
         for mode in ("cold", "prefetched", "cold", "prefetched"):
             tot = 0.0
             for _ in range(10):
-                flush.add_(1)                                   # evict: 1 GiB read + write
+                sink += flush.sum(dtype=torch.float32)          # evict: 1 GiB read only
                 if mode == "prefetched":
-                    torch.sum(w.view(-1)[::32].float(), out=sink[0])
+                    sink += w.view(-1)[::32].sum(dtype=torch.float32)
                 torch.cuda.synchronize()
                 e0.record()
                 OPS.skinny_gemm(x, w, y, cfg)
