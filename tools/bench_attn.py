@@ -63,6 +63,15 @@ def run(B, C, P, shared, Hq=32, Hkv=8, q=1, tiles=2, splits=2, iters=20):
 
 
 def main():
+    if os.environ.get("TILES_AB"):
+        # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
+        for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (3072, 800, 416, 1)]:
+            for tiles in (1, 2):
+                for splits in (1, 2):
+                    us, _ = run(B, C, P, True, q=q, tiles=tiles, splits=splits)
+                    print(json.dumps({"B": B, "ctx": C, "q": q, "tiles": tiles, "splits": splits,
+                                      "us": round(us, 1)}), flush=True)
+        return
     for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (1024, 1000, 416, 1)]:
         a = run(B, C, P, True, q=q)
         b = run(B, C, P, False, q=q)
