@@ -340,7 +340,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   TORCH_CHECK(block_tables.size(0) >= seq_q_len.numel() && seq_kv_len.numel() >= seq_q_len.numel()
                   && seq_q_start.numel() >= seq_q_len.numel(),
               "attn_decode: per-sequence arrays mismatch");
-  TORCH_CHECK(num_splits >= 1 && num_splits <= 16, "attn_decode: num_splits in [1, 16]");
+  TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "attn_decode: num_splits in [1, 32]");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
@@ -353,6 +353,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     // zero-initialised once by the caller; the merging wave resets its entry
     CHECK_DEV(*tickets); CHECK_I32(*tickets);
     TORCH_CHECK(tickets->numel() >= work_seq.numel() * Hkv, "attn_decode: ticket buffer too small");
+    TORCH_CHECK(num_splits <= 16, "attn_decode: the in-kernel merge takes at most 16 splits");
     tk = tickets->data_ptr<int32_t>();
   }
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),

@@ -178,9 +178,15 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
       }
     }
     const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
+    // the split's block-table entries, 64 pages per lane-parallel load (issued beside
+    // the Q loads): each page then costs one memory round trip (K / V), not two
+    const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
+    int pg_l = 0;
 
     for (int kt = start; kt < end; kt += kPage) {
-      const int64_t page = bt[kt / kPage];
+      const int j = kt / kPage - pg0;
+      if ((j & 63) == 0) pg_l = bt[min(pg0 + j + lane, pg_last)];
+      const int64_t page = __shfl(pg_l, j & 63, 64);
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
       const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
@@ -418,13 +424,13 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
   const int bh = blockIdx.x;
   const int b = bh / Hq, h = bh % Hq;
   const int d = threadIdx.x;
-  __shared__ float ml_s[2 * 16];
+  __shared__ float ml_s[2 * 32];
   const float* ml = part_ml + (int64_t)bh * num_splits * 2;
-  if (d < 2 * num_splits) ml_s[d] = ml[d];     // num_splits <= 16: one load per lane
+  if (d < 2 * num_splits) ml_s[d] = ml[d];     // num_splits <= 32: one load per lane
   // issue every split's partial load before the LDS round trip
-  float po[16];
+  float po[32];
 #pragma unroll
-  for (int s = 0; s < 16; ++s)
+  for (int s = 0; s < 32; ++s)
     po[s] = s < num_splits ? part_o[((int64_t)bh * num_splits + s) * kD + d] : 0.f;
   __syncthreads();
   float gm = -INFINITY;
@@ -432,7 +438,7 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
   float num = 0.f, den = 0.f;
   if (gm != -INFINITY) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < 32; ++s) {
       if (s >= num_splits) break;
       const float ms = ml_s[2 * s];
       if (ms == -INFINITY) continue;

@@ -62,7 +62,64 @@ def run(B, C, P, shared, Hq=32, Hkv=8, q=1, tiles=2, splits=2, iters=20):
     return us, kv_bytes / us / 1e6
 
 
+def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20):
+    """Batch-1 decode attention as the latency path runs it: L layers with their own
+    KV caches, the L (split kernel [+ reduce]) launches captured in one hipGraph;
+    returns µs per layer."""
+    dev = torch.device("cuda")
+    pages = (C + 31) // 32
+    ks = [torch.randn(pages + 1, Hkv, 32, 128, device=dev, dtype=torch.bfloat16) for _ in range(L)]
+    vs = [torch.randn_like(k) for k in ks]
+    bt = torch.arange(pages, dtype=torch.int32, device=dev).view(1, pages)
+    G = Hq // Hkv
+    qs = torch.zeros(1, dtype=torch.int32, device=dev)
+    ql = torch.ones(1, dtype=torch.int32, device=dev)
+    kvl = torch.full((1,), C, dtype=torch.int32, device=dev)
+    items = ((G + 15) // 16 + tiles - 1) // tiles
+    ws = torch.zeros(items, dtype=torch.int32, device=dev)
+    wct = torch.arange(items, dtype=torch.int32, device=dev)
+    qt = torch.randn(1, Hq * 128, device=dev, dtype=torch.bfloat16)
+    out = torch.empty_like(qt)
+    po = torch.empty(Hq * splits * 128, device=dev)
+    pm = torch.empty(Hq * splits * 2, device=dev)
+
+    def body():
+        for k, v in zip(ks, vs):
+            ops.attn_decode(qt, k, v, bt, qs, ql, kvl, ws, wct, out, po, pm, Hq, Hkv,
+                            1 / math.sqrt(128), splits, tiles)
+
+    body()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(3):
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / (reps * L))
+    return best
+
+
 def main():
+    if os.environ.get("LAT"):
+        # batch-1 latency path: split count vs context (8B 32/8 heads, 70B 64/8)
+        for Hq in (32, 64):
+            for C in (256, 512, 1024, 2048):
+                row = {"Hq": Hq, "Hkv": 8, "ctx": C}
+                for sp in (8, 16, 32):
+                    row[f"s{sp}_us"] = round(run_latency(C, Hq, 8, sp), 2)
+                print(json.dumps(row), flush=True)
+        return
     if os.environ.get("TILES_AB"):
         # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
         for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (3072, 800, 416, 1)]:
