@@ -125,7 +125,10 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0) -> TP
         return TPContext()
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # RFQ_DIST_BACKEND=gloo: a rehearsal of N ranks sharing one GPU (RCCL
+            # refuses two ranks on one device); production multi-GPU runs use RCCL
+            backend = os.environ.get("RFQ_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             local = int(os.environ.get("LOCAL_RANK", rank))
