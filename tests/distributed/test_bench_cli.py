@@ -78,7 +78,9 @@ def test_bench_driver_flags_time_budget():
                 "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
                 "--latency-runs", "2"], timeout=300)
     wall = time.perf_counter() - t0
-    assert wall < 240, wall
+    # ~80 s alone; the bound only has to catch an unbounded step (the driver's case),
+    # with room for a loaded CI host running tests in parallel
+    assert wall < 295, wall
     assert out["steps"] == 20 and out["warmup"] == 5
     assert out["ms_per_step"] * 20 / 1e3 < wall
     assert out["engine"]["docs_completed_in_window_rank0"] >= 40
