@@ -178,33 +178,35 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
       }
     }
     const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
-    // the split's block-table entries, 64 pages per lane-parallel load (issued beside
-    // the Q loads): each page then costs one memory round trip (K / V), not two
     const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
-    int pg_l = 0;
-
-    for (int kt = start; kt < end; kt += kPage) {
-      const int j = kt / kPage - pg0;
-      if ((j & 63) == 0) pg_l = bt[min(pg0 + j + lane, pg_last)];
-      const int64_t page = __shfl(pg_l, j & 63, 64);
+    const int np = pg_last - pg0 + 1;
+    // block-table entries by wave-uniform (scalar, lgkmcnt-counted) loads, one page
+    // ahead: a vector load here would make every page's K / V issue wait on vmcnt(0),
+    // i.e. drain the page loads already in flight
+    int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
+    // issue page j's K fragments (A operand: row = key, k = dh) and V rows (g + 4i,
+    // chunk c) into registers; must be called with j = 0, 1, 2, ...
+    auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
+      const int64_t page = pg_next;
+      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
-      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
-
-      // ---- issue K fragment loads (A operand: row = key, k = dh) ----
-      s16x8 kf[2][4];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
           kf[mt][ks] = reinterpret_cast<const s16x8*>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g)[0];
-
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vr[i] = reinterpret_cast<const s16x8*>(vb + (g + 4 * i) * kD)[c];
+    };
+    auto process = [&](int j, const s16x8 (&kf)[2][4], const s16x8 (&vr)[8]) {
+      const int kt = start + j * kPage;
+      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
       // ---- V tile -> LDS (swizzled), rows past the split/context zeroed ----
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = g + 4 * i, ch = c;
-        s16x8 v = reinterpret_cast<const s16x8*>(vb + row * kD)[ch];
-        if (row >= nvalid) v = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        const s16x8 v = row >= nvalid ? (s16x8){0, 0, 0, 0, 0, 0, 0, 0} : vr[i];
         const int pch = ch ^ ((row & 7) << 1);
         reinterpret_cast<s16x8*>(v_lds + row * kD)[pch] = v;
       }
@@ -243,9 +245,9 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
         float psum = 0.f;
         float p[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          p[j] = fast_exp2(s[j >> 2][j & 3] - m_use);
-          psum += p[j];
+        for (int jj = 0; jj < 8; ++jj) {
+          p[jj] = fast_exp2(s[jj >> 2][jj & 3] - m_use);
+          psum += p[jj];
         }
         l_run[t] = l_run[t] * alpha + psum;
         m_run[t] = m_new;
@@ -273,6 +275,34 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
                                                               o[t][m], 0, 0, 0);
       }
       __syncthreads();  // before the next tile overwrites v_lds
+    };
+
+    s16x8 kA[2][4], vA[8];
+    if constexpr (NT == 1) {
+      // NT 1 has the registers for a second page in flight: page j+1's K / V loads
+      // are issued before page j is processed (two register sets, unrolled by two), so
+      // a split walking several pages pays one memory round trip, not one per page
+      // The counted wait (a real S_WAITCNT, which the compiler's wait pass accounts
+      // for) retires page j -- in flight during page j-1 -- BEFORE page j+1 is issued.
+      // Without it the wait pass, merging its scoreboard over the loop back edge, treats
+      // page j's loads as the newest and waits on page j+1's too (vmcnt 15..0).
+      constexpr int kVmcnt0 = 0x0F70;          // vmcnt(0), expcnt / lgkmcnt untouched
+      s16x8 kB[2][4], vB[8];
+      fetch(0, kA, vA);
+      for (int j = 0; j < np; j += 2) {
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        if (j + 1 < np) fetch(j + 1, kB, vB);
+        process(j, kA, vA);
+        if (j + 1 >= np) break;
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        if (j + 2 < np) fetch(j + 2, kA, vA);
+        process(j + 1, kB, vB);
+      }
+    } else {
+      for (int j = 0; j < np; ++j) {
+        fetch(j, kA, vA);
+        process(j, kA, vA);
+      }
     }
   }
 

@@ -76,11 +76,12 @@ def test_bench_driver_flags_time_budget():
     t0 = time.perf_counter()
     out = _run([sys.executable, "bench.py", "--gpus", "1", "--steps", "20", "--warmup", "5",
                 "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
-                "--latency-runs", "2"], timeout=300)
+                "--latency-runs", "2"], timeout=600)
     wall = time.perf_counter() - t0
-    # ~80 s alone; the bound only has to catch an unbounded step (the driver's case),
-    # with room for a loaded CI host running tests in parallel
-    assert wall < 295, wall
+    # ~80 s alone; the bound only has to catch an unbounded step (the round-1 failure
+    # mode: 25 steps of 3,072 documents), with room for a CI host running the suite
+    # under pytest-xdist
+    assert wall < 590, wall
     assert out["steps"] == 20 and out["warmup"] == 5
     assert out["ms_per_step"] * 20 / 1e3 < wall
     assert out["engine"]["docs_completed_in_window_rank0"] >= 40

@@ -118,6 +118,8 @@ def main():
                 row = {"Hq": Hq, "Hkv": 8, "ctx": C}
                 for sp in (8, 16, 32):
                     row[f"s{sp}_us"] = round(run_latency(C, Hq, 8, sp), 2)
+                for sp in (8, 16):                 # one column tile per work item
+                    row[f"s{sp}_t1_us"] = round(run_latency(C, Hq, 8, sp, tiles=1), 2)
                 print(json.dumps(row), flush=True)
         return
     if os.environ.get("TILES_AB"):
