@@ -147,26 +147,33 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
       kp[ks] = sl + krow + (x ^ (32 * ks));
       asm volatile("" : "+v"(kp[ks]));
     }
+    // K fragments by inline-asm ds_read_b128 with counted waits tied to each fragment:
+    // every MFMA waits only for its own read (LDS returns in order), not lgkmcnt(0)
+    // for all eight as the compiler's waits did
     s16x8 ka[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) ka[ks] = *(const lds_s16x8*)(kp[ks]);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[ks]), as_bf16x8(qf[ks]),
-                                                     ks == 0 ? zero16 : s[0], 0, 0, 0);
-      ka[ks] = *(const lds_s16x8*)(kp[ks] + 32 * 256);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[ks]), as_bf16x8(qf[ks]),
-                                                     ks == 0 ? zero16 : s[1], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#define RFQ_KREAD(KS, OFF) \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ka[KS]) : "v"(kp[KS]), "i"(OFF))
+#define RFQ_KWAIT(KS, N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(ka[KS]))
+    RFQ_KREAD(0, 0); RFQ_KREAD(1, 0); RFQ_KREAD(2, 0); RFQ_KREAD(3, 0);
+    RFQ_KREAD(4, 0); RFQ_KREAD(5, 0); RFQ_KREAD(6, 0); RFQ_KREAD(7, 0);
+#define RFQ_QK0(KS)                                                                        \
+    RFQ_KWAIT(KS, 7);                                                                      \
+    s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[KS]), as_bf16x8(qf[KS]),   \
+                                                   (KS) == 0 ? zero16 : s[0], 0, 0, 0);    \
+    RFQ_KREAD(KS, 32 * 256);                                                               \
+    __builtin_amdgcn_sched_barrier(0);
+    RFQ_QK0(0) RFQ_QK0(1) RFQ_QK0(2) RFQ_QK0(3) RFQ_QK0(4) RFQ_QK0(5) RFQ_QK0(6) RFQ_QK0(7)
+#define RFQ_QK1(KS, N)                                                                     \
+    RFQ_KWAIT(KS, N);                                                                      \
+    s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[KS]), as_bf16x8(qf[KS]),   \
+                                                   (KS) == 0 ? zero16 : s[1], 0, 0, 0);    \
+    __builtin_amdgcn_sched_barrier(0);
+    RFQ_QK1(0, 7) RFQ_QK1(1, 6) RFQ_QK1(2, 5) RFQ_QK1(3, 4)
+    RFQ_QK1(4, 3) RFQ_QK1(5, 2) RFQ_QK1(6, 1) RFQ_QK1(7, 0)
+#undef RFQ_QK0
+#undef RFQ_QK1
+#undef RFQ_KREAD
+#undef RFQ_KWAIT
     const int kt = t * kKT;
     if (kt + kKT > ctx0 + qs || kt + kKT > kv_end) {
 #pragma unroll
