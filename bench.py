@@ -68,7 +68,26 @@ def parse():
     ap.add_argument("--time-budget", type=float, default=0.0,
                     help="seconds; if > 0 the latency phase is skipped once this much wall "
                          "time has passed (the JSON line is always printed)")
+    ap.add_argument("--tp-latency-model", default="auto",
+                    help="after the timed region, serve single requests of this model with "
+                         "ONE TP group over all N ranks (BASELINE config 4: 70B TP=8). "
+                         "'auto' = llama3-70b on the driver's 8-GPU run of the default "
+                         "8B DP bench; 'none' = off")
+    ap.add_argument("--tp-latency-runs", type=int, default=7)
+    ap.add_argument("--tp-latency-budget", type=float, default=300.0,
+                    help="seconds for the whole TP latency phase; a watchdog prints the "
+                         "JSON line (phase marked timeout) and ends every rank past it")
     return ap.parse_args()
+
+
+def _tp_latency_model(args, world: int) -> str | None:
+    m = os.environ.get("RFQ_BENCH_TP_LATENCY", args.tp_latency_model)
+    if m in ("", "none", "0"):
+        return None
+    if m == "auto":
+        return "llama3-70b" if (world == 8 and args.tp == 1 and args.model == "llama3-8b"
+                                and args.latency_runs > 0) else None
+    return m
 
 
 def _free_port() -> int:
@@ -220,6 +239,69 @@ def _single_stream(detail):
             "baseline_decode_tok_s": 350.0}
 
 
+class _Emitter:
+    """Rank 0's ONE JSON line, printed exactly once: by the main thread at the end,
+    or by the TP-phase watchdog if that phase overruns its budget."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self, out: dict) -> None:
+        with self.lock:
+            if not self.done:
+                print(json.dumps(out), flush=True)
+                self.done = True
+
+
+def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | None:
+    """BASELINE config 4 on the same node: one TP group spanning all N ranks serves
+    single /parse-text/-path requests of ``model`` (default Llama-3-70B at TP=8, RCCL
+    + the custom xGMI all-reduce, hipGraph decode).  Runs after the timed region (the
+    8B DP engine is freed first), so it never touches the docs/s measurement.
+
+    Bounded: a watchdog on every rank ends the process after ``--tp-latency-budget``
+    seconds (rank 0 first prints the JSON line with the phase marked ``timeout``); an
+    exception on any rank is reported instead of failing the whole bench."""
+    import torch
+
+    from replisense_rfq_amd.engine.engine import LLMEngine
+    from replisense_rfq_amd.utils.config import EngineConfig
+
+    budget = args.tp_latency_budget
+    timer = threading.Timer(budget, on_timeout)
+    timer.daemon = True
+    timer.start()
+    t0 = time.perf_counter()
+    res = {"model": model, "parallelism": f"tp{wctx.world}"}
+    try:
+        cfg = EngineConfig.from_env(
+            model=model, tp=wctx.world, seed=args.seed, max_num_seqs=8, max_kv_blocks=4096,
+            graph_buckets=(1, 2, 4, 8), use_graphs=not args.no_graphs,
+            jump_forward=not args.no_jump_forward, prefix_cache=not args.no_prefix_cache)
+        eng = LLMEngine(cfg, tp=wctx)
+        res["init_s"] = round(time.perf_counter() - t0, 1)
+        res["custom_allreduce"] = wctx.car is not None
+        if wctx.rank == 0:
+            lat, detail = latency(eng, 0, args.tp_latency_runs)
+            if wctx.enabled:
+                eng.shutdown()
+            res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
+            res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
+            res["single_stream"] = _single_stream(detail)
+            res["runs"] = len(lat)
+        else:
+            eng.worker_loop()
+        if eng.device.type == "cuda":
+            torch.cuda.synchronize()
+        res["status"] = "ok"
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never fatal
+        res["status"] = f"error: {type(e).__name__}: {str(e)[:300]}"
+    timer.cancel()
+    res["phase_s"] = round(time.perf_counter() - t0, 1)
+    return res
+
+
 def main():
     args = parse()
     t_start = time.perf_counter()
@@ -306,6 +388,7 @@ def main():
             lat, detail = r
     barrier()
 
+    out = None
     if rank == 0:
         docs = per * dp_world * args.steps
         value = docs / dt
@@ -346,7 +429,38 @@ def main():
                        "kv_blocks": stats.get("blocks"), "preempted": stats.get("preempted"),
                        "wall_s": round(time.perf_counter() - t_start, 1)},
         }
-        print(json.dumps(out), flush=True)
+
+    emitter = _Emitter()
+    tpl = _tp_latency_model(args, world)
+    if tpl is not None:
+        # free the DP replica (weights, KV pool, graph pools) before the TP group loads
+        import gc
+
+        del stream, engine
+        gc.collect()
+        if on_gpu:
+            torch.cuda.empty_cache()
+        barrier()
+
+        def on_timeout():
+            if out is not None:
+                emitter.emit(dict(out, tp_latency={
+                    "model": tpl, "status": f"timeout after {args.tp_latency_budget:.0f} s"}))
+            os._exit(0)
+
+        res = tp_latency_phase(tpl, args, wctx, rank, on_timeout)
+        if out is not None:
+            out["tp_latency"] = res
+            out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)
+        if res["status"] != "ok":
+            # the other ranks may be stuck mirroring a step that never comes: report
+            # and leave (their own watchdogs end them)
+            if out is not None:
+                emitter.emit(out)
+            sys.stdout.flush()
+            os._exit(0)
+    if out is not None:
+        emitter.emit(out)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

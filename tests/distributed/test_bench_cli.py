@@ -60,6 +60,43 @@ def test_bench_tp8_gloo():
     assert out["per_doc"]["valid"] == 1.0 and out["p50_parse_text_latency_s"] > 0
 
 
+def test_bench_tp_latency_phase_gloo():
+    """After the DP docs/s window the N ranks re-form as ONE TP group and serve
+    single requests (what the driver's 8-GPU run does with Llama-3-70B at TP=8):
+    the result rides in the same JSON line, the timed fields are untouched."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama", "--tp-latency-model", "tiny-llama-tp",
+                "--tp-latency-runs", "2"] + SMALL)
+    assert out["config"]["parallelism"] == "dp2"
+    tpl = out["tp_latency"]
+    assert tpl["status"] == "ok", tpl
+    assert tpl["model"] == "tiny-llama-tp" and tpl["parallelism"] == "tp2"
+    assert tpl["runs"] == 2 and tpl["p50_parse_text_latency_s"] > 0
+
+
+def test_bench_tp_latency_watchdog():
+    """A TP phase that overruns its budget still yields the JSON line (phase marked
+    timeout) and a zero exit on every rank."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama", "--tp-latency-model", "tiny-llama-tp",
+                "--tp-latency-budget", "0.05"] + SMALL)
+    assert out["tp_latency"]["status"].startswith("timeout"), out["tp_latency"]
+    assert out["value"] > 0
+
+
+def test_bench_tp_latency_auto_off():
+    """'auto' only turns the phase on for the driver's 8-GPU run of the 8B bench."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class A:
+        tp_latency_model, tp, model, latency_runs = "auto", 1, "llama3-8b", 15
+    assert bench._tp_latency_model(A, 8) == "llama3-70b"
+    assert bench._tp_latency_model(A, 4) is None and bench._tp_latency_model(A, 1) is None
+    A.tp = 8
+    assert bench._tp_latency_model(A, 8) is None
+
+
 def test_bench_self_launch():
     """`bench.py --gpus 2` outside torchrun starts 2 ranks itself (never a silent
     1-GPU run labelled whole-node)."""
