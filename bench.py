@@ -74,7 +74,7 @@ def parse():
                          "'auto' = llama3-70b on the driver's 8-GPU run of the default "
                          "8B DP bench; 'none' = off")
     ap.add_argument("--tp-latency-runs", type=int, default=7)
-    ap.add_argument("--tp-latency-budget", type=float, default=300.0,
+    ap.add_argument("--tp-latency-budget", type=float, default=240.0,
                     help="seconds for the whole TP latency phase; a watchdog prints the "
                          "JSON line (phase marked timeout) and ends every rank past it")
     return ap.parse_args()

@@ -76,7 +76,10 @@ class TPContext:
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """out: [world, *inp.shape]"""
         if self.world > 1:
-            dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group)
+            # rank-major rows: each of the world chunks of dim 0 has exactly inp's
+            # shape (gloo checks that; RCCL only checks the element count)
+            flat = out.flatten(0, 1) if inp.dim() >= 1 else out
+            dist.all_gather_into_tensor(flat, inp.contiguous(), group=self.group)
         else:
             out[0].copy_(inp)
         return out

@@ -84,6 +84,33 @@ def test_bench_tp_latency_watchdog():
     assert out["value"] > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_tp_latency_phase_one_gpu():
+    """The TP phase on the GPU path (HIP kernels at the TP shard shapes, the custom
+    IPC all-reduce inside the engine, the vocab-parallel sampler's all-gather): two
+    ranks share one MI355X over gloo (RCCL refuses two ranks per device).  The
+    pytest process itself never initialises the GPU (device_count only)."""
+    import torch
+
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    env_extra = {"RFQ_DIST_BACKEND": "gloo"}
+    os.environ.update(env_extra)
+    try:
+        out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                    "--model", "tiny-llama", "--kv-fraction", "0.05", "--no-graphs",
+                    "--tp-latency-model", "tiny-llama-tp", "--tp-latency-runs", "2"] + SMALL,
+                   timeout=380)
+    finally:
+        for k in env_extra:
+            os.environ.pop(k, None)
+    tpl = out["tp_latency"]
+    assert tpl["status"] == "ok", tpl
+    assert tpl["custom_allreduce"] is True and tpl["p50_parse_text_latency_s"] > 0
+    assert out["per_doc"]["valid"] == 1.0
+
+
 def test_bench_tp_latency_auto_off():
     """'auto' only turns the phase on for the driver's 8-GPU run of the 8B bench."""
     sys.path.insert(0, ROOT)
