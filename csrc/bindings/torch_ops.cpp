@@ -68,6 +68,9 @@ hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 uint32_t car_read_error(const void*);
+int car_norm_max_rows();
+void launch_car_oneshot_add_norm(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
+                                 const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
 void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
                        int, bf16_t*, int64_t, int, int, int, bool, bool, hipStream_t);
 void launch_moe_skinny_splitk(const bf16_t*, int64_t, const int32_t*, int, const int32_t*,
@@ -607,6 +610,35 @@ void car_allreduce(const Tensor& inp, const Tensor& out, c10::IntArrayRef bases,
     rfq::launch_car_oneshot(b, (int)rank, world, bp(inp), bpm(out), inp.numel(), cur_stream());
 }
 
+// residual <- bf16(allreduce(inp) + residual); out <- rmsnorm(residual) * w, one launch
+// (custom_ar.hip car_oneshot_add_norm_kernel).  inp: contiguous [rows, d] bf16.
+void car_allreduce_add_norm(const Tensor& inp, const Tensor& residual, const Tensor& w,
+                            double eps, const Tensor& out, c10::IntArrayRef bases, int64_t rank,
+                            int64_t capacity_bytes) {
+  CHECK_DEV(inp); CHECK_BF16(inp); CHECK_BF16(residual); CHECK_BF16(w); CHECK_BF16(out);
+  TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous(), "car_allreduce_add_norm: inp [rows, d]");
+  const int64_t rows = inp.size(0), d = inp.size(1);
+  TORCH_CHECK(residual.dim() == 2 && out.dim() == 2 && residual.size(0) == rows &&
+                  out.size(0) == rows && residual.size(1) == d && out.size(1) == d &&
+                  residual.stride(1) == 1 && out.stride(1) == 1 && w.numel() == d &&
+                  w.is_contiguous(),
+              "car_allreduce_add_norm: residual/out [rows, d] with unit column stride, w [d]");
+  TORCH_CHECK(d % 8 == 0 && d <= 16384 && residual.stride(0) % 8 == 0 && out.stride(0) % 8 == 0,
+              "car_allreduce_add_norm: d % 8 == 0, d <= 16384, 16-byte aligned rows");
+  TORCH_CHECK(rows >= 1 && rows <= rfq::car_norm_max_rows(), "car_allreduce_add_norm: rows");
+  for (const Tensor* t : {&inp, &residual, &w, &out})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "car_allreduce_add_norm: 16-byte aligned tensors required");
+  TORCH_CHECK(rows * d * 2 <= capacity_bytes, "car_allreduce_add_norm: message exceeds the buffer");
+  const int world = (int)bases.size();
+  TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "car_allreduce_add_norm: world");
+  char* b[8];
+  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  rfq::launch_car_oneshot_add_norm(b, (int)rank, world, bp(inp), bpm(residual), residual.stride(0),
+                                   bp(w), bpm(out), out.stride(0), (int)rows, (int)d, (float)eps,
+                                   cur_stream());
+}
+
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
                const Tensor& inv_pos, const Tensor& expert_of_block,
                const Tensor& expert_offsets, const Tensor& num_blocks) {
@@ -699,6 +731,8 @@ TORCH_LIBRARY(rfq_amd, m) {
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
+  m.def("car_allreduce_add_norm(Tensor inp, Tensor(a!) residual, Tensor w, float eps, "
+        "Tensor(b!) out, int[] bases, int rank, int capacity_bytes) -> ()");
   // host-side setup of the custom all-reduce regions (no tensor dispatch)
   m.def("car_alloc(int data_bytes) -> int", &car_alloc_op);
   m.def("car_free(int ptr) -> ()", &car_free_op);
@@ -755,6 +789,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("gemv_splitk", &gemv_splitk);
   m.impl("gemv_splitk_norm", &gemv_splitk_norm);
   m.impl("car_allreduce", &car_allreduce);
+  m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);
   m.impl("embed", &embed);
   m.impl("rope_kv", &rope_kv);

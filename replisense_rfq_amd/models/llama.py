@@ -146,8 +146,7 @@ class DecoderLM:
             if not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
                                                  x)):
                 o = ops.linear(attn, lw["o"])
-                self.tp.all_reduce_(o)
-                ops.fused_add_rms_norm(o, residual, lw["mlp_norm"], eps, out=x)
+                self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
             if cfg.is_moe:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
@@ -165,8 +164,7 @@ class DecoderLM:
                                                     gated=True):
                         continue
                     mo = ops.silu_linear(gu, lw["down"])
-            self.tp.all_reduce_(mo)
-            ops.fused_add_rms_norm(mo, residual, nxt, eps, out=x)
+            self.tp.all_reduce_add_norm_(mo, residual, nxt, eps, x)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
 

@@ -18,10 +18,15 @@ router then restarts the TP replica on RCCL (engine/router.py).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 from ..ops import _native
+
+# RFQ_CAR_NORM=0: keep the all-reduce and the residual-add RMSNorm as two launches
+FUSE_NORM = os.environ.get("RFQ_CAR_NORM", "1") != "0"
 
 
 class CustomAllReduce:
@@ -56,6 +61,28 @@ class CustomAllReduce:
         torch.ops.rfq_amd.car_allreduce(t, t, self.bases, self.rank, self.capacity, algo)
         self.calls += 1
         return t
+
+    # rows handled by the fused all-reduce + residual-add RMSNorm kernel (one
+    # workgroup per row; the signal area has 64 per-block flag slots)
+    NORM_MAX_ROWS = 64
+
+    def eligible_norm(self, t: torch.Tensor, residual: torch.Tensor, out: torch.Tensor) -> bool:
+        return (FUSE_NORM and self.eligible(t) and t.dim() == 2
+                and 1 <= t.shape[0] <= self.NORM_MAX_ROWS and t.shape[1] <= 16384
+                and residual.shape == t.shape and out.shape == t.shape
+                and residual.stride(1) == 1 and out.stride(1) == 1
+                and residual.stride(0) % 8 == 0 and out.stride(0) % 8 == 0
+                and all(x.data_ptr() % 16 == 0 for x in (t, residual, out)))
+
+    def all_reduce_add_norm_(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                             eps: float, out: torch.Tensor) -> torch.Tensor:
+        """residual <- bf16(sum over the group of t + residual); out <- rmsnorm(residual)
+        * w, in one launch (bit-identical to all_reduce_ + fused_add_rms_norm; t itself
+        is left holding this rank's partial)."""
+        torch.ops.rfq_amd.car_allreduce_add_norm(t, residual, w, eps, out, self.bases,
+                                                 self.rank, self.capacity)
+        self.calls += 1
+        return out
 
     def errors(self) -> int:
         return int(_native.ops().car_error(self.ptr))

@@ -45,6 +45,19 @@ class TPContext:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_add_norm_(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                             eps: float, out: torch.Tensor) -> torch.Tensor:
+        """Row-parallel projection epilogue of a decoder layer: all-reduce ``t``, then
+        residual += t and out = rmsnorm(residual) * w.  Decode-size messages on the
+        custom xGMI path run both in ONE kernel (custom_ar.hip
+        car_oneshot_add_norm_kernel); everything else is all_reduce_ + the fused norm."""
+        if self.world > 1 and self.car is not None and self.car.eligible_norm(t, residual, out):
+            return self.car.all_reduce_add_norm_(t, residual, w, eps, out)
+        from .. import ops
+
+        self.all_reduce_(t)
+        return ops.fused_add_rms_norm(t, residual, w, eps, out=out)
+
     def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
         """Switch all-reduces up to ``capacity_bytes`` to the xGMI one-/two-shot kernels
         (GPU groups only).  A start-up self-test runs both algorithms against the known

@@ -69,6 +69,47 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             errs.append(float((x.float() - want).abs().max()))
         dist.barrier()
+        # fused all-reduce + residual-add RMSNorm (car_oneshot_add_norm_kernel) is bit
+        # identical to the one-shot all-reduce followed by fused_add_rms_norm; calls
+        # interleave with the plain kernels on the shared per-block counters
+        from replisense_rfq_amd import ops
+
+        for rows, d in ((1, 8192), (3, 4096), (8, 1024), (2, 1000), (64, 8192)):
+            g = torch.Generator(device="cuda").manual_seed(rows * 100_003 + d)
+            parts = [torch.randn(rows, d, generator=g, device="cuda").to(torch.bfloat16)
+                     for _ in range(world)]
+            resid = torch.randn(rows, d, generator=g, device="cuda").to(torch.bfloat16)
+            w = (1 + 0.1 * torch.randn(d, generator=g, device="cuda")).to(torch.bfloat16)
+            t1, r1 = parts[rank].clone(), resid.clone()
+            o1 = torch.empty_like(t1)
+            assert car.eligible_norm(t1, r1, o1)
+            car.all_reduce_add_norm_(t1, r1, w, 1e-5, o1)
+            t2, r2 = parts[rank].clone(), resid.clone()
+            car.all_reduce_(t2, 1)
+            o2 = ops.fused_add_rms_norm(t2, r2, w, 1e-5)
+            torch.cuda.synchronize()
+            errs.append(0.0 if (torch.equal(r1, r2) and torch.equal(o1, o2)) else 99.0)
+        # ... and inside a captured graph, replayed with fresh inputs
+        t = torch.empty(4, 8192, device="cuda", dtype=torch.bfloat16)
+        r = torch.empty_like(t)
+        o = torch.empty_like(t)
+        w = torch.ones(8192, device="cuda", dtype=torch.bfloat16)
+        t.fill_(1.0)
+        r.fill_(0.0)
+        car.all_reduce_add_norm_(t, r, w, 1e-5, o)      # warm-up outside the capture
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            car.all_reduce_add_norm_(t, r, w, 1e-5, o)
+        for k in range(3):
+            t.fill_(float(rank + 1))
+            r.fill_(float(k))
+            dist.barrier()
+            graph.replay()
+            torch.cuda.synchronize()
+            errs.append(float((r.float() - (want + k)).abs().max()))
+            errs.append(float((o.float() - 1.0).abs().max()))     # rmsnorm of a constant row
+        dist.barrier()
         nerr = car.errors()
         car.close()
         # the engine's entry point: self-test, then route eligible all-reduces
