@@ -36,20 +36,37 @@ class CustomAllReduce:
         ops = _native.ops()
         self.rank, self.world, self.group = rank, world, group
         self.capacity = capacity_bytes
-        self.ptr = ops.car_alloc(capacity_bytes)
-        handle = ops.car_ipc_handle(self.ptr).numpy().tobytes()
+        self.bases, self._opened = [], []
+        self.calls = 0
+        # ``ok`` is False when this rank could not allocate, export or open a region.
+        # The group's collectives below still run on every rank (no rank leaves the
+        # set-up early and strands its peers); TPContext.enable_custom_allreduce then
+        # agrees on RCCL for the whole group.
+        self.ok = True
+        self.ptr = 0
+        handle = b""
+        try:
+            self.ptr = ops.car_alloc(capacity_bytes)
+            handle = ops.car_ipc_handle(self.ptr).numpy().tobytes()
+        except RuntimeError:
+            self.ok = False
         handles = [None] * world
         dist.all_gather_object(handles, handle, group=group)
-        self.bases, self._opened = [], []
-        for r in range(world):
-            if r == rank:
-                self.bases.append(self.ptr)
-            else:
-                p = ops.car_ipc_open(torch.frombuffer(bytearray(handles[r]), dtype=torch.uint8))
-                self.bases.append(p)
-                self._opened.append(p)
+        if self.ok and all(handles):
+            try:
+                for r in range(world):
+                    if r == rank:
+                        self.bases.append(self.ptr)
+                    else:
+                        p = ops.car_ipc_open(torch.frombuffer(bytearray(handles[r]),
+                                                              dtype=torch.uint8))
+                        self.bases.append(p)
+                        self._opened.append(p)
+            except RuntimeError:
+                self.ok = False
+        else:
+            self.ok = False
         dist.barrier(group=group)
-        self.calls = 0
 
     def eligible(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()

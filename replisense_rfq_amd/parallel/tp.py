@@ -67,6 +67,17 @@ class TPContext:
         from .custom_ar import CustomAllReduce
 
         car = CustomAllReduce(self.rank, self.world, self.group, capacity_bytes)
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+
+        def everyone(ok: bool) -> bool:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            return int(flag.item()) == 1
+
+        # a rank that could not set up its region votes RCCL before any kernel runs
+        if not everyone(car.ok):
+            car.close()
+            return False
         ok = True
         try:
             want = float(sum(range(1, self.world + 1)))
@@ -74,13 +85,16 @@ class TPContext:
                 x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
                 car.all_reduce_(x, algo)
                 ok &= bool((x.float() == want).all().item())
+            t = torch.full((2, 4096), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
+            r, o = torch.zeros_like(t), torch.empty_like(t)
+            if car.eligible_norm(t, r, o):       # the fused decode epilogue, same vote
+                car.all_reduce_add_norm_(t, r, torch.ones(4096, dtype=torch.bfloat16,
+                                                          device="cuda"), 1e-5, o)
+                ok &= bool((r.float() == want).all().item())
             ok &= car.errors() == 0
         except RuntimeError:
             ok = False
-        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        if int(flag.item()) == 0:
+        if not everyone(ok):
             car.close()
             return False
         self.car = car
