@@ -239,6 +239,26 @@ def _single_stream(detail):
             "baseline_decode_tok_s": 350.0}
 
 
+class _Heartbeat:
+    """Rank 0 prints a progress line to stderr every ``period`` seconds, so a long
+    silent phase (engine init, the timed window, the TP phase) never looks hung to
+    a supervisor watching the output.  stdout keeps exactly the one JSON line."""
+
+    def __init__(self, t_start: float, period: float = 30.0):
+        self.t_start = t_start
+        self.phase = "init"
+        self.stream = None
+        self.stop = threading.Event()
+        self.thread = threading.Thread(target=self._run, args=(period,), daemon=True)
+        self.thread.start()
+
+    def _run(self, period: float):
+        while not self.stop.wait(period):
+            done = self.stream.completed if self.stream is not None else 0
+            print(f"[bench] t={time.perf_counter() - self.t_start:.0f}s phase={self.phase} "
+                  f"docs_completed={done}", file=sys.stderr, flush=True)
+
+
 class _Emitter:
     """Rank 0's ONE JSON line, printed exactly once: by the main thread at the end,
     or by the TP-phase watchdog if that phase overruns its budget."""
@@ -327,6 +347,12 @@ def main():
         prefix_cache=not args.no_prefix_cache, max_batched_tokens=args.prefill_chunk,
         kv_fraction=args.kv_fraction)
     t_init = time.perf_counter()
+    hb = _Heartbeat(t_start) if rank == 0 else None
+
+    def mark(name):
+        if hb is not None:
+            hb.phase = name
+
     engine = LLMEngine(cfg, tp=tp)
     t_init = time.perf_counter() - t_init
     on_gpu = engine.device.type == "cuda"
@@ -352,12 +378,16 @@ def main():
 
     stream = DocStream(engine, dp_rank, args.seed, args.max_num_seqs) if tp.rank == 0 else None
     per = args.docs_per_step
+    if hb is not None:
+        hb.stream = stream
+    mark("warmup")
     phase(lambda: stream.run_until(args.warmup * per))
     if stream is not None:
         stream.finished.clear()
     steps0 = engine.num_steps
     barrier()
     sync()
+    mark("timed")
     t0 = time.perf_counter()
     phase(lambda: stream.run_until((args.warmup + args.steps) * per))
     sync()
@@ -382,6 +412,7 @@ def main():
         f = torch.tensor([int(run_lat)], device=engine.device if on_gpu else "cpu")
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         run_lat = bool(f.item())
+    mark("latency")
     if run_lat and dp_rank == 0:
         r = phase(lambda: latency(engine, dp_rank, args.latency_runs))
         if r is not None:
@@ -436,6 +467,8 @@ def main():
         # free the DP replica (weights, KV pool, graph pools) before the TP group loads
         import gc
 
+        if hb is not None:
+            hb.stream = None          # the heartbeat must not keep the DP engine alive
         del stream, engine
         gc.collect()
         if on_gpu:
@@ -448,6 +481,7 @@ def main():
                     "model": tpl, "status": f"timeout after {args.tp_latency_budget:.0f} s"}))
             os._exit(0)
 
+        mark(f"tp_latency:{tpl}")
         res = tp_latency_phase(tpl, args, wctx, rank, on_timeout)
         if out is not None:
             out["tp_latency"] = res
