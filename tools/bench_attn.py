@@ -122,6 +122,14 @@ def main():
                     row[f"s{sp}_t1_us"] = round(run_latency(C, Hq, 8, sp, tiles=1), 2)
                 print(json.dumps(row), flush=True)
         return
+    if os.environ.get("LAT_TP8"):
+        # Llama-3-70B TP=8 rank shape (Hq 8, Hkv 1): only splits x 1 kv head waves
+        for C in (512, 1024, 2048, 4096):
+            row = {"Hq": 8, "Hkv": 1, "ctx": C}
+            for sp in (8, 16, 32):
+                row[f"s{sp}_us"] = round(run_latency(C, 8, 1, sp, L=80), 2)
+            print(json.dumps(row), flush=True)
+        return
     if os.environ.get("TILES_AB"):
         # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
         for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (3072, 800, 416, 1)]:
