@@ -216,9 +216,11 @@ def latency(engine, dp_rank: int, runs: int):
         t0 = time.perf_counter()
         ids = tok.chat_ids(build_messages(d.text))
         s, = engine.generate([ids], engine.default_params(**synth.decode_hints(d)))
-        parse_and_validate_response(engine.decode_text(s), "direct_text_input")
+        r = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
         out.append(time.perf_counter() - t0)
-        detail.append((s.num_generated, s.num_sampled, s.span().get("ttft_ms") or 0.0, out[-1]))
+        ok = bool(r.get("success")) and "validation warnings" not in r.get("message", "")
+        detail.append((s.num_generated, s.num_sampled, s.span().get("ttft_ms") or 0.0, out[-1],
+                       ok))
     return out, detail
 
 
@@ -228,7 +230,7 @@ def _single_stream(detail):
     if not detail:
         return None
     rates, steps, ttft = [], [], []
-    for gen, sampled, ttft_ms, total in detail:
+    for gen, sampled, ttft_ms, total, _ in detail:
         dec = max(total - ttft_ms / 1e3, 1e-6)
         rates.append(gen / dec)
         steps.append(sampled / dec)
@@ -236,7 +238,8 @@ def _single_stream(detail):
     return {"completion_tok_s_p50": round(statistics.median(rates), 1),
             "sampled_steps_per_s_p50": round(statistics.median(steps), 1),
             "ttft_ms_p50": round(statistics.median(ttft), 1),
-            "baseline_decode_tok_s": 350.0}
+            "baseline_decode_tok_s": 350.0,
+            "valid": round(sum(d[4] for d in detail) / len(detail), 3)}
 
 
 class _Heartbeat:
