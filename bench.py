@@ -74,6 +74,10 @@ def parse():
                          "'auto' = llama3-70b on the driver's 8-GPU run of the default "
                          "8B DP bench; 'none' = off")
     ap.add_argument("--tp-latency-runs", type=int, default=7)
+    ap.add_argument("--tp-docs", type=int, default=256,
+                    help="TP phase: documents timed in a continuous stream (0 = skip)")
+    ap.add_argument("--tp-in-flight", type=int, default=128,
+                    help="TP phase: documents in flight during that stream")
     ap.add_argument("--tp-latency-budget", type=float, default=240.0,
                     help="seconds for the whole TP latency phase; a watchdog prints the "
                          "JSON line (phase marked timeout) and ends every rank past it")
@@ -279,40 +283,66 @@ class _Emitter:
 
 def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | None:
     """BASELINE config 4 on the same node: one TP group spanning all N ranks serves
-    single /parse-text/-path requests of ``model`` (default Llama-3-70B at TP=8, RCCL
-    + the custom xGMI all-reduce, hipGraph decode).  Runs after the timed region (the
+    ``model`` (default Llama-3-70B at TP=8: RCCL + the custom xGMI all-reduce fused
+    with the residual-add RMSNorm, hipGraph decode).  Runs after the timed region (the
     8B DP engine is freed first), so it never touches the docs/s measurement.
 
+      1. single /parse-text/-path requests on the idle group (p50, decode rates);
+      2. ``--tp-docs`` documents of a continuous stream with ``--tp-in-flight`` in
+         flight, after a warm-up of half that many (docs/s of the TP group).
+
     Bounded: a watchdog on every rank ends the process after ``--tp-latency-budget``
-    seconds (rank 0 first prints the JSON line with the phase marked ``timeout``); an
-    exception on any rank is reported instead of failing the whole bench."""
+    seconds (rank 0 first prints the JSON line with whatever the phase measured so
+    far, marked ``timeout``); an exception on any rank is reported instead of failing
+    the whole bench."""
     import torch
 
     from replisense_rfq_amd.engine.engine import LLMEngine
     from replisense_rfq_amd.utils.config import EngineConfig
 
-    budget = args.tp_latency_budget
-    timer = threading.Timer(budget, on_timeout)
+    res = {"model": model, "parallelism": f"tp{wctx.world}"}
+    timer = threading.Timer(args.tp_latency_budget, lambda: on_timeout(res))
     timer.daemon = True
     timer.start()
     t0 = time.perf_counter()
-    res = {"model": model, "parallelism": f"tp{wctx.world}"}
     try:
+        nseq = max(8, args.tp_in_flight)
+        buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256) if b <= nseq)
         cfg = EngineConfig.from_env(
-            model=model, tp=wctx.world, seed=args.seed, max_num_seqs=8, max_kv_blocks=4096,
-            graph_buckets=(1, 2, 4, 8), use_graphs=not args.no_graphs,
-            jump_forward=not args.no_jump_forward, prefix_cache=not args.no_prefix_cache)
+            model=model, tp=wctx.world, seed=args.seed, max_num_seqs=nseq,
+            max_kv_blocks=max(4096, nseq * 48), graph_buckets=buckets,
+            use_graphs=not args.no_graphs, jump_forward=not args.no_jump_forward,
+            prefix_cache=not args.no_prefix_cache)
         eng = LLMEngine(cfg, tp=wctx)
         res["init_s"] = round(time.perf_counter() - t0, 1)
         res["custom_allreduce"] = wctx.car is not None
         if wctx.rank == 0:
-            lat, detail = latency(eng, 0, args.tp_latency_runs)
-            if wctx.enabled:
-                eng.shutdown()
-            res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
-            res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
-            res["single_stream"] = _single_stream(detail)
-            res["runs"] = len(lat)
+            try:
+                lat, detail = latency(eng, 0, args.tp_latency_runs)
+                res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
+                res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
+                res["single_stream"] = _single_stream(detail)
+                res["runs"] = len(lat)
+                if args.tp_docs > 0:
+                    stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
+                    warm = max(1, args.tp_in_flight // 2)
+                    stream.run_until(warm)
+                    stream.finished.clear()
+                    if eng.device.type == "cuda":
+                        torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    stream.run_until(warm + args.tp_docs)
+                    if eng.device.type == "cuda":
+                        torch.cuda.synchronize()
+                    dt = time.perf_counter() - t1
+                    res["docs_per_s"] = round(args.tp_docs / dt, 3)
+                    res["docs"], res["in_flight"] = args.tp_docs, args.tp_in_flight
+                    res["per_doc"] = {k: round(v, 2)
+                                      for k, v in validate(eng, stream.finished).items()}
+                    stream.close()
+            finally:
+                if wctx.enabled:
+                    eng.shutdown()
         else:
             eng.worker_loop()
         if eng.device.type == "cuda":
@@ -478,10 +508,10 @@ def main():
             torch.cuda.empty_cache()
         barrier()
 
-        def on_timeout():
+        def on_timeout(partial):
             if out is not None:
-                emitter.emit(dict(out, tp_latency={
-                    "model": tpl, "status": f"timeout after {args.tp_latency_budget:.0f} s"}))
+                emitter.emit(dict(out, tp_latency=dict(
+                    partial, status=f"timeout after {args.tp_latency_budget:.0f} s")))
             os._exit(0)
 
         mark(f"tp_latency:{tpl}")

@@ -66,12 +66,13 @@ def test_bench_tp_latency_phase_gloo():
     the result rides in the same JSON line, the timed fields are untouched."""
     out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
                 "--model", "tiny-llama", "--tp-latency-model", "tiny-llama-tp",
-                "--tp-latency-runs", "2"] + SMALL)
+                "--tp-latency-runs", "2", "--tp-docs", "4", "--tp-in-flight", "2"] + SMALL)
     assert out["config"]["parallelism"] == "dp2"
     tpl = out["tp_latency"]
     assert tpl["status"] == "ok", tpl
     assert tpl["model"] == "tiny-llama-tp" and tpl["parallelism"] == "tp2"
     assert tpl["runs"] == 2 and tpl["p50_parse_text_latency_s"] > 0
+    assert tpl["docs"] == 4 and tpl["docs_per_s"] > 0 and tpl["per_doc"]["valid"] == 1.0
 
 
 def test_bench_tp_latency_watchdog():
@@ -100,7 +101,8 @@ def test_bench_tp_latency_phase_one_gpu():
     try:
         out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
                     "--model", "tiny-llama", "--kv-fraction", "0.05", "--no-graphs",
-                    "--tp-latency-model", "tiny-llama-tp", "--tp-latency-runs", "2"] + SMALL,
+                    "--tp-latency-model", "tiny-llama-tp", "--tp-latency-runs", "2",
+                    "--tp-docs", "8", "--tp-in-flight", "4"] + SMALL,
                    timeout=380)
     finally:
         for k in env_extra:
@@ -108,6 +110,7 @@ def test_bench_tp_latency_phase_one_gpu():
     tpl = out["tp_latency"]
     assert tpl["status"] == "ok", tpl
     assert tpl["custom_allreduce"] is True and tpl["p50_parse_text_latency_s"] > 0
+    assert tpl["docs_per_s"] > 0 and tpl["per_doc"]["valid"] == 1.0
     assert out["per_doc"]["valid"] == 1.0
 
 
