@@ -152,10 +152,11 @@ class DecoderLM:
                 mo = moe_mlp(x, lw["router"], lw["w13"], lw["w2"], cfg.moe_topk, moe_bufs,
                              expert_offset=self.expert_offset)
             else:
-                # latency path: gate|up with the SwiGLU epilogue (one kernel, [M, F] out)
-                act = ops.linear_swiglu(x, lw["gate_up"]) if fuse else None
+                # latency path (any TP degree): gate|up with the SwiGLU epilogue (one
+                # kernel, [M, F] out); TP = 1 may also fold the norm into down
+                act = ops.linear_swiglu(x, lw["gate_up"]) if T <= ops.NORM_FUSE_MAX_M else None
                 if act is not None:
-                    if ops.linear_add_norm(act, lw["down"], residual, nxt, eps, x):
+                    if fuse and ops.linear_add_norm(act, lw["down"], residual, nxt, eps, x):
                         continue
                     mo = ops.linear(act, lw["down"])
                 else:

@@ -342,6 +342,12 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
         rplan, rreport = tune_rope(groups["qkv"], ms, model.cos_sin, model.hq, model.hkv)
         set_rope_plan(rplan)
         report += rreport
+    if "gate_up" in groups and os.environ.get("RFQ_FUSE_SWIGLU", "1") != "0":
+        # column-parallel gate|up: the SwiGLU epilogue needs no collective, so the
+        # plan applies at any TP degree (the shard's own F = ffn / TP)
+        wplan, wreport = tune_swiglu(groups["gate_up"], ms)
+        set_swiglu_plan(wplan)
+        report += wreport
     tp = getattr(model, "tp", None)
     if os.environ.get("RFQ_FUSE_NORM", "1") != "0" and not (tp is not None and tp.enabled):
         # TP = 1 only: with TP an all-reduce sits between the projection and the norm
@@ -355,10 +361,6 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
             p3, r3 = tune_norm(groups["down"], ms, nw, gated=False)
             nplan.update(p3)
             nreport += [("down(act)+norm",) + tuple(r[1:]) for r in r3]
-        if "gate_up" in groups and os.environ.get("RFQ_FUSE_SWIGLU", "1") != "0":
-            wplan, wreport = tune_swiglu(groups["gate_up"], ms)
-            set_swiglu_plan(wplan)
-            nreport += wreport
         set_norm_plan(nplan)
         report += nreport
     if max_tokens > 0:
