@@ -26,6 +26,7 @@ class TPContext:
     world: int = 1
     group: object = None
     car: object = None            # CustomAllReduce (RFQ_CUSTOM_AR, on by default)
+    car_status: str = ""          # why the custom all-reduce is (not) in use
 
     @property
     def enabled(self) -> bool:
@@ -77,26 +78,33 @@ class TPContext:
         # a rank that could not set up its region votes RCCL before any kernel runs
         if not everyone(car.ok):
             car.close()
+            self.car_status = "set-up failed" + ("" if car.ok else " on this rank")
             return False
-        ok = True
+        why = []
         try:
             want = float(sum(range(1, self.world + 1)))
             for algo, n in ((1, 4096), (2, 1 << 19)):
                 x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
                 car.all_reduce_(x, algo)
-                ok &= bool((x.float() == want).all().item())
+                if not bool((x.float() == want).all().item()):
+                    why.append(f"algo {algo} sum")
             t = torch.full((2, 4096), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
             r, o = torch.zeros_like(t), torch.empty_like(t)
             if car.eligible_norm(t, r, o):       # the fused decode epilogue, same vote
                 car.all_reduce_add_norm_(t, r, torch.ones(4096, dtype=torch.bfloat16,
                                                           device="cuda"), 1e-5, o)
-                ok &= bool((r.float() == want).all().item())
-            ok &= car.errors() == 0
-        except RuntimeError:
-            ok = False
-        if not everyone(ok):
+                if not bool((r.float() == want).all().item()):
+                    why.append("add-norm residual")
+            if car.errors():
+                why.append(f"{car.errors()} flag timeouts")
+        except RuntimeError as e:
+            why.append(f"{type(e).__name__}: {str(e)[:120]}")
+        if not everyone(not why):
             car.close()
+            self.car_status = "self-test failed" + (f" on this rank: {'; '.join(why)}"
+                                                    if why else " on a peer")
             return False
+        self.car_status = "ok"
         self.car = car
         return True
 

@@ -111,17 +111,20 @@ def _worker(rank, world, port, q):
             errs.append(float((o.float() - 1.0).abs().max()))     # rmsnorm of a constant row
         dist.barrier()
         nerr = car.errors()
-        car.close()
-        # the engine's entry point: self-test, then route eligible all-reduces
+        # the engine's entry point: self-test, then route eligible all-reduces.  The
+        # first region stays open meanwhile (an engine opens its region once; freeing
+        # and re-exporting at the same address is not a production pattern)
         from replisense_rfq_amd.parallel.tp import TPContext
 
         tp = TPContext(rank=rank, world=world, group=dist.group.WORLD)
-        assert tp.enable_custom_allreduce(capacity_bytes=2 << 20), "self-test failed"
+        assert tp.enable_custom_allreduce(capacity_bytes=2 << 20), tp.car_status
         y = torch.full((8192,), float(rank + 1), device="cuda", dtype=torch.bfloat16)
         tp.all_reduce_(y)
         errs.append(float((y.float() - want).abs().max()))
         nerr += tp.car.errors()
+        dist.barrier()
         tp.car.close()
+        car.close()
         q.put((rank, errs, nerr))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
