@@ -22,6 +22,13 @@ def _col(row, *names):
     raise KeyError(names)
 
 
+def _short(n):
+    if n is None:
+        return "-"
+    n = n.split("(")[0]
+    return n if len(n) <= 60 else n[:57] + "..."
+
+
 def main(d, window_s=3.0):
     traces = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     if not traces:
@@ -39,6 +46,8 @@ def main(d, window_s=3.0):
     ev = [x for x in ev if x[0] >= lo]
     busy, cur_s, cur_e = 0, None, None
     gaps = []
+    where = defaultdict(lambda: [0, 0])       # (kernel before, kernel after) of big gaps
+    prev_n = None
     per = defaultdict(lambda: [0, 0])
     for s, e, n in ev:
         per[n][0] += 1
@@ -48,9 +57,14 @@ def main(d, window_s=3.0):
         elif s > cur_e:
             busy += cur_e - cur_s
             gaps.append(s - cur_e)
+            if s - cur_e >= 20_000:
+                k = (_short(prev_n), _short(n))
+                where[k][0] += 1
+                where[k][1] += s - cur_e
             cur_s, cur_e = s, e
         else:
             cur_e = max(cur_e, e)
+        prev_n = n
     busy += cur_e - cur_s
     wall = ev[-1][1] - ev[0][0]
     gaps.sort()
@@ -62,6 +76,10 @@ def main(d, window_s=3.0):
         print(f"gaps < 20 us (between kernels of a step): {len(small)} summing "
               f"{sum(small) / 1e6:.1f} ms, median {small[len(small) // 2] / 1e3:.2f} us")
     print(f"gaps >= 20 us (host waits between steps): {len(big)} summing {sum(big) / 1e6:.1f} ms")
+    if where:
+        print("\n| big gap after | before | count | total ms |\n|---|---|---|---|")
+        for (a, b), (c, t) in sorted(where.items(), key=lambda kv: -kv[1][1])[:8]:
+            print(f"| `{a}` | `{b}` | {c} | {t / 1e6:.1f} |")
     print("\n| kernel | calls | total ms | avg us | % of busy |\n|---|---|---|---|---|")
     for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:25]:
         nm = n if len(n) <= 90 else n[:87] + "..."
