@@ -272,6 +272,14 @@ void EngineCore::set_graph_keys(const std::vector<std::pair<int32_t, int32_t>>& 
     if (nb_buckets_.empty() || nb_buckets_.back() != k.first) nb_buckets_.push_back(k.first);
 }
 
+// Smallest captured (sequence bucket, token bucket) that holds na sequences and t
+// tokens.  Normally only the first sequence bucket >= na is tried: past it the
+// padding would cost more than eager launches save.  In the latency regime (a
+// bucket of at most kLatencyBucket sequences) a step whose jump-forward extends
+// outgrow that bucket's token multiples (t > 8 na) moves up to the next buckets:
+// padded rows of a replayed graph cost far less than ~500 eager launches.
+constexpr int32_t kLatencyBucket = 16;
+
 bool EngineCore::graph_key(int32_t na, int32_t t, int32_t& nb, int32_t& tb) const {
   for (int32_t b : nb_buckets_) {
     if (b < na) continue;
@@ -283,7 +291,7 @@ bool EngineCore::graph_key(int32_t na, int32_t t, int32_t& nb, int32_t& tb) cons
         return true;
       }
     }
-    return false;
+    if (b >= kLatencyBucket) return false;
   }
   return false;
 }
