@@ -291,7 +291,7 @@ bool EngineCore::graph_key(int32_t na, int32_t t, int32_t& nb, int32_t& tb) cons
         return true;
       }
     }
-    if (b >= kLatencyBucket) return false;
+    if (b > kLatencyBucket) return false;
   }
   return false;
 }

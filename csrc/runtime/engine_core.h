@@ -119,6 +119,13 @@ class EngineCore {
   std::vector<int32_t> drain_finished();
 
   void set_graph_keys(const std::vector<std::pair<int32_t, int32_t>>& keys);
+  // (nb, tb) of the captured graph a step of na sequences / t tokens would replay,
+  // or (-1, -1) for an eager step (exposed for tests)
+  std::pair<int32_t, int32_t> find_graph_key(int32_t na, int32_t t) const {
+    int32_t nb = -1, tb = -1;
+    if (!graph_key(na, t, nb, tb)) nb = tb = -1;
+    return {nb, tb};
+  }
   // Pin the cached full blocks of `tokens` (a prompt prefix whose KV is already
   // published, e.g. by a warm-up prefill): they hold a reference for the engine's
   // lifetime, so the shared prompt template is never evicted.  Returns the number

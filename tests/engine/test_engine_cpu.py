@@ -217,3 +217,25 @@ def test_shared_prefix_warm_and_pinned(engine):
     assert s.prefix_hit_tokens >= engine.pinned_blocks * engine.kv.block_size
     assert engine.core.prefix_hits > hits0
     assert engine.stats()["pinned_blocks"] == engine.pinned_blocks
+
+
+def test_graph_key_latency_fallthrough():
+    """Graph selection (engine_core.cpp graph_key): the first sequence bucket >= na
+    with a token multiple >= t; in the latency regime (buckets <= 16) a step whose
+    jump-forward extends outgrow that bucket moves up to the next bucket's padded
+    graph instead of running eagerly; larger buckets never pad across buckets."""
+    from replisense_rfq_amd.engine.runner import TOKEN_MULTS
+
+    core = _core(token_mults=list(TOKEN_MULTS))
+    buckets = (1, 2, 4, 8, 16, 32, 64)
+    core.set_graph_keys(sorted((b, b * m) for b in buckets for m in TOKEN_MULTS))
+    assert core.graph_key(1, 1) == (1, 1)
+    assert core.graph_key(1, 7) == (1, 8)
+    assert core.graph_key(1, 9) == (2, 12)        # was eager
+    assert core.graph_key(1, 30) == (4, 32)
+    assert core.graph_key(3, 20) == (4, 24)
+    assert core.graph_key(3, 40) == (8, 48)
+    assert core.graph_key(16, 200) == (32, 256)   # bucket 16 still falls through
+    assert core.graph_key(17, 300) == (-1, -1)    # bucket 32: eager, no cross-bucket pad
+    assert core.graph_key(64, 512) == (64, 512)
+    assert core.graph_key(65, 65) == (-1, -1)     # beyond the captured buckets
