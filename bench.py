@@ -529,6 +529,11 @@ def main():
     if out is not None:
         emitter.emit(out)
     if world > 1:
+        if tpl is not None:
+            # a peer whose TP phase failed has already left: never wait on it forever
+            guard = threading.Timer(60.0, lambda: os._exit(0))
+            guard.daemon = True
+            guard.start()
         dist.barrier()
         dist.destroy_process_group()
 

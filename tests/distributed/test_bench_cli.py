@@ -85,6 +85,15 @@ def test_bench_tp_latency_watchdog():
     assert out["value"] > 0
 
 
+def test_bench_tp_latency_error_reported():
+    """A TP phase that raises (here: an unknown model) is reported in the JSON line;
+    the timed fields stand and every rank exits 0."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama", "--tp-latency-model", "no-such-model"] + SMALL)
+    assert out["tp_latency"]["status"].startswith("error"), out["tp_latency"]
+    assert out["value"] > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(400)
 def test_bench_tp_latency_phase_one_gpu():
