@@ -208,6 +208,30 @@ def validate(engine, seqs) -> dict:
         valid=ok / n)
 
 
+def _pcts(vals) -> dict | None:
+    """p50 / p90 / p99 / max / mean of a list of seconds (nearest-rank percentiles)."""
+    if not vals:
+        return None
+    v = sorted(vals)
+
+    def q(p):
+        return v[min(len(v) - 1, max(0, int(round(p / 100.0 * len(v) + 0.5)) - 1))]
+    return {"p50": round(q(50), 3), "p90": round(q(90), 3), "p99": round(q(99), 3),
+            "max": round(v[-1], 3), "mean": round(sum(v) / len(v), 3), "n": len(v)}
+
+
+def loaded_latency(seqs) -> dict:
+    """Latency under load of the documents that completed inside a timed window:
+    submission to the engine -> last token (``e2e``) and -> first sampled token
+    (``ttft``), the server-side time a closed-loop client with this many requests
+    in flight waits per document (the reference's only metric is per-request
+    server time, /root/reference/app/rfq_agent.py:158-168; its LLM call times out
+    at 30 s, rfq_agent.py:69)."""
+    e2e = [s.t_finish - s.t_arrival for s in seqs if s.t_finish and s.t_arrival]
+    ttft = [s.t_first_token - s.t_arrival for s in seqs if s.t_first_token and s.t_arrival]
+    return {"e2e_s": _pcts(e2e), "ttft_s": _pcts(ttft)}
+
+
 def latency(engine, dp_rank: int, runs: int):
     """Single-request end-to-end latency of the extraction path (idle engine)."""
     from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response

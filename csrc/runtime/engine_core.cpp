@@ -24,7 +24,8 @@ inline int32_t f2i(float f) {
 }  // namespace
 
 EngineCore::EngineCore(const CoreConfig& cfg, std::shared_ptr<const Grammar> grammar)
-    : cfg_(cfg), grammar_(std::move(grammar)), bm_(cfg.num_blocks, cfg.block_size) {}
+    : cfg_(cfg), max_batched_tokens0_(cfg.max_batched_tokens), grammar_(std::move(grammar)),
+      bm_(cfg.num_blocks, cfg.block_size) {}
 
 // ------------------------------------------------------------------ requests
 int32_t EngineCore::add(const int32_t* prompt, int32_t n, const SeqParams& p, double t_arrival) {

@@ -20,6 +20,7 @@
 // The Python engine keeps request intake, the device side and result delivery.
 #pragma once
 #include <cstdint>
+#include <algorithm>
 #include <deque>
 #include <memory>
 #include <utility>
@@ -119,6 +120,11 @@ class EngineCore {
   std::vector<int32_t> drain_finished();
 
   void set_graph_keys(const std::vector<std::pair<int32_t, int32_t>>& keys);
+  // Lower the per-step token budget (prefill chunk) at run time; never above the
+  // construction value, so payload_bound() stays an upper bound of every step.
+  void set_max_batched_tokens(int32_t n) {
+    cfg_.max_batched_tokens = std::max(1, std::min(n, max_batched_tokens0_));
+  }
   // (nb, tb) of the captured graph a step of na sequences / t tokens would replay,
   // or (-1, -1) for an eager step (exposed for tests)
   std::pair<int32_t, int32_t> find_graph_key(int32_t na, int32_t t) const {
@@ -157,6 +163,7 @@ class EngineCore {
   bool graph_key(int32_t na, int32_t t, int32_t& nb, int32_t& tb) const;
 
   CoreConfig cfg_;
+  int32_t max_batched_tokens0_;
   std::shared_ptr<const Grammar> grammar_;
   BlockManager bm_;
   std::vector<Seq> seqs_;

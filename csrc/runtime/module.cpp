@@ -228,6 +228,9 @@ PYBIND11_MODULE(_runtime, m) {
       })
       .def("release", &EngineCore::release)
       .def("set_graph_keys", &EngineCore::set_graph_keys)
+      .def("set_max_batched_tokens", &EngineCore::set_max_batched_tokens)
+      .def_property_readonly("max_batched_tokens",
+                             [](const EngineCore& e) { return e.cfg().max_batched_tokens; })
       .def("graph_key", &EngineCore::find_graph_key)
       .def("pin_prefix", [](EngineCore& e, arr<int32_t> tokens) {
         return e.pin_prefix(tokens.data(), (int32_t)tokens.size());

@@ -42,7 +42,8 @@ from fastapi.responses import JSONResponse
 from ..service.extract import ExtractService
 from ..service.parser import FileParser, FileParsingError
 from ..utils.dotenv import load_dotenv
-from .multipart import MultipartError, MultipartStream, missing_field_detail
+from .multipart import (MultipartError, MultipartLimitError, MultipartStream,
+                        missing_field_detail)
 
 load_dotenv()                              # app/main.py:23 (before the constants below)
 logging.basicConfig(level=logging.INFO,
@@ -263,6 +264,9 @@ async def _upload_file_param(request: Request):
         async for chunk in request.stream():
             mp.feed(chunk)
         form = mp.close()
+    except MultipartLimitError as e:
+        # FastAPI's answer to a form Starlette refuses (field / file / part limits)
+        raise HTTPException(status_code=400, detail="There was an error parsing the body") from e
     except MultipartError:
         form = {}
     files = form.get("file")

@@ -8,6 +8,11 @@ above 1 MiB, like Starlette).  The body is never held in memory as a whole, and 
 file part is stored only up to ``max_file_bytes + 1`` bytes: past that the
 response is decided already (400 for a missing name / unsupported type, else 413,
 in the reference's order, app/main.py:214-227), so the rest is counted, not kept.
+Only the first file part of each field name is stored at all (the route reads
+``files[0]``); later ones are counted.  Starlette's limits hold for the rest:
+non-file parts up to 1 MiB, at most 1,000 fields and 1,000 files
+(:class:`MultipartLimitError`, answered 400 "There was an error parsing the body"
+as FastAPI does for a form Starlette refuses).
 Missing fields reproduce FastAPI's RequestValidationError body for
 ``file: UploadFile = File(...)`` (reference app/main.py:205-209).
 """
@@ -22,10 +27,17 @@ _BOUNDARY = re.compile(r'boundary="?([^";]+)"?', re.I)
 _DISP = re.compile(r'(\w+)\*?=(?:"((?:[^"\\]|\\.)*)"|([^;]*))')
 SPOOL_BYTES = 1024 * 1024
 MAX_HEADER_BYTES = 16 * 1024
+MAX_PART_BYTES = 1024 * 1024       # Starlette's max_part_size for non-file parts
+MAX_FIELDS = 1000                  # Starlette's max_fields / max_files
+MAX_FILES = 1000
 
 
 class MultipartError(ValueError):
     pass
+
+
+class MultipartLimitError(MultipartError):
+    """The body breaks a size / count limit (answered 400, not treated as 'no form')."""
 
 
 def _parse_disposition(value: str) -> dict:
@@ -58,6 +70,9 @@ class _Part:
             if keep:
                 self.sink.write(bytes(data[:keep]))
         else:
+            if self.size + n > MAX_PART_BYTES:
+                raise MultipartLimitError(
+                    f"Part exceeded maximum size of {MAX_PART_BYTES // 1024}KB.")
             self.sink += data
         self.size += n
 
@@ -90,6 +105,7 @@ class MultipartStream:
         self.state = "preamble"
         self.part: _Part | None = None
         self.fields: dict[str, list] = {}
+        self.nfields = self.nfiles = 0
 
     def _finish_part(self) -> None:
         p = self.part
@@ -136,7 +152,20 @@ class MultipartStream:
                         k, v = line.split(":", 1)
                         hdrs[k.strip().lower()] = v.strip()
                 del self.buf[:i + skip]
-                self.part = _Part(hdrs, self.limit)
+                part = _Part(hdrs, self.limit)
+                if part.is_file:
+                    self.nfiles += 1
+                    if self.nfiles > MAX_FILES:
+                        raise MultipartLimitError(
+                            f"Too many files. Maximum number of files is {MAX_FILES}.")
+                    if part.name in self.fields:      # only files[0] is ever read
+                        part.limit = -1
+                else:
+                    self.nfields += 1
+                    if self.nfields > MAX_FIELDS:
+                        raise MultipartLimitError(
+                            f"Too many fields. Maximum number of fields is {MAX_FIELDS}.")
+                self.part = part
                 self.state = "body"
             elif self.state == "body":
                 i = self.buf.find(self.body_delim)

@@ -205,7 +205,7 @@ class LLMEngine:
     def step(self) -> list[Sequence]:
         ts = time.perf_counter()
         if self.faults.active and self.core.has_work:
-            self.faults.on_step(self.num_steps)
+            self.faults.on_step(self.num_steps, self.tp.enabled and self.cfg.custom_allreduce)
         with trace_range("execute"):
             toks = self.runner.execute(self.core, ts)
         if toks is None:

@@ -72,6 +72,7 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
     from ..utils.config import EngineConfig
     from ..utils.faults import FaultInjector
     from .engine import LLMEngine
+    from ..utils.faults import CustomAllReduceError
     from .sequence import SamplingParams
 
     cfg = EngineConfig(**cfg_dict)
@@ -100,8 +101,16 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
             pass
         if not eng.has_work():
             continue
+        fatal = False
         try:
             finished = eng.step()
+        except CustomAllReduceError:
+            # the custom all-reduce's flag protocol failed: this replica's sums can no
+            # longer be trusted (the error counter is sticky).  Fail what it holds and
+            # exit, so _check_workers restarts the TP group on RCCL all-reduces.
+            log.exception("replica %d: custom all-reduce failure, restarting on RCCL", idx)
+            finished = eng.abort_all("engine_error")
+            fatal = True
         except Exception:                      # fail this replica's in-flight work
             log.exception("replica %d step failed", idx)
             finished = eng.abort_all("engine_error")
@@ -111,10 +120,10 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
                 outq.put(("done", rid, {"text": eng.decode_text(s), "finish": s.finish_reason,
                                         "span": s.span()}))
                 served += 1
-        if exit_after is not None and served >= exit_after:
-            outq.close()                       # flush what was served, then crash
+        if fatal or (exit_after is not None and served >= exit_after):
+            outq.close()                       # flush what was served, then leave
             outq.join_thread()
-            os._exit(3)                        # injected replica crash
+            os._exit(4 if fatal else 3)        # 3 = injected replica crash
 
 
 class DPRouter:

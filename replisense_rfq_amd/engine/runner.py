@@ -30,6 +30,7 @@ import torch
 from .. import ops
 from ..models.llama import DecoderLM, ForwardMeta
 from ..parallel.tp import TPContext
+from ..utils.faults import CustomAllReduceError
 from .kv_cache import KVCache
 
 (H_T, H_TA, H_NA, H_WA, H_NB, H_WB, H_S, H_MAXB, H_GNB, H_GTB, H_SPLITS, H_PAYLOAD,
@@ -78,7 +79,9 @@ class ModelRunner:
         self._stage = None                   # its numpy view
         self._header = np.zeros(HEADER, np.int32)
         self.decode_tiles = int(getattr(cfg, "decode_tiles", 1))
-        self.prefill_qblk = ops.prefill_qblk(model.hq, model.hkv) if self.is_cuda else 32
+        # validated on every device (a config the GPU kernels cannot run fails at start-up)
+        qblk = ops.prefill_qblk(model.hq, model.hkv)
+        self.prefill_qblk = qblk if self.is_cuda else 32
         self.ring = None
         # SURVEY.md §5.2 debug check: Inf/NaN logits are counted on device inside the step
         # (captured into the decode graphs too) and read back with the sampled tokens
@@ -266,10 +269,11 @@ class ModelRunner:
         car = self.tp.car
         if car is not None and car.errors():
             # a peer's flag never arrived inside the kernel's bounded spin: the sums of
-            # this step may be stale.  Fail the step (its requests get engine_error);
-            # on a TP follower this ends the process and the router restarts the
-            # replica with RCCL all-reduces (router.py).
-            raise RuntimeError(f"custom all-reduce: {car.errors()} flag timeouts on TP rank "
+            # this step may be stale.  The error counter is never reset: the replica
+            # is done.  On a TP follower this ends the process; TP rank 0's router
+            # worker fails its requests and exits (router.py), and the router
+            # restarts the whole group with RCCL all-reduces.
+            raise CustomAllReduceError(f"custom all-reduce: {car.errors()} flag timeouts on TP rank "
                                f"{self.tp.rank}; results of this step are unreliable")
         self.stats["steps"] += 1
         self.stats["graph_steps"] += bool(key[0])

@@ -409,10 +409,19 @@ def attn_decode_shared(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len
                          out, Hq, Hkv, scale)
 
 
+PREFILL_GROUPS = {2: 64, 4: 64, 8: 32}
+
+
 def prefill_qblk(Hq: int, Hkv: int) -> int:
-    """Queries per prefill work item: 256 (query, head) rows per workgroup (8 waves)
-    -> 64 queries at GQA group 4 (Llama-3-8B, Mixtral), 32 at group 8 (Llama-3-70B)."""
-    return 64 if Hq // Hkv == 4 else 32
+    """Queries per prefill work item: 128 or 256 (query, head) rows per workgroup (4 or
+    8 waves, attn_prefill.hip) -> 64 queries at GQA group 4 (Llama-3-8B, Mixtral) and
+    2, 32 at group 8 (Llama-3-70B).  Other groups have no prefill kernel instance:
+    rejected here, when the model is built, not at the first prefill."""
+    g = Hq // Hkv if Hkv else 0
+    if Hkv <= 0 or Hq % Hkv or g not in PREFILL_GROUPS:
+        raise ValueError(f"attn_prefill supports GQA groups {sorted(PREFILL_GROUPS)} "
+                         f"(Hq / Hkv per rank); got Hq={Hq}, Hkv={Hkv}")
+    return PREFILL_GROUPS[g]
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,

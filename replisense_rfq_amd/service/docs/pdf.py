@@ -24,8 +24,11 @@ The reference extracts PDF text with PyMuPDF ``page.get_text()``, table rows wit
 """
 from __future__ import annotations
 
+import logging
 import re
 import zlib
+
+log = logging.getLogger("replisense_rfq_amd.service.docs.pdf")
 
 # ------------------------------------------------------------------ lexer
 
@@ -438,7 +441,9 @@ class PdfDocument:
                   for x0, x1, y, s, c in pt.glyphs]
         try:               # table failures never fail the page (file_parser.py:194-196)
             return text, extract_tables(pt.segments, glyphs, h)
-        except (ValueError, TypeError, KeyError, IndexError, ZeroDivisionError):
+        except Exception as e:  # noqa: BLE001 -- like the reference (file_parser.py:194-196),
+            # a table failure never fails the page: keep its text, drop its tables
+            log.warning("table extraction failed on page %d: %s", i + 1, e)
             return text, []
 
     def page_images(self, i: int) -> list:

@@ -18,6 +18,12 @@ Same pipeline as that strategy (the pdfplumber lattice algorithm it is built on)
                box lies more than half inside it, grouped into lines by baseline,
                lines joined by "\\n".
 
+Untrusted uploads bound the work per page: a page with more than MAX_SEGMENTS
+path segments, or whose snapped grid could hold more than MAX_POINTS crossings,
+skips table detection (its page text is still emitted); the cell search stops at
+the first uncovered candidate and glyphs are looked up through a top-sorted
+index, so a dense ruled grid costs O(points + cells x glyphs-per-cell).
+
 PyMuPDF is not installable here, so byte parity with its table text is
 unpinned; tests/parser/test_pdf_tables.py pins this implementation on generated
 ruled-table PDFs and checks that the reference fixture (no ruled tables) still
@@ -25,8 +31,11 @@ parses byte-identically.
 """
 from __future__ import annotations
 
+import bisect
 from collections import defaultdict
 
+MAX_SEGMENTS = 20_000      # painted path segments per page considered for tables
+MAX_POINTS = 20_000        # horizontal x vertical snapped lines per page
 SNAP = 3.0
 JOIN = 3.0
 ISECT = 3.0
@@ -91,6 +100,16 @@ def _covers(segs, a: float, b: float, tol: float) -> bool:
     return any(s0 - tol <= a and b <= s1 + tol for s0, s1 in segs)
 
 
+def _reach(coords: list, start: float, segs) -> list:
+    """Sorted coords > start that the edge segs spans continuously from start."""
+    out = []
+    for c in coords[bisect.bisect_right(coords, start):]:
+        if not _covers(segs, start, c, ISECT):
+            break
+        out.append(c)
+    return out
+
+
 def find_cells(H: dict, V: dict) -> list[tuple[float, float, float, float]]:
     points = set()
     for y, hsegs in H.items():
@@ -106,8 +125,10 @@ def find_cells(H: dict, V: dict) -> list[tuple[float, float, float, float]]:
         ys_at_x[x].append(y)
     cells = []
     for x, y in pts:
-        below = [b for b in sorted(ys_at_x[x]) if b > y and _covers(V[x], y, b, ISECT)]
-        right = [r for r in sorted(xs_at_y[y]) if r > x and _covers(H[y], x, r, ISECT)]
+        # candidates in increasing distance; once an edge stops covering the span,
+        # every farther candidate fails too (a segment covering [y, b'] covers [y, b])
+        below = _reach(ys_at_x[x], y, V[x])
+        right = _reach(xs_at_y[y], x, H[y])
         found = None
         for b in below:
             for r in right:
@@ -148,9 +169,27 @@ def group_tables(cells) -> list[list[tuple]]:
     return tables
 
 
+class GlyphIndex:
+    """Glyphs sorted by top: the candidates of a cell [t, b] are the glyphs whose top
+    lies in [t - tallest glyph, b)."""
+
+    def __init__(self, glyphs):
+        self.glyphs = sorted(glyphs, key=lambda g: g[2])
+        self.tops = [g[2] for g in self.glyphs]
+        self.tallest = max((g[3] - g[2] for g in self.glyphs), default=0.0)
+
+    def near(self, t: float, b: float):
+        lo = bisect.bisect_left(self.tops, t - self.tallest)
+        hi = bisect.bisect_left(self.tops, b)
+        return self.glyphs[lo:hi]
+
+
 def cell_text(glyphs, cell) -> str:
-    """glyphs: [(x0, x1, top, bottom, baseline, size, ch)] in top-left coordinates."""
+    """glyphs: [(x0, x1, top, bottom, baseline, size, ch)] in top-left coordinates, or
+    a GlyphIndex of them."""
     x0, t, x1, b = cell
+    if isinstance(glyphs, GlyphIndex):
+        glyphs = glyphs.near(t, b)
     inside = []
     for g in glyphs:
         gx0, gx1, gt, gb = g[0], g[1], g[2], g[3]
@@ -186,9 +225,12 @@ def cell_text(glyphs, cell) -> str:
 
 def extract_tables(segments, glyphs, height: float) -> list[list[list]]:
     """-> tables, each a list of rows, each a list of cell strings (or None)."""
-    H, V = edges_from_segments(segments, height)
-    if not H or not V:
+    if len(segments) > MAX_SEGMENTS:
         return []
+    H, V = edges_from_segments(segments, height)
+    if not H or not V or len(H) * len(V) > MAX_POINTS:
+        return []
+    glyphs = GlyphIndex(glyphs)
     tables = []
     for cells in group_tables(find_cells(H, V)):
         cols = sorted({round(c[0], 3) for c in cells})

@@ -10,6 +10,9 @@ tests drive each one deterministically.
   step_raise:N      raise RuntimeError on engine step N (0-based)
   step_sleep:N:MS   sleep MS milliseconds inside step N (watchdog tests)
   replica_exit:N    a DP replica process exits after serving N requests
+  car_error:N       engine step N fails as if the custom all-reduce had counted a
+                    flag timeout (only on an engine configured with the custom
+                    all-reduce; the replica then restarts on RCCL)
 """
 from __future__ import annotations
 
@@ -19,6 +22,11 @@ import time
 
 class InjectedFault(RuntimeError):
     pass
+
+
+class CustomAllReduceError(RuntimeError):
+    """A custom all-reduce flag timed out during a step: its sums may be stale.
+    Fatal for the whole TP replica (engine/router.py restarts it on RCCL)."""
 
 
 class FaultInjector:
@@ -33,11 +41,15 @@ class FaultInjector:
     def active(self) -> bool:
         return bool(self.rules)
 
-    def on_step(self, step: int) -> None:
+    def on_step(self, step: int, custom_allreduce: bool = False) -> None:
         for i, (kind, args) in enumerate(self.rules):
             if kind == "step_raise" and args and args[0] == step:
                 del self.rules[i]                    # each fault fires once
                 raise InjectedFault(f"injected fault at step {step}")
+            if kind == "car_error" and args and args[0] == step and custom_allreduce:
+                del self.rules[i]
+                raise CustomAllReduceError(f"custom all-reduce: injected flag timeout at "
+                                           f"step {step}")
             if kind == "step_sleep" and len(args) == 2 and args[0] == step:
                 time.sleep(args[1] / 1000.0)
 

@@ -86,3 +86,38 @@ def test_api_order_400_before_413(monkeypatch):
     r = client.post("/upload/", files={"file": ("doc.txt", big, "text/plain")})
     assert r.status_code == 413
     assert r.json()["error"] == "File too large. Maximum size: 1MB"
+
+
+def test_limits_text_part_field_and_file_counts():
+    """non-file parts are capped at 1 MiB and the field / file
+    counts at 1,000 (Starlette's limits); a second file part under the same name is
+    counted but never stored."""
+    from replisense_rfq_amd.api.multipart import MultipartLimitError
+
+    with pytest.raises(MultipartLimitError):
+        parse_form(_body([("note", None, b"y" * (1024 * 1024 + 1))]), CT)
+    with pytest.raises(MultipartLimitError):
+        parse_form(_body([(f"f{i}", None, b"v") for i in range(1001)]), CT)
+    with pytest.raises(MultipartLimitError):
+        parse_form(_body([("file", f"{i}.txt", b"v") for i in range(1001)]), CT)
+    form = parse_form(_body([("file", "a.txt", b"first"), ("file", "b.txt", b"x" * 4096)]), CT)
+    first, second = form["file"]
+    assert _dump({"f": [first]})["f"][0] == ("a.txt", 5, b"first")
+    assert second.size == 4096
+    second.file.seek(0, 2)
+    assert second.file.tell() == 0
+
+
+def test_api_oversized_text_field_is_400(monkeypatch):
+    from replisense_rfq_amd.api import main
+    from replisense_rfq_amd.service.extract import ExtractService, MockBackend
+    from replisense_rfq_amd.service.parser import FileParser
+
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_parser, lambda: FileParser())
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_field_generator,
+                        lambda: ExtractService(MockBackend()))
+    client = TestClient(main.app)
+    r = client.post("/upload/", files={"file": ("a.txt", b"hello", "text/plain")},
+                    data={"note": "z" * (1024 * 1024 + 10)})
+    assert r.status_code == 400
+    assert r.json()["error"] == "There was an error parsing the body"

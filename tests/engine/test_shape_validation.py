@@ -1,0 +1,33 @@
+"""a GQA group the prefill kernel has no instance for is rejected
+when the model / runner is built (a clear ValueError), not by a TORCH_CHECK at the
+first prefill on the GPU."""
+from dataclasses import replace
+
+import pytest
+
+from replisense_rfq_amd import ops
+from replisense_rfq_amd.engine.engine import LLMEngine
+from replisense_rfq_amd.models.config import TINY_LLAMA, get_config
+from replisense_rfq_amd.utils.config import EngineConfig
+
+
+@pytest.mark.parametrize("hq,hkv,qblk", [(32, 8, 64), (64, 8, 32), (8, 1, 32), (16, 8, 64),
+                                          (4, 1, 64)])
+def test_supported_groups(hq, hkv, qblk):
+    assert ops.prefill_qblk(hq, hkv) == qblk
+    assert qblk * (hq // hkv) // 32 in (4, 8)          # the kernel's wave counts
+
+
+@pytest.mark.parametrize("hq,hkv", [(16, 1), (12, 1), (8, 8), (6, 4), (4, 0)])
+def test_unsupported_groups_rejected(hq, hkv):
+    with pytest.raises(ValueError, match="GQA groups"):
+        ops.prefill_qblk(hq, hkv)
+
+
+def test_engine_build_rejects_group16(monkeypatch):
+    bad = replace(TINY_LLAMA, name="tiny-g16", n_heads=16, n_kv_heads=1)
+    import replisense_rfq_amd.engine.engine as E
+
+    monkeypatch.setattr(E, "get_config", lambda name: bad if name == "tiny-g16" else get_config(name))
+    with pytest.raises(ValueError, match="GQA groups"):
+        LLMEngine(EngineConfig(model="tiny-g16", device="cpu", max_num_seqs=2))

@@ -142,3 +142,40 @@ def test_request_deadline_aborts_and_frees_kv():
     assert not eng.has_work()
     assert eng.kv.stats()["free"] == free0
     aeng.shutdown()
+
+
+@pytest.mark.slow
+def test_router_custom_allreduce_error_restarts_on_rccl(monkeypatch):
+    """a custom all-reduce flag timeout on TP rank 0 (simulated by
+    the car_error fault, which fires only while the custom all-reduce is configured)
+    fails that replica's requests, the rank-0 worker exits, and the router restarts
+    the whole TP group with custom_allreduce=False -- which then serves."""
+    from replisense_rfq_amd.engine.router import DPRouter
+
+    monkeypatch.setenv("RFQ_FAULT", "car_error:8")
+    cfg = _cfg(model="tiny-llama-tp", tp=2, max_num_seqs=2, custom_allreduce=True)
+    router = DPRouter(cfg, 1, 2)
+    try:
+        tok = router.backend().tokenizer
+        ids = tok.chat_ids(build_messages(synth.make_rfq(1).text))
+        params = dict(temperature=0.1, max_tokens=1200, grammar=True, min_items=0, profile=1)
+        import time
+
+        try:
+            out = asyncio.run(router.generate(ids, params, timeout=300))
+            assert out["finish"] == "engine_error", out
+        except RuntimeError as e:            # the replica died before replying
+            assert "replica died" in str(e)
+        deadline = time.time() + 300
+        while router.restarts == 0 and time.time() < deadline:
+            time.sleep(0.2)
+        assert router.restarts >= 1
+        assert router._cfg_dict["custom_allreduce"] is False
+        while not router.healthy and time.time() < deadline:
+            time.sleep(0.2)
+        out = asyncio.run(router.generate(ids, params, timeout=300))
+        assert out["finish"] == "stop"
+        RFQResponse(**json.loads(out["text"]))
+        assert router.restarts == 1
+    finally:
+        router.shutdown()

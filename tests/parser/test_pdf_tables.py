@@ -67,3 +67,27 @@ def test_fixture_has_no_ruled_tables():
         pytest.skip("fixture not present")
     doc = PdfDocument.open(fx)
     assert all(doc.page_text_and_tables(i)[1] == [] for i in range(len(doc)))
+
+
+def test_pathological_grid_is_bounded():
+    """table detection on untrusted uploads is bounded per page.  A
+    260 x 200-line ruled grid (52,000 crossings) is skipped within a time bound; a
+    dense grid under the cap (100 x 100 lines, ~10^4 cells, a glyph in each) is
+    extracted with the indexed glyph lookup, also within a bound."""
+    import time
+
+    h = 800.0
+    seg = [(0, float(y), 600, float(y)) for y in range(0, 780, 3)][:260]
+    seg += [(float(x) * 3, 0, float(x) * 3, 780) for x in range(200)]
+    t0 = time.perf_counter()
+    assert extract_tables(seg, [], h) == []
+    assert time.perf_counter() - t0 < 5.0
+    n = 100
+    seg = [(0, 7.0 * i, 7.0 * (n - 1), 7.0 * i) for i in range(n)]
+    seg += [(7.0 * i, 0, 7.0 * i, 7.0 * (n - 1)) for i in range(n)]
+    glyphs = [(7.0 * i + 2, 7.0 * i + 4, h - (7.0 * j + 5), h - (7.0 * j + 2), h - (7.0 * j + 2.5),
+               3.0, "x") for i in range(n - 1) for j in range(n - 1)]
+    t0 = time.perf_counter()
+    t = extract_tables(seg, glyphs, h)
+    assert time.perf_counter() - t0 < 30.0
+    assert len(t) == 1 and len(t[0]) == n - 1 and all(c == "x" for c in t[0][0])
