@@ -63,6 +63,8 @@ void launch_moe_grouped_gemm(const bf16_t*, const bf16_t*, bf16_t*, const int32_
                              int, int, int, int, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, int, bf16_t*,
                         int64_t, hipStream_t);
+void launch_gemm_dense(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int, int,
+                       int, int, bool, int, hipStream_t);
 int64_t car_signal_bytes();
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -702,6 +704,29 @@ void moe_gemm8(const Tensor& x, const Tensor& w, const Tensor& out,
                         x.size(0) / 128, n_out, K, E, N, n_out, swiglu, (int)tile, cur_stream());
 }
 
+// Dense large-M GEMM (gemm_dense.hip): out[M, N] = x[M, K] . w[N, K]^T, or with swiglu
+// (w = [Wg; Wu] [2F, K]) out[M, F] = silu(x Wg^T) * (x Wu^T).
+void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu, int64_t cfg) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_dense: w must be row-major [N, K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  const int64_t n_out = swiglu ? N / 2 : N;
+  TORCH_CHECK(w.size(1) == K && K % 64 == 0 && K >= 64, "gemm_dense: w [N, K], K % 64 == 0");
+  TORCH_CHECK(swiglu ? (N % 256 == 0) : (N % 256 == 0),
+              "gemm_dense: N % 256 == 0 (2F with F % 128 == 0 for swiglu)");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "gemm_dense: out shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0,
+              "gemm_dense: 16-byte aligned operand rows");
+  TORCH_CHECK(x.stride(0) * 256 < (int64_t)INT32_MAX && N * w.stride(0) < (int64_t)INT32_MAX,
+              "gemm_dense: operand offsets exceed int32");
+  rfq::launch_gemm_dense(bp(x), x.stride(0), bp(w), w.stride(0), bpm(out), out.stride(0), (int)M,
+                         (int)n_out, (int)K, (int)n_out, swiglu, (int)cfg, cur_stream());
+}
+
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
 void moe_combine(const Tensor& y, const Tensor& inv_pos, const Tensor& weights, int64_t topk,
                  const Tensor& out) {
@@ -772,6 +797,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("moe_grouped_gemm(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_of_block, "
         "Tensor num_blocks) -> ()");
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
+  m.def("gemm_dense(Tensor x, Tensor w, Tensor(a!) out, bool swiglu=False, int cfg=0) -> ()");
   m.def("moe_skinny_splitk(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) yf, int max_rows, int splits) -> ()");
   m.def("moe_combine_splitk(Tensor yf, int splits, Tensor inv_pos, Tensor weights, int topk, "
@@ -806,6 +832,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("moe_gemm8", &moe_gemm8);
   m.impl("count_nonfinite", &count_nonfinite);
   m.impl("moe_combine", &moe_combine);
+  m.impl("gemm_dense", &gemm_dense);
   m.impl("moe_skinny_splitk", &moe_skinny_splitk);
   m.impl("moe_combine_splitk", &moe_combine_splitk);
 }

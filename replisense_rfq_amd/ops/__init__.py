@@ -21,6 +21,7 @@ __all__ = [
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
     "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
+    "gemm_dense", "gemm_dense_ok",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -320,6 +321,29 @@ def linear(x, w, out=None, plan: int | None = None):
     if out is None:
         return x @ w.t()
     torch.matmul(x, w.t(), out=out)
+    return out
+
+
+def gemm_dense_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
+    """Shapes the hand-written 256x256 MFMA GEMM (csrc/kernels/gemm_dense.hip) takes:
+    K % 64 == 0, N % 256 == 0 (N = 2F with F % 128 == 0 under swiglu)."""
+    return M >= 1 and K % 64 == 0 and K >= 64 and N % 256 == 0
+
+
+def gemm_dense(x, w, out=None, swiglu: bool = False, cfg: int = 0):
+    """out[M, N] = x[M, K] . w[N, K]^T on the 8-wave ping-pong MFMA kernel; swiglu:
+    w = gate|up [2F, K] and out[M, F] = silu(x Wg^T) * (x Wu^T) (rounded like the
+    unfused GEMM -> bf16 -> silu_mul).  GPU only; CPU tensors use the torch oracle."""
+    M, N = x.shape[0], w.shape[0]
+    n_out = N // 2 if swiglu else N
+    if out is None:
+        out = torch.empty((M, n_out), dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        _native.ops().gemm_dense(x, w, out, swiglu, cfg)
+    elif swiglu:
+        ref.silu_mul(x @ w.t(), out)
+    else:
+        torch.matmul(x, w.t(), out=out)
     return out
 
 

@@ -162,3 +162,13 @@ def test_bench_driver_flags_time_budget():
     assert out["ms_per_step"] * 20 / 1e3 < wall
     assert out["engine"]["docs_completed_in_window_rank0"] >= 40
     assert out["per_doc"]["valid"] == 1.0
+    # latency under load of the timed window's documents, the
+    # service's deadline, the shaped-workload label, no docs/s baseline to divide by
+    lat = out["loaded_latency_s"]
+    assert {"p50", "p90", "p99", "max", "mean", "n"} <= set(lat)
+    assert 0 < lat["p50"] <= lat["p90"] <= lat["p99"] <= lat["max"]
+    assert lat["n"] == out["engine"]["docs_completed_in_window_rank0"]
+    assert out["loaded_ttft_s"]["p50"] <= lat["p50"]
+    assert out["latency_slo_s"] == 30.0 and isinstance(out["slo_met_p99"], bool)
+    assert out["config"]["profile"] == "synthetic" and out["config"]["in_flight_per_replica"] == 4
+    assert out["vs_baseline"] is None

@@ -677,3 +677,41 @@ def test_gemv_splitk(gpu, M, cfg, N, K):
         _close(out, want, 3e-2, 2e-2, f"gemv_splitk_norm cfg={cfg} it={it}")
     torch.cuda.synchronize()
     assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 128), (256, 768, 1024),
+                                   (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096)])
+def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
+    """The 256x256 8-wave MFMA GEMM (gemm_dense.hip) against the fp32 oracle, asymmetric
+    operands, row tails (M % 256 != 0), one-tile and many-tile K loops; swiglu vs the
+    unfused GEMM -> bf16 -> silu_mul rounding."""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    x = ((torch.rand(M, K, device="cuda", generator=g) * 2 - 1)).to(BF)
+    w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(BF)
+    out = ops.gemm_dense(x, w, swiglu=swiglu, cfg=cfg)
+    r = x.float() @ w.float().t()
+    if swiglu:
+        F = N // 2
+        gg, u = r[:, :F].to(BF).float(), r[:, F:].to(BF).float()
+        r = (gg * torch.sigmoid(gg)).to(BF).float() * u
+    _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+def test_gemm_dense_identity_asymmetric(gpu, cfg):
+    """A = I with an asymmetric B catches a transposed C write (§3)."""
+    K = 256
+    x = torch.eye(K, device="cuda", dtype=BF)
+    w = (torch.arange(512 * K, device="cuda", dtype=torch.float32).reshape(512, K) % 97 - 48).to(BF)
+    out = ops.gemm_dense(x, w, cfg=cfg)
+    assert torch.equal(out.float(), w.float().t()[:K])
+
+
+def test_gemm_dense_strided_rows(gpu):
+    x = torch.randn(300, 1024 + 64, device="cuda", dtype=BF)[:, :1024]
+    w = (torch.randn(512, 1024, device="cuda") / 32).to(BF)
+    out = torch.empty(300, 512 + 256, device="cuda", dtype=BF)[:, :512]
+    ops.gemm_dense(x, w, out=out)
+    _close(out, x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, what="strided")

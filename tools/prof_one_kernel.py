@@ -44,6 +44,18 @@ def run(kind, *a):
         for _ in range(5):
             ops.moe_gemm8(bufs.xs[:cap], w13, bufs.act[:cap], bufs.expert_of_block[:nb],
                           bufs.num_blocks, bufs.expert_offsets, True, tile)
+    elif kind == "gemm":
+        # python tools/prof_one_kernel.py run gemm M N K swiglu(0|1) cfg
+        from replisense_rfq_amd import ops
+
+        M, N, K, swi, cfg = (int(x) for x in a)
+        dev = torch.device("cuda:0")
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        for _ in range(10):
+            ops.gemm_dense(x, w, swiglu=bool(swi), cfg=cfg)
+        for _ in range(10):
+            torch.matmul(x, w.t())
     torch.cuda.synchronize()
 
 
