@@ -274,6 +274,17 @@ def _single_stream(detail):
             "valid": round(sum(d[4] for d in detail) / len(detail), 3)}
 
 
+def _gemm_plan_summary() -> dict:
+    """Which large-M projections the start-up plan put on the hand-written MFMA GEMM
+    (ops/autotune.py tune_split): buckets won per projection."""
+    try:
+        from replisense_rfq_amd.ops.autotune import SPLIT_REPORT
+    except Exception:  # noqa: BLE001
+        return {}
+    return {r[0].split(":", 1)[1]: r[5] for r in SPLIT_REPORT
+            if r[0].startswith("dense:") and isinstance(r[5], str) and "buckets" in r[5]}
+
+
 class _Heartbeat:
     """Rank 0 prints a progress line to stderr every ``period`` seconds, so a long
     silent phase (engine init, the timed window, the TP phase) never looks hung to
@@ -526,6 +537,7 @@ def main():
             "per_doc": {k: round(v, 2) for k, v in shape.items()},
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
                        "gemm_tune_s": round(engine.tune_s, 1),
+                       "gemm_plan": _gemm_plan_summary(),
                        "timed_engine_steps": steps_timed,
                        "docs_completed_in_window_rank0": done_in_window,
                        "graph_steps": stats.get("graph_steps"), "steps": stats.get("steps"),

@@ -56,7 +56,7 @@ __device__ __forceinline__ void gbar() {
   asm volatile("" ::: "memory");
 }
 
-template <int EPI, int MF>
+template <int EPI, int MF, int PH>
 __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
     bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off, int tiles_m, int tiles_n) {
@@ -79,29 +79,42 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
   const int g = wid >> 2, wn = wid & 3;
   const int r = lane & 31, h2 = lane >> 5;
 
-  // ---- LDS-DMA pieces of this wave (per K-tile): 8 pieces of 8 rows x 128 B.
-  // piece slot i (0..7) -> (half H, piece P) ; R segment of slot i = i >> 1.
-  //   g0: R1 W[24+2wn..]  R2 XA[8+2wn..]  R3 XB[8+2wn..]  R4 W[8+2wn..]
-  //   g1: R1 XA[2wn..]    R2 XB[2wn..]    R3 W[2wn..]     R4 W[16+2wn..]
+  // ---- LDS-DMA pieces of this wave (per K-tile): 8 pieces of 8 rows x 128 B, issued
+  // PH = 4: two per R segment (slot = segment);  PH = 2: four per R segment.
+  //   PH 4  g0: R1 W[24+2wn..]  R2 XA[8+2wn..]  R3 XB[8+2wn..]  R4 W[8+2wn..]
+  //         g1: R1 XA[2wn..]    R2 XB[2wn..]    R3 W[2wn..]     R4 W[16+2wn..]
+  //   PH 2  g0: R1 W[16+4wn..]  R2 XB[4wn..]
+  //         g1: R1 XA[4wn..]    R2 W[4wn..]
   // W pieces 0..15 are half W0 (tile rows 0..127), 16..31 half W1.
+  constexpr int PPS = 8 / PH;                      // pieces per R segment per wave
   const int prow = lane >> 3, pch = lane & 7;
   int src_off[8];             // element offset from the x / w tile base (+ k0)
   int dst_off[8];             // bf16 element offset inside a stage (wave-uniform)
   bool src_is_w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int seg = i >> 1, pp = i & 1;
+    const int seg = i / PPS, pp = i % PPS;
     int half, piece;          // half: 0 XA, 1 XB, 2 W (piece 0..31 over W0|W1)
-    if (g == 0) {
-      if (seg == 0) { half = 2; piece = 24 + 2 * wn + pp; }
-      else if (seg == 1) { half = 0; piece = 8 + 2 * wn + pp; }
-      else if (seg == 2) { half = 1; piece = 8 + 2 * wn + pp; }
-      else { half = 2; piece = 8 + 2 * wn + pp; }
+    if constexpr (PH == 4) {
+      if (g == 0) {
+        if (seg == 0) { half = 2; piece = 24 + 2 * wn + pp; }
+        else if (seg == 1) { half = 0; piece = 8 + 2 * wn + pp; }
+        else if (seg == 2) { half = 1; piece = 8 + 2 * wn + pp; }
+        else { half = 2; piece = 8 + 2 * wn + pp; }
+      } else {
+        if (seg == 0) { half = 0; piece = 2 * wn + pp; }
+        else if (seg == 1) { half = 1; piece = 2 * wn + pp; }
+        else if (seg == 2) { half = 2; piece = 2 * wn + pp; }
+        else { half = 2; piece = 16 + 2 * wn + pp; }
+      }
     } else {
-      if (seg == 0) { half = 0; piece = 2 * wn + pp; }
-      else if (seg == 1) { half = 1; piece = 2 * wn + pp; }
-      else if (seg == 2) { half = 2; piece = 2 * wn + pp; }
-      else { half = 2; piece = 16 + 2 * wn + pp; }
+      if (g == 0) {
+        if (seg == 0) { half = 2; piece = 16 + 4 * wn + pp; }
+        else { half = 1; piece = 4 * wn + pp; }
+      } else {
+        if (seg == 0) { half = 0; piece = 4 * wn + pp; }
+        else { half = 2; piece = 4 * wn + pp; }
+      }
     }
     const int prow_in_half = (piece & 15) * 8 + prow;          // row inside its half
     const int gch = pch ^ ((prow_in_half >> 1) & 7);            // source chunk
@@ -130,8 +143,8 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
   auto issue = [&](int slot, int stage, int k0) {
     bf16_t* st = lds + stage * kGStage;
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const int i = 2 * slot + pp;
+    for (int pp = 0; pp < PPS; ++pp) {
+      const int i = PPS * slot + pp;
       const bf16_t* src = (src_is_w[i] ? w : xt) + src_off[i] + k0;
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(st + dst_off[i]), 16, 0, 0);
     }
@@ -163,7 +176,7 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
 #pragma unroll
     for (int j = 0; j < 2 * XS; ++j)
 #pragma unroll
-      for (int q = 0; q < MF / 2; ++q) acc[i][j][q] = 0.f;
+      for (int q = 0; q < (MF == 32 ? 16 : 4); ++q) acc[i][j][q] = 0.f;
 
   s16x8 xf[XS][KS];           // x fragments of the current m-quadrant: [subtile][k-step]
   s16x8 wf[2][WS][KS];        // w fragments: [n-quadrant][subtile][k-step]
@@ -204,6 +217,7 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
   };
 
   const int nk = K / kGK;
+  if constexpr (PH == 4) {
   // ---- prologue: tile 0 whole (every wave its 8 pieces), then the W pieces of tile 1
   // that the steady state issues in period -1 (g1: R3 and R4 slots, g0: R4 slot)
 #pragma unroll
@@ -259,6 +273,57 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
     gbar();
   }
   if (g == 0) gbar();                               // balance the stagger barrier
+  } else {
+  // ---- PH = 2: R1 = x(m0) + w(n0, n1), M1 = (n0, m0), (n1, m0); R2 = x(m1), M2 = (n*, m1).
+  // Per period t: g0 R1 issues W[16..31] of tile t+1, R2 XB of t+1; g1 R1 XA of t+1,
+  // R2 W[0..15] of t+2.  Waits: g0 end of R1 and end of M2 vmcnt(4), g1 end of R2
+  // vmcnt(4) (docs/GEMM_DENSE.md).  Prologue: tile 0 whole, then g1's period -1 slot.
+  issue(0, 0, 0);
+  issue(1, 0, 0);
+  if (nk > 1 && g == 1) {
+    issue(1, 1, kGK);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  gbar();
+  if (g == 1) gbar();                               // stagger waves 4-7 by one segment
+  for (int t = 0; t < nk; ++t) {
+    const bf16_t* cur = lds + (t & 1) * kGStage;
+    const int nxt = (t + 1) & 1;
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    const bool steady = has2;
+    const int k1 = (t + 1) * kGK, k2 = (t + 2) * kGK;
+    read_x(cur, 0);                                 // R1
+    read_w(cur, 0);
+    read_w(cur, 1);
+    if (has1) issue(0, nxt, k1);
+    if (g == 0) {
+      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gbar();
+    mma(0, 0);                                      // M1
+    mma(1, 0);
+    gbar();
+    read_x(cur, 1);                                 // R2
+    if (g == 0) { if (has1) issue(1, nxt, k1); }
+    else {
+      if (has2) issue(1, t & 1, k2);
+      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gbar();
+    mma(1, 1);                                      // M2 (n1 first: w(n1) is the newest)
+    mma(0, 1);
+    if (g == 0) {
+      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gbar();
+  }
+  if (g == 0) gbar();                               // balance the stagger barrier
+  }
 
   // ---- epilogue.  C^T lane layout -- MF 32: w row (q&3) + 8(q>>2) + 4 h2 of the
   // subtile, x row r; MF 16: w row 4 (l >> 4) + q, x row l & 15.  Either way each
@@ -311,15 +376,19 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   const int tiles_m = (M + kGM - 1) / kGM;
   const int tiles_n = swiglu ? n_out / 128 : n_out / kGN;
   const int grid = tiles_m * tiles_n;
-  const int mf = (cfg & 1) ? 32 : 16;              // cfg bit 0: the 32x32x16 variant
-#define RFQ_GD_LAUNCH(E, F) \
-  gemm_dense_kernel<E, F><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off, \
-                                                   tiles_m, tiles_n)
-  if (swiglu) {
-    if (mf == 32) RFQ_GD_LAUNCH(EPI_SWIGLU, 32); else RFQ_GD_LAUNCH(EPI_SWIGLU, 16);
-  } else {
-    if (mf == 32) RFQ_GD_LAUNCH(EPI_STORE, 32); else RFQ_GD_LAUNCH(EPI_STORE, 16);
+  // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile
+#define RFQ_GD_LAUNCH(E, F, P) \
+  gemm_dense_kernel<E, F, P><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off, \
+                                                      tiles_m, tiles_n)
+#define RFQ_GD_EPI(E)                                                  \
+  switch (cfg & 3) {                                                   \
+    case 0: RFQ_GD_LAUNCH(E, 16, 4); break;                            \
+    case 1: RFQ_GD_LAUNCH(E, 32, 4); break;                            \
+    case 2: RFQ_GD_LAUNCH(E, 16, 2); break;                            \
+    default: RFQ_GD_LAUNCH(E, 32, 2); break;                           \
   }
+  if (swiglu) { RFQ_GD_EPI(EPI_SWIGLU) } else { RFQ_GD_EPI(EPI_STORE) }
+#undef RFQ_GD_EPI
 #undef RFQ_GD_LAUNCH
 }
 

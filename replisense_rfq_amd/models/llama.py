@@ -160,6 +160,13 @@ class DecoderLM:
                         continue
                     mo = ops.linear(act, lw["down"])
                 else:
+                    # throughput path: gate|up with the SwiGLU epilogue in the hand-written
+                    # large-M MFMA GEMM when the start-up plan measured it faster
+                    act = ops.swiglu_large(x, lw["gate_up"])
+                    if act is not None:
+                        mo = ops.linear(act, lw["down"])
+                        self.tp.all_reduce_add_norm_(mo, residual, nxt, eps, x)
+                        continue
                     gu = ops.linear(x, lw["gate_up"])
                     if fuse and ops.linear_add_norm(gu, lw["down"], residual, nxt, eps, x,
                                                     gated=True):

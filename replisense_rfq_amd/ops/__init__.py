@@ -21,7 +21,7 @@ __all__ = [
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
     "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
-    "gemm_dense", "gemm_dense_ok",
+    "gemm_dense", "gemm_dense_ok", "swiglu_large",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -279,6 +279,36 @@ def split_chunks(M: int, N: int, K: int) -> list[int] | None:
 _LT_BAD: set = set()        # (algo, M) pairs hipBLASLt rejected: plain matmul for those
 
 
+def _dense_cfg(M: int, N: int, K: int, swiglu: bool = False) -> int:
+    """gemm_dense cfg the start-up plan chose for this M bucket, or -1 (library)."""
+    p = _SPLIT_PLAN.get((N, K))
+    if p is None or len(p) < 5:
+        return -1
+    q, sel = p[0], p[4 if swiglu else 3]
+    j = -(-M // q)
+    if j < len(sel):
+        return sel[j]
+    return sel[-1] if len(sel) > 1 else -1        # past the tuned range: the largest bucket
+
+
+def swiglu_large(x, w):
+    """act[M, F] = silu(x Wg^T) * (x Wu^T) for large M in one hand-written MFMA GEMM with
+    the SwiGLU epilogue (gemm_dense.hip) when the start-up plan measured it faster than
+    the library GEMM + silu_mul; None otherwise (the caller runs that unfused path)."""
+    if not _gpu(x) or x.stride(1) != 1 or x.stride(0) % 8:
+        return None
+    M, K = x.shape
+    N = w.shape[0]
+    if M <= SKINNY_MAX_M:
+        return None
+    cfg = _dense_cfg(M, N, K, swiglu=True)
+    if cfg < 0:
+        return None
+    out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
+    _native.ops().gemm_dense(x, w, out, True, cfg)
+    return out
+
+
 def _lt_or_torch(x, w, out) -> None:
     """out = x w^T with the algorithm the start-up plan measured fastest for this
     M bucket (csrc/bindings/gemm_lt.cpp), else torch.matmul."""
@@ -312,6 +342,10 @@ def linear(x, w, out=None, plan: int | None = None):
         if _SPLIT_PLAN and M > SKINNY_MAX_M and (N, K) in _SPLIT_PLAN:
             if out is None:
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            dc = _dense_cfg(M, N, K)
+            if dc >= 0 and out.stride(1) == 1 and out.stride(0) % 4 == 0:
+                _native.ops().gemm_dense(x, w, out, False, dc)
+                return out
             rows = split_chunks(M, N, K) or [M]
             a = 0
             for r in rows:

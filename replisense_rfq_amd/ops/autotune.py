@@ -14,8 +14,8 @@ import os
 
 import torch
 
-from . import (_native, set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan,
-               set_split_plan, set_swiglu_plan, silu_linear, silu_mul)
+from . import (_native, gemm_dense_ok, set_linear_plan, set_norm_plan, set_rope_plan,
+               set_silu_plan, set_split_plan, set_swiglu_plan, silu_linear, silu_mul)
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -272,6 +272,10 @@ def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0
 
 
 LT_CANDIDATES = int(os.environ.get("RFQ_GEMM_LT_CANDIDATES", "6"))   # heuristic algorithms timed per (M bucket, N, K)
+# RFQ_GEMM_DENSE=0 keeps every large-M projection on hipBLASLt
+DENSE_ON = os.environ.get("RFQ_GEMM_DENSE", "1") != "0"
+DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2").split(","))
+DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 
 def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], quantum: int = 256,
@@ -310,8 +314,48 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
             times.append(t_best)
             algos.append(a_best)
         table = plan_splits(times)
-        plan[(N, K)] = (quantum, table, algos)
+        # the hand-written 256x256 MFMA GEMM (gemm_dense.hip) per bucket, against the
+        # library's best (one call or the split plan); for gate|up the comparison is
+        # GEMM + silu_mul vs the same kernel with the SwiGLU epilogue
+        dense = [-1] * (J + 1)
+        swi = [-1] * (J + 1)
+        n_dense = n_swi = 0
+        if DENSE_ON and gemm_dense_ok(quantum, N, K):
+            act = torch.empty(J * quantum, N // 2, device=w.device, dtype=w.dtype) \
+                if name == "gate_up" else None
+            for j in range(1, J + 1):
+                m = j * quantum
+                t_lib = times[j] if table[j] is None else \
+                    sum(times[c] for c in table[j]) + 4.0 * (len(table[j]) - 1)
+                best_c, t_best = -1, t_lib * DENSE_MARGIN
+                for c in DENSE_CFGS:
+                    t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, out[:m], False, c),
+                              [w], reps, graph=False)
+                    if t < t_best:
+                        best_c, t_best = c, t
+                dense[j] = best_c
+                n_dense += best_c >= 0
+                if act is not None:
+                    t_silu = _time(lambda w_, m=m: silu_mul(out[:m], act[:m]), [w], reps,
+                                   graph=False)
+                    t_ref = min(t_lib, t_best) + t_silu
+                    bs, ts = -1, t_ref * DENSE_MARGIN
+                    for c in DENSE_CFGS:
+                        t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, act[:m], True, c),
+                                  [w], reps, graph=False)
+                        if t < ts:
+                            bs, ts = c, t
+                    swi[j] = bs
+                    n_swi += bs >= 0
+                    report.append(("swiglu:" + name, m, N, K, round(t_ref, 1),
+                                   f"dense{bs}" if bs >= 0 else "lib", round(min(ts, t_ref), 1)))
+                report.append(("dense:" + name, m, N, K, round(t_lib, 1),
+                               f"dense{best_c}" if best_c >= 0 else "lib", round(t_best, 1)))
+            del act
+        plan[(N, K)] = (quantum, table, algos, dense, swi)
         report.append(("lt:" + name, J * quantum, N, K, J, f"{n_lt}/{J} buckets", 0.0))
+        report.append(("dense:" + name, J * quantum, N, K, J,
+                       f"{n_dense}/{J} buckets, swiglu {n_swi}/{J}", 0.0))
         for j, parts in enumerate(table):
             if parts is not None:
                 t_split = sum(times[c] for c in parts)
@@ -370,7 +414,7 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
         set_split_plan(xplan)
         SPLIT_REPORT[:] = xreport
         for r in xreport:
-            log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d one call %.1fus -> %s %.1fus", *r)
+            log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d lib %.1fus -> %s %.1fus", *r)
     for r in report:
         log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
                  r[0], r[1], r[2], r[3], r[4], "lib" if r[5] < 0 else f"skinny{r[5]}", r[6])

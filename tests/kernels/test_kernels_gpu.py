@@ -679,7 +679,7 @@ def test_gemv_splitk(gpu, M, cfg, N, K):
     assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 128), (256, 768, 1024),
                                    (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096)])
@@ -699,7 +699,7 @@ def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_gemm_dense_identity_asymmetric(gpu, cfg):
     """A = I with an asymmetric B catches a transposed C write (§3)."""
     K = 256

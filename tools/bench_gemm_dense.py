@@ -39,8 +39,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--check-only", action="store_true")
     ap.add_argument("--cfg", type=int, default=0, help="numerics check variant")
+    ap.add_argument("--cfgs", default="0,1,2,3", help="kernel variants timed")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "gemm_dense.md"))
     a = ap.parse_args()
+    a.cfgs = [int(c) for c in a.cfgs.split(",")]
 
     import torch
 
@@ -73,11 +75,8 @@ def main():
                 out = torch.empty_like(y)
                 gu = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if swi else None
 
-                def mine():
-                    ops.gemm_dense(x, w, out=out, swiglu=swi)
-
-                def mine32():
-                    ops.gemm_dense(x, w, out=out, swiglu=swi, cfg=1)
+                def mk(c):
+                    return lambda: ops.gemm_dense(x, w, out=out, swiglu=swi, cfg=c)
 
                 def blt():
                     if swi:
@@ -85,23 +84,28 @@ def main():
                         ops.silu_mul(gu, out)
                     else:
                         torch.matmul(x, w.t(), out=out)
-                for f in (mine, mine32, blt):
+                fns = [("cfg%d" % c, mk(c)) for c in a.cfgs] + [("blt", blt)]
+                for _, f in fns:
                     for _ in range(3):
                         f()
-                tm, tb, t32 = [], [], []
+                ts = {k: [] for k, _ in fns}
                 for _ in range(a.rounds):
-                    for f, acc in ((mine, tm), (mine32, t32), (blt, tb)):
+                    for k, f in fns:
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
                         for _ in range(a.iters):
                             f()
                         e1.record()
                         torch.cuda.synchronize()
-                        acc.append(e0.elapsed_time(e1) * 1e3 / a.iters)
+                        ts[k].append(e0.elapsed_time(e1) * 1e3 / a.iters)
+                med = {k: statistics.median(v) for k, v in ts.items()}
+                best = min((k for k in med if k != "blt"), key=lambda k: med[k])
+                tm, tb = ts[best], ts["blt"]
+                row["us"] = {k: round(v, 1) for k, v in med.items()}
+                row["best_cfg"] = best
                 flops = 2.0 * M * N * K
                 us_m, us_b = statistics.median(tm), statistics.median(tb)
                 row.update(us_mine=round(us_m, 1), us_hipblaslt=round(us_b, 1),
-                           us_mfma32=round(statistics.median(t32), 1),
                            pf_mine=round(flops / us_m / 1e9, 3),
                            pf_hipblaslt=round(flops / us_b / 1e9, 3),
                            speedup=round(us_b / us_m, 3))
@@ -110,10 +114,10 @@ def main():
     bad = [r for r in rows if not r["ok"]]
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
-        f.write("| shape | M | N | K | mine us | PF/s | hipBLASLt(+silu_mul) us | PF/s | speedup | max err |\n")
-        f.write("|---|---|---|---|---|---|---|---|---|---|\n")
+        f.write("| shape | M | N | K | best cfg | us | PF/s | hipBLASLt(+silu_mul) us | PF/s | speedup | max err |\n")
+        f.write("|---|---|---|---|---|---|---|---|---|---|---|\n")
         for r in rows:
-            f.write(f"| {r['shape']} | {r['M']} | {r['N']} | {r['K']} | {r.get('us_mine', '')} | "
+            f.write(f"| {r['shape']} | {r['M']} | {r['N']} | {r['K']} | {r.get('best_cfg', '')} | {r.get('us_mine', '')} | "
                     f"{r.get('pf_mine', '')} | {r.get('us_hipblaslt', '')} | "
                     f"{r.get('pf_hipblaslt', '')} | {r.get('speedup', '')} | "
                     f"{r['max_abs_err']:.3g} |\n")
