@@ -34,13 +34,15 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import queue
 import socket
 import statistics
 import subprocess
 import sys
 import threading
 import time
+
+from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, loaded_latency,
+                                                  single_stream as _single_stream, validate)
 
 BASELINE_P50_S = 0.883          # Groq llama3-70b p50 server time per request
 
@@ -77,6 +79,20 @@ def parse():
                          "ONE TP group over all N ranks (BASELINE config 4: 70B TP=8). "
                          "'auto' = llama3-70b on the driver's 8-GPU run of the default "
                          "8B DP bench; 'none' = off")
+    ap.add_argument("--phases", default="auto",
+                    help="extra phases after the timed window: comma list of http, mixtral, "
+                         "70b; 'auto' = all on the 1-GPU run of the 8B bench, 'none' = off")
+    ap.add_argument("--phase-budget", type=float, default=300.0,
+                    help="seconds for all extra phases together (each is bounded; a watchdog "
+                         "prints the JSON line if they overrun)")
+    ap.add_argument("--http-docs", type=int, default=512)
+    ap.add_argument("--http-clients", type=int, default=64)
+    ap.add_argument("--mixtral-model", default="mixtral-8x7b")
+    ap.add_argument("--mixtral-in-flight", type=int, default=768)
+    ap.add_argument("--mixtral-warm", type=int, default=768)
+    ap.add_argument("--mixtral-docs", type=int, default=1536)
+    ap.add_argument("--big-model", default="llama3-70b")
+    ap.add_argument("--big-latency-runs", type=int, default=5)
     ap.add_argument("--tp-latency-runs", type=int, default=7)
     ap.add_argument("--tp-docs", type=int, default=256,
                     help="TP phase: documents timed in a continuous stream (0 = skip)")
@@ -98,6 +114,18 @@ def _tp_latency_model(args, world: int) -> str | None:
     return m
 
 
+def _phase_list(args, world: int) -> list:
+    """Extra phases after the timed window (benchmarks/phases.py).  'auto': on the
+    driver's 1-GPU run of the default 8B bench, all three."""
+    v = args.phases
+    if v in ("", "none", "0"):
+        return []
+    if v == "auto":
+        return ["http", "mixtral", "70b"] if (world == 1 and args.tp == 1
+                                              and args.model == "llama3-8b") else []
+    return [p for p in v.split(",") if p]
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -114,164 +142,6 @@ def _self_launch(args) -> int:
            "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     return subprocess.call(cmd, env=env)
-
-
-class DocStream:
-    """One replica's continuous document stream over an LLMEngine.
-
-    A producer thread builds and tokenises prompts ahead of the engine (as the
-    HTTP front-end does while the engine steps); the engine loop keeps
-    ``in_flight`` documents admitted and counts completions.  ``run_until(n)``
-    steps the engine until ``n`` documents have completed in total and returns,
-    leaving the in-flight documents in place for the next call.
-    """
-
-    def __init__(self, engine, dp_rank: int, seed: int, in_flight: int):
-        from replisense_rfq_amd.service.extract import build_messages
-        from replisense_rfq_amd.service.prompt import register_prompt_prefix
-        from replisense_rfq_amd.utils import synth
-
-        self.engine = engine
-        self.tok = engine.tokenizer
-        register_prompt_prefix(self.tok)         # what the service's EngineBackend does
-        self.in_flight = in_flight
-        self.base = (seed * 7919 + dp_rank) * 1_000_003
-        self.ready: queue.Queue = queue.Queue(maxsize=max(64, in_flight))
-        self.stop = threading.Event()
-        self.live = 0
-        self.completed = 0
-        self.finished = []                       # sequences completed in the current window
-        self._build, self._synth = build_messages, synth
-        self.thread = threading.Thread(target=self._produce, name="bench-tokenize", daemon=True)
-        self.thread.start()
-
-    def _produce(self):
-        i = 0
-        while not self.stop.is_set():
-            d = self._synth.make_rfq(self.base + i)
-            ids = self.tok.chat_ids(self._build(d.text))
-            params = self.engine.default_params(seed=(self.base + i) & 0xFFFFFF,
-                                                **self._synth.decode_hints(d))
-            while not self.stop.is_set():
-                try:
-                    self.ready.put((ids, params), timeout=0.1)
-                    break
-                except queue.Full:
-                    continue
-            i += 1
-
-    def _top_up(self, block: bool):
-        eng = self.engine
-        while self.live < self.in_flight:
-            try:
-                ids, params = self.ready.get(block=block and not eng.has_work(), timeout=1.0)
-            except queue.Empty:
-                return
-            eng.add_request(ids, params)
-            self.live += 1
-
-    def run_until(self, target: int):
-        eng = self.engine
-        while self.completed < target:
-            self._top_up(block=True)
-            if not eng.has_work():
-                continue
-            done = eng.step()
-            self.live -= len(done)
-            self.completed += len(done)
-            self.finished.extend(done)
-
-    def close(self):
-        self.stop.set()
-        try:
-            while True:
-                self.ready.get_nowait()
-        except queue.Empty:
-            pass
-        self.thread.join(timeout=10)
-        if self.engine.has_work():
-            self.engine.abort_all("abort")
-        self.live = 0
-
-
-def validate(engine, seqs) -> dict:
-    """Post-process the window's completions like the service does and report the
-    per-document token shape."""
-    from replisense_rfq_amd.service.extract import parse_and_validate_response
-
-    n = max(1, len(seqs))
-    ok = 0
-    for s in seqs:
-        out = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
-        ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
-    return dict(
-        prompt_tokens=sum(s.prompt_len for s in seqs) / n,
-        completion_tokens=sum(s.num_generated for s in seqs) / n,
-        sampled_tokens=sum(s.num_sampled for s in seqs) / n,
-        prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n,
-        valid=ok / n)
-
-
-def _pcts(vals) -> dict | None:
-    """p50 / p90 / p99 / max / mean of a list of seconds (nearest-rank percentiles)."""
-    if not vals:
-        return None
-    v = sorted(vals)
-
-    def q(p):
-        return v[min(len(v) - 1, max(0, int(round(p / 100.0 * len(v) + 0.5)) - 1))]
-    return {"p50": round(q(50), 3), "p90": round(q(90), 3), "p99": round(q(99), 3),
-            "max": round(v[-1], 3), "mean": round(sum(v) / len(v), 3), "n": len(v)}
-
-
-def loaded_latency(seqs) -> dict:
-    """Latency under load of the documents that completed inside a timed window:
-    submission to the engine -> last token (``e2e``) and -> first sampled token
-    (``ttft``), the server-side time a closed-loop client with this many requests
-    in flight waits per document (the reference's only metric is per-request
-    server time, /root/reference/app/rfq_agent.py:158-168; its LLM call times out
-    at 30 s, rfq_agent.py:69)."""
-    e2e = [s.t_finish - s.t_arrival for s in seqs if s.t_finish and s.t_arrival]
-    ttft = [s.t_first_token - s.t_arrival for s in seqs if s.t_first_token and s.t_arrival]
-    return {"e2e_s": _pcts(e2e), "ttft_s": _pcts(ttft)}
-
-
-def latency(engine, dp_rank: int, runs: int):
-    """Single-request end-to-end latency of the extraction path (idle engine)."""
-    from replisense_rfq_amd.service.extract import build_messages, parse_and_validate_response
-    from replisense_rfq_amd.utils import synth
-
-    out, detail = [], []
-    tok = engine.tokenizer
-    for i in range(runs):
-        d = synth.make_rfq(10_000_000 + dp_rank * 1000 + i)
-        t0 = time.perf_counter()
-        ids = tok.chat_ids(build_messages(d.text))
-        s, = engine.generate([ids], engine.default_params(**synth.decode_hints(d)))
-        r = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
-        out.append(time.perf_counter() - t0)
-        ok = bool(r.get("success")) and "validation warnings" not in r.get("message", "")
-        detail.append((s.num_generated, s.num_sampled, s.span().get("ttft_ms") or 0.0, out[-1],
-                       ok))
-    return out, detail
-
-
-def _single_stream(detail):
-    """Single-request decode rates (Groq 350 tok/s per stream): output
-    tokens/s after the first token, and the sampled (non-jump-forward) step rate."""
-    if not detail:
-        return None
-    rates, steps, ttft = [], [], []
-    for gen, sampled, ttft_ms, total, _ in detail:
-        dec = max(total - ttft_ms / 1e3, 1e-6)
-        rates.append(gen / dec)
-        steps.append(sampled / dec)
-        ttft.append(ttft_ms)
-    return {"completion_tok_s_p50": round(statistics.median(rates), 1),
-            "sampled_steps_per_s_p50": round(statistics.median(steps), 1),
-            "ttft_ms_p50": round(statistics.median(ttft), 1),
-            "baseline_decode_tok_s": 350.0,
-            "valid": round(sum(d[4] for d in detail) / len(detail), 3)}
 
 
 def _gemm_plan_summary() -> dict:
@@ -546,6 +416,57 @@ def main():
         }
 
     emitter = _Emitter()
+    phases = _phase_list(args, world)
+    if phases:
+        # BASELINE configs 3 and 5 and the reference's own model, driver-clocked in the
+        # same JSON line (world == 1: every rank is rank 0)
+        from replisense_rfq_amd.benchmarks import phases as ph
+
+        out["phases"] = {}
+        t_ph = time.perf_counter()
+
+        def left():
+            return args.phase_budget - (time.perf_counter() - t_ph)
+
+        def on_overrun():
+            out["phases"]["status"] = f"timeout after {args.phase_budget:.0f} s"
+            out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)
+            emitter.emit(out)
+            os._exit(0)
+
+        guard = threading.Timer(args.phase_budget + 120.0, on_overrun)
+        guard.daemon = True
+        guard.start()
+        if "http" in phases:
+            mark("phase:http")
+            out["phases"]["http_upload"] = ph.http_upload_phase(
+                engine, n_docs=args.http_docs, clients=args.http_clients,
+                budget_s=min(120.0, left()), seed=args.seed)
+        import gc
+
+        if hb is not None:
+            hb.stream = None
+        del stream, engine
+        gc.collect()
+        if on_gpu:
+            torch.cuda.empty_cache()
+        if "mixtral" in phases and left() > 60:
+            mark("phase:mixtral")
+            out["phases"]["mixtral"] = ph.model_phase(
+                args.mixtral_model, seed=args.seed, in_flight=args.mixtral_in_flight,
+                warm_docs=args.mixtral_warm, docs=args.mixtral_docs, formats=("pdf", "xlsx"),
+                budget_s=min(160.0, left() - 60 if "70b" in phases else left()),
+                max_batched_tokens=args.prefill_chunk)
+        if "70b" in phases and left() > 30:
+            mark("phase:70b")
+            out["phases"]["llama3_70b"] = ph.model_phase(
+                args.big_model, seed=args.seed, latency_runs=args.big_latency_runs,
+                budget_s=left(), in_flight=8)
+        guard.cancel()
+        out["phases"]["phase_s"] = round(time.perf_counter() - t_ph, 1)
+        out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)
+        emitter.emit(out)
+        return
     tpl = _tp_latency_model(args, world)
     if tpl is not None:
         # free the DP replica (weights, KV pool, graph pools) before the TP group loads

@@ -56,7 +56,7 @@ __device__ __forceinline__ void gbar() {
   asm volatile("" ::: "memory");
 }
 
-template <int EPI, int MF, int PH>
+template <int EPI, int MF, int PH, int ABL = 0>
 __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
     bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off, int tiles_m, int tiles_n) {
@@ -215,6 +215,19 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
         }
     __builtin_amdgcn_s_setprio(0);
   };
+  // (diagnostic ablations only: keep the fragments live without reading LDS)
+  auto opaque_frags = [&]() {
+#pragma unroll
+    for (int j = 0; j < XS; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(xf[j][ks]));
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < WS; ++i)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(wf[n][i][ks]));
+  };
 
   const int nk = K / kGK;
   if constexpr (PH == 4) {
@@ -294,30 +307,35 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
     const bool steady = has2;
     const int k1 = (t + 1) * kGK, k2 = (t + 2) * kGK;
-    read_x(cur, 0);                                 // R1
-    read_w(cur, 0);
-    read_w(cur, 1);
-    if (has1) issue(0, nxt, k1);
+    if constexpr (!(ABL & 4)) {                     // R1
+      read_x(cur, 0);
+      read_w(cur, 0);
+      read_w(cur, 1);
+    } else {
+      opaque_frags();
+    }
+    if (has1 && !(ABL & 2)) issue(0, nxt, k1);
     if (g == 0) {
-      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (steady) { if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     gbar();
     mma(0, 0);                                      // M1
     mma(1, 0);
     gbar();
-    read_x(cur, 1);                                 // R2
-    if (g == 0) { if (has1) issue(1, nxt, k1); }
+    if constexpr (!(ABL & 4)) read_x(cur, 1);       // R2
+    else opaque_frags();
+    if (g == 0) { if (has1 && !(ABL & 2)) issue(1, nxt, k1); }
     else {
-      if (has2) issue(1, t & 1, k2);
-      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (has2 && !(ABL & 2)) issue(1, t & 1, k2);
+      if (steady) { if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     gbar();
     mma(1, 1);                                      // M2 (n1 first: w(n1) is the newest)
     mma(0, 1);
     if (g == 0) {
-      if (steady) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (steady) { if constexpr (!(ABL & 1)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     gbar();
@@ -386,6 +404,23 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
     case 1: RFQ_GD_LAUNCH(E, 32, 4); break;                            \
     case 2: RFQ_GD_LAUNCH(E, 16, 2); break;                            \
     default: RFQ_GD_LAUNCH(E, 32, 2); break;                           \
+  }
+  // cfg bits 4-6 (diagnostic timing builds, WRONG results): 16 = no counted vmcnt
+  // waits, 32 = no DMA in the loop, 64 = no fragment reads (16x16x32, 2 phases only)
+  const int abl = (cfg >> 4) & 7;
+  if (abl && !swiglu) {
+#define RFQ_GD_ABL(A) \
+    gemm_dense_kernel<EPI_STORE, 16, 2, A><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, \
+                                                                  K, up_off, tiles_m, tiles_n)
+    switch (abl) {
+      case 1: RFQ_GD_ABL(1); break;
+      case 2: RFQ_GD_ABL(2); break;
+      case 3: RFQ_GD_ABL(3); break;
+      case 4: RFQ_GD_ABL(4); break;
+      default: RFQ_GD_ABL(6); break;
+    }
+#undef RFQ_GD_ABL
+    return;
   }
   if (swiglu) { RFQ_GD_EPI(EPI_SWIGLU) } else { RFQ_GD_EPI(EPI_STORE) }
 #undef RFQ_GD_EPI

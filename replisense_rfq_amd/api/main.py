@@ -59,6 +59,14 @@ TEMP_DIR.mkdir(exist_ok=True)
 parser: Optional[FileParser] = None
 field_generator: Optional[ExtractService] = None
 _engine_handles: dict = {}
+# An ExtractService built by the embedding process (bench.py's in-process HTTP phase
+# serves the engine it already owns); the lifespan then builds no backend of its own.
+_provided_generator: Optional[ExtractService] = None
+
+
+def provide_generator(svc: Optional[ExtractService]) -> None:
+    global _provided_generator
+    _provided_generator = svc
 
 
 def build_generator() -> ExtractService:
@@ -114,7 +122,7 @@ async def lifespan(app: FastAPI):
     try:
         parser = FileParser(max_file_size_mb=MAX_FILE_SIZE_MB,
                             processes=int(os.getenv("RFQ_PARSER_PROCS", "0")))
-        field_generator = build_generator()
+        field_generator = _provided_generator or build_generator()
         logger.info("Services initialized successfully")
     except Exception as e:
         logger.error("Failed to initialize services: %s", e)

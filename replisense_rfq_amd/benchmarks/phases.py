@@ -1,0 +1,243 @@
+"""Extra measured phases of the driver's 1-GPU bench run (bench.py), after the timed
+Llama-3-8B docs/s window, so BASELINE.json's other configs get driver-clocked
+numbers in the same JSON line:
+
+  http      config 3: the FastAPI service (api/main.py, the reference's
+            app/main.py:205-288 contract) served in-process over real sockets by
+            uvicorn, on the 8B engine the bench already built; ``clients``
+            closed-loop HTTP clients (spawned processes) POST /upload/ with
+            generated PDF / XLSX / DOCX attachments -> multipart parse -> CPU
+            parser pool -> engine -> JSON recovery/validation -> envelope.
+  mixtral   config 5: Mixtral-8x7B (MoE grouped GEMMs, JSON-schema-constrained
+            decode) over a mixed PDF / XLSX stream parsed by the service parser:
+            docs/s and the latency under load of the timed window.
+  70b       the reference's own model (llama3-70b-8192, rfq_agent.py:62) at TP=1
+            on one MI355X: idle single-request p50 and decode rates.
+
+Every phase is bounded by a wall-clock budget: it reports what it measured so far
+with ``status`` set, and a model phase frees its engine before the next starts.
+"""
+from __future__ import annotations
+
+import gc
+import os
+import statistics
+import threading
+import time
+
+from .stream import (DocStream, latency, loaded_latency, pcts, single_stream, validate)
+
+BASELINE_P50_S = 0.883            # Groq llama3-70b p50 server time per request
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# ------------------------------------------------------------------ HTTP clients
+async def _client_loop(url: str, docs: list, clients: int, deadline: float):
+    import asyncio
+
+    import aiohttp
+
+    q: asyncio.Queue = asyncio.Queue()
+    for d in docs:
+        q.put_nowait(d)
+    lat, ok, bad = [], 0, 0
+
+    async def worker(sess):
+        nonlocal ok, bad
+        while time.time() < deadline:
+            try:
+                name, blob = q.get_nowait()
+            except asyncio.QueueEmpty:
+                return
+            form = aiohttp.FormData()
+            form.add_field("file", blob, filename=name)
+            t0 = time.perf_counter()
+            try:
+                async with sess.post(url + "/upload/", data=form) as r:
+                    status, body = r.status, await r.json()
+            except (aiohttp.ClientError, asyncio.TimeoutError):
+                status, body = 0, {}
+            lat.append(time.perf_counter() - t0)
+            data = body.get("data", {}) if status == 200 else {}
+            if data.get("success") and "validation warnings" not in data.get("message", ""):
+                ok += 1
+            else:
+                bad += 1
+
+    conn = aiohttp.TCPConnector(limit=clients, limit_per_host=clients)
+    async with aiohttp.ClientSession(connector=conn,
+                                     timeout=aiohttp.ClientTimeout(total=120)) as sess:
+        await asyncio.gather(*(worker(sess) for _ in range(clients)))
+    return lat, ok, bad
+
+
+def _client_proc(url, docs, clients, deadline, start_evt, out_q):
+    import asyncio
+
+    start_evt.wait()
+    out_q.put(asyncio.run(_client_loop(url, docs, clients, deadline)))
+
+
+def http_upload_phase(engine, n_docs: int = 512, clients: int = 64, client_procs: int = 4,
+                      parse_procs: int = 4, budget_s: float = 90.0, seed: int = 0) -> dict:
+    """BASELINE config 3 over real HTTP on the already-built engine."""
+    import multiprocessing as mp
+
+    import uvicorn
+
+    from ..api import main as api
+    from ..engine.engine import AsyncEngine
+    from ..service.extract import EngineBackend, ExtractService
+    from ..utils import docgen, synth
+
+    t_start = time.perf_counter()
+    res = {"config": "POST /upload/ mixed pdf/xlsx/docx, closed loop", "clients": clients,
+           "status": "running"}
+    import logging
+
+    pkg_log = logging.getLogger("replisense_rfq_amd")
+    level0 = pkg_log.level
+    pkg_log.setLevel(logging.WARNING)       # per-request INFO lines would load the server loop
+    hints0 = engine.cfg.decode_hints
+    engine.cfg.decode_hints = True          # random-init weights: the bench decode profile
+    aeng = AsyncEngine(engine)
+    api.provide_generator(ExtractService(EngineBackend(engine, aeng)))
+    os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
+    port = _free_port()
+    server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
+                                           log_level="warning", access_log=False))
+    th = threading.Thread(target=server.run, name="bench-uvicorn", daemon=True)
+    th.start()
+    procs = []
+    try:
+        t0 = time.time()
+        while not server.started and time.time() - t0 < 60 and th.is_alive():
+            time.sleep(0.05)
+        if not server.started:
+            raise RuntimeError("uvicorn did not start")
+        fmts = ("pdf", "xlsx", "docx")
+        base = 40_000_000 + seed * 100_000
+        docs = [(f"rfq_{i}.{fmts[i % 3]}",
+                 docgen.rfq_attachment(synth.make_rfq(base + i), fmts[i % 3]))
+                for i in range(n_docs + clients)]
+        url = f"http://127.0.0.1:{port}"
+        ctx = mp.get_context("spawn")
+        client_procs = max(1, min(client_procs, clients))
+        # warm-up: the parser pool spawns its workers, every client connects once
+        warm, docs = docs[:clients], docs[clients:]
+        deadline = time.time() + max(10.0, budget_s - (time.perf_counter() - t_start))
+        for phase_docs, measure in ((warm, False), (docs, True)):
+            start_evt, out_q = ctx.Event(), ctx.Queue()
+            procs = [ctx.Process(target=_client_proc,
+                                 args=(url, phase_docs[i::client_procs],
+                                       clients // client_procs + (i < clients % client_procs),
+                                       deadline, start_evt, out_q), daemon=True)
+                     for i in range(client_procs)]
+            for p in procs:
+                p.start()
+            time.sleep(2.0)                   # let the client processes import aiohttp
+            t1 = time.perf_counter()
+            start_evt.set()
+            outs = [out_q.get(timeout=max(5.0, deadline - time.time() + 30)) for _ in procs]
+            dt = time.perf_counter() - t1
+            for p in procs:
+                p.join(timeout=10)
+            if measure:
+                lat = [x for o in outs for x in o[0]]
+                ok, bad = sum(o[1] for o in outs), sum(o[2] for o in outs)
+                res.update(docs=len(lat), docs_per_s=round(len(lat) / dt, 3),
+                           http_latency_s=pcts(lat), valid=round(ok / max(1, ok + bad), 3),
+                           seconds=round(dt, 1))
+        res["status"] = "ok" if res.get("docs") == n_docs else "timeout"
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        server.should_exit = True
+        th.join(timeout=15)
+        aeng.shutdown()
+        api.provide_generator(None)
+        engine.cfg.decode_hints = hints0
+        pkg_log.setLevel(level0)
+        if engine.has_work():
+            engine.abort_all("abort")
+    res["phase_s"] = round(time.perf_counter() - t_start, 1)
+    return res
+
+
+# --------------------------------------------------------------- model phases
+def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 0,
+                docs: int = 0, latency_runs: int = 0, formats: tuple | None = None,
+                budget_s: float = 120.0, parse_procs: int = 4, **cfg_over) -> dict:
+    """Build ``model`` on this GPU, then (a) ``latency_runs`` idle single requests and
+    (b) a closed-loop stream of ``docs`` documents at ``in_flight`` after
+    ``warm_docs`` of warm-up; free everything before returning."""
+    import torch
+
+    from ..engine.engine import LLMEngine
+    from ..utils.config import EngineConfig
+
+    t_start = time.perf_counter()
+    deadline = t_start + budget_s
+    res = {"model": model, "parallelism": "tp1", "status": "running"}
+    eng = stream = None
+    try:
+        nseq = max(8, in_flight)
+        cfg = EngineConfig.from_env(model=model, seed=seed, max_num_seqs=nseq, **cfg_over)
+        eng = LLMEngine(cfg)
+        res["init_s"] = round(time.perf_counter() - t_start, 1)
+        if latency_runs:
+            lat, detail = latency(eng, 0, latency_runs)
+            res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
+            res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
+            res["single_stream"] = single_stream(detail)
+            res["runs"] = len(lat)
+        if docs and time.perf_counter() < deadline:
+            stream = DocStream(eng, 0, seed + 1, in_flight, formats=formats,
+                               parse_procs=parse_procs)
+            on_gpu = eng.device.type == "cuda"
+            if stream.run_until(warm_docs, deadline):
+                stream.finished.clear()
+                if on_gpu:
+                    torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                done = stream.run_until(warm_docs + docs, deadline)
+                if on_gpu:
+                    torch.cuda.synchronize()
+                dt = time.perf_counter() - t1
+                n = len(stream.finished)
+                res.update(docs=n, in_flight=in_flight, docs_per_s=round(n / dt, 3),
+                           seconds=round(dt, 1),
+                           loaded_latency_s=loaded_latency(stream.finished)["e2e_s"],
+                           formats=list(formats) if formats else None,
+                           per_doc={k: round(v, 2) for k, v in
+                                    validate(eng, stream.finished[:1024]).items()})
+                if not done:
+                    res["status"] = "timeout"
+            else:
+                res["status"] = "timeout"
+        if res["status"] == "running":
+            res["status"] = "ok"
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"
+    finally:
+        if stream is not None:
+            stream.close()
+        del stream, eng
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    res["phase_s"] = round(time.perf_counter() - t_start, 1)
+    return res

@@ -172,3 +172,41 @@ def test_bench_driver_flags_time_budget():
     assert out["latency_slo_s"] == 30.0 and isinstance(out["slo_met_p99"], bool)
     assert out["config"]["profile"] == "synthetic" and out["config"]["in_flight_per_replica"] == 4
     assert out["vs_baseline"] is None
+
+
+def test_bench_extra_phases_cpu():
+    """after the timed window the 1-GPU run serves BASELINE config 3
+    over real HTTP (/upload/ of generated pdf/xlsx/docx through uvicorn), config 5
+    (the MoE model over a parsed pdf/xlsx stream) and the 70B-architecture latency
+    phase, all in the same JSON line (tiny models of the same architectures here)."""
+    out = _run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
+                "--latency-runs", "1", "--phases", "http,mixtral,70b", "--http-docs", "6",
+                "--http-clients", "3", "--mixtral-model", "tiny-mixtral",
+                "--mixtral-in-flight", "4", "--mixtral-warm", "2", "--mixtral-docs", "4",
+                "--big-model", "tiny-llama70", "--big-latency-runs", "1"], timeout=800)
+    ph = out["phases"]
+    h = ph["http_upload"]
+    assert h["status"] == "ok" and h["docs"] == 6 and h["valid"] == 1.0, h
+    assert h["docs_per_s"] > 0 and h["http_latency_s"]["n"] == 6
+    m = ph["mixtral"]
+    assert m["status"] == "ok" and m["model"] == "tiny-mixtral", m
+    assert m["docs"] >= 4 and m["formats"] == ["pdf", "xlsx"] and m["per_doc"]["valid"] == 1.0
+    assert m["loaded_latency_s"]["p50"] > 0
+    b = ph["llama3_70b"]
+    assert b["status"] == "ok" and b["runs"] == 1 and b["p50_parse_text_latency_s"] > 0, b
+    assert out["value"] > 0 and out["steps"] == 1
+
+
+def test_bench_phases_auto_only_on_one_gpu_8b():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class A:
+        phases, tp, model = "auto", 1, "llama3-8b"
+    assert bench._phase_list(A, 1) == ["http", "mixtral", "70b"]
+    assert bench._phase_list(A, 8) == [] and bench._phase_list(A, 2) == []
+    A.model = "tiny-llama"
+    assert bench._phase_list(A, 1) == []
+    A.phases = "none"
+    assert bench._phase_list(A, 1) == []

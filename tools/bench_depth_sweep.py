@@ -36,7 +36,7 @@ def main():
 
     import torch
 
-    import bench
+    from replisense_rfq_amd.benchmarks import stream as bench
     from replisense_rfq_amd.engine.engine import LLMEngine
     from replisense_rfq_amd.utils.config import EngineConfig
 
