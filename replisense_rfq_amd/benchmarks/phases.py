@@ -168,6 +168,10 @@ def http_upload_phase(engine, n_docs: int = 512, clients: int = 64, client_procs
         th.join(timeout=15)
         aeng.shutdown()
         api.provide_generator(None)
+        # the lifespan's module globals would keep the engine (and its HBM) alive
+        if api.parser is not None:
+            api.parser.close()
+        api.parser = api.field_generator = None
         engine.cfg.decode_hints = hints0
         pkg_log.setLevel(level0)
         if engine.has_work():
@@ -194,6 +198,8 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
     eng = stream = None
     try:
         nseq = max(8, in_flight)
+        if torch.cuda.is_available():
+            res["free_hbm_gb_at_start"] = round(torch.cuda.mem_get_info()[0] / 2**30, 1)
         cfg = EngineConfig.from_env(model=model, seed=seed, max_num_seqs=nseq, **cfg_over)
         eng = LLMEngine(cfg)
         res["init_s"] = round(time.perf_counter() - t_start, 1)

@@ -210,3 +210,24 @@ def test_bench_phases_auto_only_on_one_gpu_8b():
     assert bench._phase_list(A, 1) == []
     A.phases = "none"
     assert bench._phase_list(A, 1) == []
+
+
+def test_http_phase_releases_the_engine():
+    """The 1-GPU run frees the 8B engine after the HTTP phase before it builds Mixtral
+    (an engine kept alive by the API's module globals ran the next phase out of HBM)."""
+    import gc
+    import weakref
+
+    sys.path.insert(0, ROOT)
+    from replisense_rfq_amd.benchmarks.phases import http_upload_phase
+    from replisense_rfq_amd.engine.engine import LLMEngine
+    from replisense_rfq_amd.utils.config import EngineConfig
+
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4))
+    res = http_upload_phase(eng, n_docs=2, clients=2, client_procs=1, parse_procs=1,
+                            budget_s=120)
+    assert res["status"] == "ok", res
+    wr = weakref.ref(eng)
+    del eng
+    gc.collect()
+    assert wr() is None, [type(r).__name__ for r in gc.get_referrers(wr())]
