@@ -152,6 +152,49 @@ class TPContext:
 SINGLE = TPContext()
 
 
+class EmulatedTP(TPContext):
+    """One rank of a TP group, alone on one GPU, with every collective a local no-op.
+
+    Builds the rank's exact shard (column / row / vocab-parallel weight shapes, local
+    heads, KV heads and FFN columns) so one GPU can time what one rank of the real
+    group computes per step -- the evidence for BASELINE config 4 (Llama-3-70B TP=8)
+    on a single MI355X (tools/tp8_rank_emulation.py).  The all-reduce epilogue keeps
+    its local work (residual add + RMSNorm); the all-reduce itself, whose xGMI cost
+    is priced separately, is skipped, and the sampler's partial all-gather copies this
+    rank's partials into every slot."""
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def all_reduce_add_norm_(self, t, residual, w, eps, out):
+        from .. import ops
+
+        return ops.fused_add_rms_norm(t, residual, w, eps, out=out)
+
+    def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
+        self.car_status = "emulated (collectives skipped)"
+        return False
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        out.copy_(inp.unsqueeze(0).expand_as(out))
+        return out
+
+    def reduce_scatter_rows(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        n = out.shape[0]
+        out.copy_(inp[self.rank * n:(self.rank + 1) * n])
+        return out
+
+    def all_gather_rows(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        out.copy_(inp.repeat(self.world, 1))
+        return out
+
+    def broadcast_obj(self, obj, src: int = 0):
+        return obj
+
+    def barrier(self):
+        return None
+
+
 def init_distributed(backend: str | None = None, timeout_s: float = 600.0) -> TPContext:
     """Initialise the default process group from torchrun env vars (RANK/WORLD_SIZE/...).
 
