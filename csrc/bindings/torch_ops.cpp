@@ -70,6 +70,7 @@ hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 uint32_t car_read_error(const void*);
+uint32_t car_read_info(const void*);
 int car_norm_max_rows();
 void launch_car_oneshot_add_norm(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
                                  const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
@@ -589,6 +590,10 @@ void car_ipc_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<vo
 
 int64_t car_data_offset() { return rfq::car_signal_bytes(); }
 
+int64_t car_error_info(int64_t ptr) {
+  return (int64_t)rfq::car_read_info(reinterpret_cast<const void*>(ptr));
+}
+
 int64_t car_error(int64_t ptr) {
   return (int64_t)rfq::car_read_error(reinterpret_cast<const void*>(ptr));
 }
@@ -766,6 +771,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
   m.def("car_data_offset() -> int", &car_data_offset);
   m.def("car_error(int ptr) -> int", &car_error);
+  m.def("car_error_info(int ptr) -> int", &car_error_info);
   m.def("moe_skinny(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) out, bool gated, bool gather, int max_rows) -> ()");
   m.def("embed(Tensor ids, Tensor table, Tensor(a!) out, int vocab_start) -> ()");

@@ -39,7 +39,8 @@ struct CarSignal {
   uint32_t end[kCarMaxBlocks][kCarMaxRanks];
   uint32_t counter[kCarMaxBlocks];
   uint32_t error;
-  uint32_t pad[63];
+  uint32_t info;             // first timeout: 0x80000000 | phase << 24 | block << 8 | peer
+  uint32_t pad[62];
 };
 
 constexpr int64_t kCarDataOffset = (sizeof(CarSignal) + 4095) / 4096 * 4096;
@@ -52,12 +53,25 @@ __device__ __forceinline__ void car_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ bool car_wait(uint32_t* p, uint32_t v) {
-  for (int it = 0; it < (1 << 22); ++it) {
+// Spins are bounded in wall time (the 100 MHz s_memrealtime clock), not in
+// iterations: a peer whose queue the hardware scheduler has not mapped yet (more GPU
+// processes than concurrent process slots, e.g. 8 ranks + a launcher sharing one
+// device) is waited for the same 2 s however slow each poll is.  A timeout records
+// the first failing (phase, block, peer) in `info` for the host's diagnostics.
+constexpr uint64_t kCarSpinTicks = 200000000ull;           // 2 s at 100 MHz
+enum : uint32_t { kCarStart = 1, kCarMid = 2, kCarEnd = 3 };
+
+__device__ __forceinline__ bool car_wait(CarSignal* self, uint32_t* p, uint32_t v,
+                                         uint32_t phase, int b, int peer) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
     if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == v) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kCarSpinTicks) {
+      atomicCAS(&self->info, 0u, 0x80000000u | (phase << 24) | ((uint32_t)b << 8) | (uint32_t)peer);
+      return false;
+    }
     __builtin_amdgcn_s_sleep(2);
   }
-  return false;
 }
 
 __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
@@ -85,7 +99,7 @@ __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->start[b][rank], c);
-    if (!car_wait(&self->start[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
   // 4. reduce slice b
@@ -103,7 +117,7 @@ __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->end[b][rank], c);
-    if (!car_wait(&self->end[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   __syncthreads();
   if (tid == 0) {
@@ -153,7 +167,7 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->start[b][rank], c);
-    if (!car_wait(&self->start[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
   // 2. reduce-scatter: own slice, summed over every rank's staged copy
@@ -175,7 +189,7 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->mid[b][rank], c);
-    if (!car_wait(&self->mid[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->mid[b][tid], c, kCarMid, b, tid)) fail_s = 1;
   }
   __syncthreads();
   // 3. all-gather the reduced slices
@@ -190,7 +204,7 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->end[b][rank], c);
-    if (!car_wait(&self->end[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   __syncthreads();
   if (tid == 0) {
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->start[b][rank], c);
-    if (!car_wait(&self->start[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
   // 2. sum row b over the ranks (rank order, fp32, rounded to bf16 = the all-reduce
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
     car_store(&peer->end[b][rank], c);
-    if (!car_wait(&self->end[b][tid], c)) fail_s = 1;
+    if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   ss = block_sum(ss, scratch);        // its barriers also order the end handshake
   const float rs = rsqrtf(ss / (float)d + eps);
@@ -359,6 +373,13 @@ uint32_t car_read_error(const void* base) {
   hipMemcpy(&err, reinterpret_cast<const char*>(base) + offsetof(CarSignal, error), 4,
             hipMemcpyDeviceToHost);
   return err;
+}
+
+uint32_t car_read_info(const void* base) {
+  uint32_t info = 0;
+  hipMemcpy(&info, reinterpret_cast<const char*>(base) + offsetof(CarSignal, info), 4,
+            hipMemcpyDeviceToHost);
+  return info;
 }
 
 }  // namespace rfq

@@ -104,6 +104,15 @@ class CustomAllReduce:
     def errors(self) -> int:
         return int(_native.ops().car_error(self.ptr))
 
+    def error_info(self) -> str:
+        """The first flag timeout this region recorded: which protocol phase, block and
+        peer never answered within the kernel's 2 s bound ("" if none)."""
+        v = int(_native.ops().car_error_info(self.ptr))
+        if not v & 0x80000000:
+            return ""
+        phase = {1: "start", 2: "mid", 3: "end"}.get((v >> 24) & 0x7F, "?")
+        return f"{phase} flag of peer {v & 0xFF} at block {(v >> 8) & 0xFFFF} timed out"
+
     def close(self) -> None:
         ops = _native.ops()
         for p in self._opened:

@@ -96,7 +96,7 @@ class TPContext:
                 if not bool((r.float() == want).all().item()):
                     why.append("add-norm residual")
             if car.errors():
-                why.append(f"{car.errors()} flag timeouts")
+                why.append(f"{car.errors()} flag timeouts ({car.error_info()})")
         except RuntimeError as e:
             why.append(f"{type(e).__name__}: {str(e)[:120]}")
         if not everyone(not why):
