@@ -65,6 +65,8 @@ void launch_moe_combine(const bf16_t*, const int32_t*, const float*, int, int, i
                         int64_t, hipStream_t);
 void launch_gemm_dense(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int, int,
                        int, int, bool, int, hipStream_t);
+void launch_gemm_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
+                         int, int64_t, bool, hipStream_t);
 int64_t car_signal_bytes();
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -732,6 +734,27 @@ void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu
                          (int)n_out, (int)K, (int)n_out, swiglu, (int)cfg, cur_stream());
 }
 
+// Grouped MoE GEMM on the dense kernel's structure (gemm_dense.hip GROUPED): x = the
+// expert-sorted rows padded to 128 per expert, w [E, N, K], expert_offsets [E+1] (device).
+void moe_gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out,
+                    const Tensor& expert_offsets, bool swiglu) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_I32(expert_offsets);
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && out.is_contiguous(), "contiguous");
+  TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
+  const int E = w.size(0), N = w.size(1), K = w.size(2);
+  const int n_out = swiglu ? N / 2 : N;
+  TORCH_CHECK(x.size(1) == K && out.size(1) == n_out && out.size(0) == x.size(0),
+              "moe_gemm_dense shape");
+  TORCH_CHECK(K % 64 == 0 && (swiglu ? n_out % 128 == 0 : N % 256 == 0),
+              "moe_gemm_dense: K % 64, N % 256 (F % 128 with swiglu)");
+  TORCH_CHECK(x.size(0) % 128 == 0, "moe_gemm_dense: rows must be padded to 128");
+  TORCH_CHECK(expert_offsets.numel() >= E + 1, "expert_offsets too short");
+  TORCH_CHECK((int64_t)x.size(0) * K < (int64_t)INT32_MAX && (int64_t)N * K < (int64_t)INT32_MAX,
+              "moe_gemm_dense: offsets exceed int32");
+  rfq::launch_gemm_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
+                           x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
+}
+
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
 void moe_combine(const Tensor& y, const Tensor& inv_pos, const Tensor& weights, int64_t topk,
                  const Tensor& out) {
@@ -804,6 +827,8 @@ TORCH_LIBRARY(rfq_amd, m) {
         "Tensor num_blocks) -> ()");
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
   m.def("gemm_dense(Tensor x, Tensor w, Tensor(a!) out, bool swiglu=False, int cfg=0) -> ()");
+  m.def("moe_gemm_dense(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_offsets, "
+        "bool swiglu) -> ()");
   m.def("moe_skinny_splitk(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) yf, int max_rows, int splits) -> ()");
   m.def("moe_combine_splitk(Tensor yf, int splits, Tensor inv_pos, Tensor weights, int topk, "
@@ -839,6 +864,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("count_nonfinite", &count_nonfinite);
   m.impl("moe_combine", &moe_combine);
   m.impl("gemm_dense", &gemm_dense);
+  m.impl("moe_gemm_dense", &moe_gemm_dense);
   m.impl("moe_skinny_splitk", &moe_skinny_splitk);
   m.impl("moe_combine_splitk", &moe_combine_splitk);
 }

@@ -56,23 +56,69 @@ __device__ __forceinline__ void gbar() {
   asm volatile("" ::: "memory");
 }
 
-template <int EPI, int MF, int PH, int ABL = 0>
+// Grouped form (GROUPED, Mixtral's routed experts): x = the
+// expert-sorted, 128-row-padded gathered rows (moe_align / moe_gather), w = [E, N, K],
+// expert_offsets[E+1] = padded row offsets.  A tile is two consecutive 128-row blocks
+// of ONE expert (the second absent when the expert has an odd block count: its rows
+// are neither loaded past the buffer nor stored); live tiles are enumerated
+// expert-major from the device-side offsets, so no host sync and a fixed grid.
+template <int EPI, int MF, int PH, int ABL = 0, bool GROUPED = false>
 __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
-    bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off, int tiles_m, int tiles_n) {
+    bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off, int tiles_m, int tiles_n,
+    const int32_t* __restrict__ expert_offsets, int E, int64_t w_estride) {
   extern __shared__ __attribute__((aligned(16))) char smem_g[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem_g);
 
   // ---- block -> (row tile, weight tile)
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
-  const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
-  const int per_group = kGroupM * tiles_n;
-  const int gid = wg / per_group, first_m = gid * kGroupM;
-  const int gm = min(tiles_m - first_m, kGroupM);
-  const int rin = wg - gid * per_group;
-  const int tm = first_m + rin % gm, tn = rin / gm;
+  int row0, tn, m_load, m_store;           // first row, w tile, rows readable / stored
+  const bf16_t* xt;
+  const bf16_t* wt = w;
+  if constexpr (GROUPED) {
+    constexpr int kB = 128;
+    int nchunks = 0;
+    for (int e = 0; e < E; ++e)
+      nchunks += ((expert_offsets[e + 1] - expert_offsets[e]) / kB + 1) >> 1;
+    const int nlive = nchunks * tiles_n;
+    const int bid = blockIdx.x;
+    if (bid >= nlive) return;                // before any barrier: the whole block leaves
+    const int q8 = nlive >> 3, r8 = nlive & 7, xg = bid & 7;
+    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    // expert-major, then weight tile, then 256-row chunk: the chunks sharing a weight
+    // tile run back to back on one XCD (the remap above) and hit its L2
+    int e = 0, p0 = 0, s0 = 0, nbe = 0, che = 0;
+    for (; e < E; ++e) {
+      s0 = expert_offsets[e] / kB;
+      nbe = expert_offsets[e + 1] / kB - s0;
+      che = (nbe + 1) >> 1;
+      if (wg < (p0 + che) * tiles_n) break;
+      p0 += che;
+    }
+    if (e >= E) return;
+    const int local = wg - p0 * tiles_n;
+    tn = local / che;
+    const int chunk = local % che;
+    row0 = (s0 + 2 * chunk) * kB;
+    const bool two = 2 * chunk + 1 < nbe;
+    m_store = two ? 256 : 128;
+    m_load = min(expert_offsets[E] - row0, 256);
+    xt = x + (int64_t)row0 * ldx;
+    wt = w + (int64_t)e * w_estride;
+  } else {
+    const int nwg = tiles_m * tiles_n;
+    const int bid = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
+    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    const int per_group = kGroupM * tiles_n;
+    const int gid = wg / per_group, first_m = gid * kGroupM;
+    const int gm = min(tiles_m - first_m, kGroupM);
+    const int rin = wg - gid * per_group;
+    const int tm = first_m + rin % gm;
+    tn = rin / gm;
+    row0 = tm * kGM;
+    m_load = m_store = min(M - row0, 256);
+    xt = x + (int64_t)row0 * ldx;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -119,9 +165,9 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const int prow_in_half = (piece & 15) * 8 + prow;          // row inside its half
     const int gch = pch ^ ((prow_in_half >> 1) & 7);            // source chunk
     if (half < 2) {
-      int row = tm * kGM + half * 128 + prow_in_half;
-      row = row < M ? row : M - 1;
-      src_off[i] = (row - tm * kGM) * (int)ldx + 8 * gch;       // from the x tile base
+      int row = half * 128 + prow_in_half;                      // inside the tile
+      row = row < m_load ? row : m_load - 1;
+      src_off[i] = row * (int)ldx + 8 * gch;                    // from the x tile base
       dst_off[i] = half * kGHalf + (piece & 15) * 512;
       src_is_w[i] = false;
     } else {
@@ -133,19 +179,18 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
       } else {
         wrow = tn * kGN + j;
       }
-      src_off[i] = wrow * (int)ldw + 8 * gch;                   // from w
+      src_off[i] = wrow * (int)ldw + 8 * gch;                   // from w (this expert's)
       dst_off[i] = (2 + (piece >> 4)) * kGHalf + (piece & 15) * 512;
       src_is_w[i] = true;
     }
   }
-  const bf16_t* xt = x + (int64_t)tm * kGM * ldx;
 
   auto issue = [&](int slot, int stage, int k0) {
     bf16_t* st = lds + stage * kGStage;
 #pragma unroll
     for (int pp = 0; pp < PPS; ++pp) {
       const int i = PPS * slot + pp;
-      const bf16_t* src = (src_is_w[i] ? w : xt) + src_off[i] + k0;
+      const bf16_t* src = (src_is_w[i] ? wt : xt) + src_off[i] + k0;
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(st + dst_off[i]), 16, 0, 0);
     }
   };
@@ -349,8 +394,9 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
   constexpr int NG = MF == 32 ? 4 : 1;             // 4-register groups per accumulator
 #pragma unroll
   for (int j = 0; j < 2 * XS; ++j) {
-    const int row = tm * kGM + g * 128 + MF * j + (MF == 32 ? r : (lane & 15));
-    if (row >= M) continue;
+    const int trow = g * 128 + MF * j + (MF == 32 ? r : (lane & 15));
+    if (trow >= m_store) continue;
+    const int row = row0 + trow;
     const int lane_col = MF == 32 ? 4 * h2 : 4 * (lane >> 4);
     if constexpr (EPI == EPI_SWIGLU) {
       bf16_t* orow = out + (int64_t)row * ldo + tn * 128 + 32 * wn + lane_col;
@@ -397,7 +443,7 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile
 #define RFQ_GD_LAUNCH(E, F, P) \
   gemm_dense_kernel<E, F, P><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off, \
-                                                      tiles_m, tiles_n)
+                                                      tiles_m, tiles_n, nullptr, 0, 0)
 #define RFQ_GD_EPI(E)                                                  \
   switch (cfg & 3) {                                                   \
     case 0: RFQ_GD_LAUNCH(E, 16, 4); break;                            \
@@ -411,7 +457,8 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   if (abl && !swiglu) {
 #define RFQ_GD_ABL(A) \
     gemm_dense_kernel<EPI_STORE, 16, 2, A><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, \
-                                                                  K, up_off, tiles_m, tiles_n)
+                                                                  K, up_off, tiles_m, tiles_n, \
+                                                                  nullptr, 0, 0)
     switch (abl) {
       case 1: RFQ_GD_ABL(1); break;
       case 2: RFQ_GD_ABL(2); break;
@@ -425,6 +472,25 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   if (swiglu) { RFQ_GD_EPI(EPI_SWIGLU) } else { RFQ_GD_EPI(EPI_STORE) }
 #undef RFQ_GD_EPI
 #undef RFQ_GD_LAUNCH
+}
+
+// Grouped (MoE) form: x = [rows, K] expert-sorted 128-row-padded rows, w = [E, N, K],
+// expert_offsets [E+1] (device, padded row offsets), max_blocks = rows / 128.  swiglu:
+// N = 2F (gate | up per expert), out [rows, F].  Fixed grid for graph capture.
+void launch_gemm_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
+                         const int32_t* expert_offsets, int max_blocks, int n_out, int K, int E,
+                         int64_t w_rows, bool swiglu, hipStream_t s) {
+  if (max_blocks <= 0) return;
+  const int tiles_n = swiglu ? n_out / 128 : n_out / kGN;
+  const int chunks = (max_blocks + E) / 2 + 1;    // live 256-row tiles <= this
+  const int grid = chunks * tiles_n;
+  const int64_t estride = w_rows * K;
+  if (swiglu)
+    gemm_dense_kernel<EPI_SWIGLU, 16, 2, 0, true><<<grid, 512, kGLds, s>>>(
+        x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, expert_offsets, E, estride);
+  else
+    gemm_dense_kernel<EPI_STORE, 16, 2, 0, true><<<grid, 512, kGLds, s>>>(
+        x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, expert_offsets, E, estride);
 }
 
 }  // namespace rfq

@@ -571,6 +571,18 @@ def moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu: bo
                             tile or MOE_TILE_ROWS)
 
 
+def moe_gemm_dense(x, w, out, expert_offsets, swiglu: bool = False):
+    """Grouped GEMM over expert segments (moe_align with block 128) on the dense
+    kernel's 8-wave ping-pong MFMA structure (gemm_dense.hip GROUPED): no host sync,
+    fixed grid; swiglu: w = [E, 2F, K] gate|up and out = silu(x Wg^T) * (x Wu^T)."""
+    _native.ops().moe_gemm_dense(x, w, out, expert_offsets, swiglu)
+
+
+def moe_gemm_dense_ok(w, swiglu: bool) -> bool:
+    N, K = w.shape[1], w.shape[2]
+    return K % 64 == 0 and ((N // 2) % 128 == 0 if swiglu else N % 256 == 0)
+
+
 def moe_route(x, router_w, topk, renorm, weights, ids):
     """Router logits (x . router_w^T, bf16-rounded) + softmax top-k in one kernel (GPU,
     small T); CPU: the same two steps in torch."""

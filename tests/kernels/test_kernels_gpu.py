@@ -715,3 +715,43 @@ def test_gemm_dense_strided_rows(gpu):
     out = torch.empty(300, 512 + 256, device="cuda", dtype=BF)[:, :512]
     ops.gemm_dense(x, w, out=out)
     _close(out, x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, what="strided")
+
+
+@pytest.mark.parametrize("T", [65, 300, 1000])
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_moe_gemm_dense(gpu, T, swiglu):
+    """The grouped form of the dense MFMA GEMM over moe_align's 128-row expert segments
+    (odd block counts, empty experts) against the per-expert fp32 oracle; padding rows
+    of an expert with an odd block count must not spill into the next expert."""
+    from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
+
+    d, F, E, k = 256, 384, 8, 2
+    g = torch.Generator(device="cuda").manual_seed(T)
+    N = 2 * F if swiglu else d
+    K = d if swiglu else F
+    w = ((torch.rand(E, N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(BF)
+    bufs = MoEBuffers.allocate(T, k, E, max(d, K), F, "cuda")
+    logits = torch.randn(T, E, device="cuda", generator=g).to(BF)
+    logits[:, 3] = -30.0                                  # expert 3 gets no rows
+    n = T * k
+    cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+    wts, ids = bufs.weights[:T], bufs.ids[:T]
+    ops.moe_topk(logits, k, True, wts, ids)
+    ops.moe_align(ids, E, BLOCK_M, bufs.sorted_ids[:cap], bufs.inv_pos[:n],
+                  bufs.expert_of_block[:cap // BLOCK_M], bufs.expert_offsets, bufs.num_blocks)
+    xs = (torch.rand(cap, K, device="cuda", generator=g) * 2 - 1).to(BF)
+    out = torch.full((cap, F if swiglu else N), 7.0, device="cuda", dtype=BF)
+    ops.moe_gemm_dense(xs, w, out, bufs.expert_offsets, swiglu)
+    off = bufs.expert_offsets.tolist()
+    assert off[4] == off[3]
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        if b <= a:
+            continue
+        r = xs[a:b].float() @ w[e].float().t()
+        if swiglu:
+            gg, u = r[:, :F].to(BF).float(), r[:, F:].to(BF).float()
+            r = (gg * torch.sigmoid(gg)).to(BF).float() * u
+        _close(out[a:b], r, atol=2e-2, rtol=2e-2, what=f"expert {e} rows {a}:{b}")
+    if off[E] < cap:                                       # rows past the live segments
+        assert bool((out[off[E]:].float() == 7.0).all())
