@@ -24,15 +24,7 @@ BLOCK_S = 16            # expert segment padding on the small-batch path
 SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
 # K slices of the latency-path w2 (gemm_skinny.hip moe_skinny_kernel SPLIT): 0/1 = off
 W2_SPLITS = int(os.environ.get("RFQ_MOE_W2_SPLITS", "2"))
-# Eager steps of at least this many tokens run one hipBLASLt GEMM per expert (one host
-# sync per layer for the segment offsets) instead of the hand-written grouped GEMMs.
-# Measured (profiles/r2_moe_grouped_gemm.md): the grouped w13+SwiGLU (256x256) + w2
-# pair beats hipBLASLt w13 + silu_mul + w2 from 192 to 1536 rows per expert (top-2 of
-# 8: T = 768-6144 tokens); the large prefill-chunk steps (up to 16K tokens, 4K rows
-# per expert) stay on hipBLASLt.  End to end (bench.py --model mixtral): threshold
-# 4096: 77.9 docs/s, 8192: 77.0, 1025: 75.7-77.6, grouped everywhere: 68.3.
-# RFQ_MOE_BLT_MIN_TOKENS=0 sends all eager steps to hipBLASLt.
-BLT_MIN_TOKENS = int(os.environ.get("RFQ_MOE_BLT_MIN_TOKENS", "4096"))
+
 
 
 @dataclass
@@ -128,8 +120,6 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
         return out
     logits = x @ router_w.t()
-    if T >= BLT_MIN_TOKENS and not torch.cuda.is_current_stream_capturing():
-        return _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset, E)
     cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
     nb = cap // BLOCK_M
     ops.moe_topk(logits, topk, True, w, ids)
@@ -140,10 +130,16 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
                   bufs.num_blocks)
     xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
     ops.moe_gather(x, sorted_ids, topk, xs)
-    if ops.moe_gemm8_ok(w13, True) and ops.moe_gemm8_ok(w2, False):
-        # grouped MFMA GEMMs; w13's epilogue applies SwiGLU (no h13 pass).  w13 always
-        # on the 256x256 tile; w2 (N = d, 16x fewer weight tiles) on 128x256 below
-        # ~320 rows per expert, where the 256-row tile leaves CUs idle
+    if ops.moe_gemm_dense_ok(w13, True) and ops.moe_gemm_dense_ok(w2, False):
+        # grouped GEMMs on the dense kernel's 8-wave ping-pong MFMA structure
+        # (gemm_dense.hip GROUPED): the segment offsets are read on the device, the
+        # grid is fixed by the capacity, w13's epilogue applies SwiGLU.  Measured
+        # (profiles/r3_moe_dense_grouped.md) faster than round 2's grouped kernel and
+        # than one hipBLASLt GEMM per expert at every step size from 512 to 16K tokens,
+        # so no step reads the offsets back to the host
+        ops.moe_gemm_dense(xs, w13, act, bufs.expert_offsets, True)
+        ops.moe_gemm_dense(act, w2, y, bufs.expert_offsets, False)
+    elif ops.moe_gemm8_ok(w13, True) and ops.moe_gemm8_ok(w2, False):
         w2_tile = 256 if n >= 320 * w13.shape[0] else 128
         ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, bufs.expert_offsets, True, 256)
         ops.moe_gemm8(act, w2, y, eob, bufs.num_blocks, bufs.expert_offsets, False, w2_tile)
@@ -163,36 +159,3 @@ def _localize(ids: torch.Tensor, w: torch.Tensor, e0: int, e_local: int) -> None
     ids.copy_(torch.where(mine, loc, torch.full_like(loc, e_local)))
     w.mul_(mine.to(w.dtype))
 
-
-def _moe_per_expert(x, w13, w2, topk, bufs, logits, out, expert_offset=0, E_align=None):
-    """Large eager steps: expert segments padded to 16 rows, one hipBLASLt GEMM per
-    routed expert.  Reading the 9 segment offsets costs one host sync per layer,
-    which only eager (non-graph) steps can afford; at >= 768 rows per expert it buys
-    ~1.05 PF/s GEMMs vs the grouped gemm8's ~0.85 (tools/bench_moe.py) and 1/8 of
-    its row padding."""
-    T = x.shape[0]
-    E = E_align or w13.shape[0]
-    n = T * topk
-    w, ids = bufs.weights[:T], bufs.ids[:T]
-    ops.moe_topk(logits, topk, True, w, ids)
-    if E != w13.shape[0]:
-        _localize(ids, w, expert_offset, w13.shape[0])
-    cap = (n + E * (BLOCK_S - 1) + BLOCK_S - 1) // BLOCK_S * BLOCK_S
-    sorted_ids = bufs.sorted_ids[:cap]
-    ops.moe_align(ids, E, BLOCK_S, sorted_ids, bufs.inv_pos[:n],
-                  bufs.expert_of_block[:cap // BLOCK_S], bufs.expert_offsets, bufs.num_blocks)
-    xs, h13, act, y = bufs.xs[:cap], bufs.h13[:cap], bufs.act[:cap], bufs.y[:cap]
-    ops.moe_gather(x, sorted_ids, topk, xs)
-    off = bufs.expert_offsets[:E + 1].tolist()
-    for e in range(w13.shape[0]):
-        a, b = off[e], off[e + 1]
-        if b > a:
-            torch.matmul(xs[a:b], w13[e].t(), out=h13[a:b])
-    total = off[w13.shape[0]]
-    ops.silu_mul(h13[:total], act[:total])
-    for e in range(w13.shape[0]):
-        a, b = off[e], off[e + 1]
-        if b > a:
-            torch.matmul(act[a:b], w2[e].t(), out=y[a:b])
-    ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
-    return out
