@@ -32,13 +32,18 @@ void launch_gemv_splitk_plain(const bf16_t*, int64_t, const bf16_t*, int, int, b
 void launch_gemv_splitk_norm(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
                              int, int, float*, unsigned*, bf16_t*, int64_t, const bf16_t*,
                              bf16_t*, int64_t, float, unsigned*, hipStream_t);
+void launch_gemv_splitk_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
+                               int, int, float*, unsigned*, hipStream_t);
+void launch_gemv_splitk_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
+                             int, float*, unsigned*, const int32_t*, const float*, const int32_t*,
+                             bf16_t*, bf16_t*, int, int, int, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
-                        float, int, int, int32_t*, hipStream_t);
+                        float, int, int, int32_t*, int, hipStream_t);
 void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16_t*,
                                const int32_t*, int, const int32_t*, const int32_t*,
                                const int32_t*, int, const int32_t*, const int32_t*, int, int,
@@ -195,20 +200,63 @@ void skinny_gemm_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, int
                                  (int)cfg, cur_stream());
 }
 
+// y_cols: the output's column count (N, or F = N/2 for the SwiGLU epilogue);
+// tiles: output tiles = ticket counters the launch uses
 static void check_splitk(const char* what, const Tensor& x, const Tensor& w, const Tensor& y,
-                         const Tensor& part, const Tensor& tile_cnt, int64_t cfg) {
+                         const Tensor& part, const Tensor& tile_cnt, int64_t cfg,
+                         int64_t y_cols = -1, int64_t tiles = -1) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_I32(tile_cnt);
   CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(y);
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), what, ": w must be contiguous [N, K]");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0), KS = 2 << (cfg & 3);
+  if (y_cols < 0) y_cols = N;
+  if (tiles < 0) tiles = N / 16;
   TORCH_CHECK(M >= 1 && M <= 16, what, ": M must be in [1, 16]");
   TORCH_CHECK(w.size(1) == K && K % 128 == 0 && N % 16 == 0 && (K / 128) >= KS, what,
               ": K % 128 == 0, N % 16 == 0 and K / 128 >= KS required");
-  TORCH_CHECK(y.size(0) == M && y.size(1) == N, what, ": y [M, N]");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == y_cols, what, ": y shape");
   TORCH_CHECK(x.stride(0) % 8 == 0 && y.stride(0) % 4 == 0, what, ": alignment");
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
               what, ": fp32 partials workspace of KS*M*N floats");
-  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, what, ": N/16 tile counters");
+  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= tiles, what, ": one counter per tile");
+}
+
+// out[M, F] = silu(x Wg^T) * (x Wu^T) for w = [Wg; Wu] [2F, K], split K (M <= 16)
+void gemv_splitk_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, const Tensor& part,
+                        const Tensor& tile_cnt, int64_t cfg) {
+  const int64_t F = w.size(0) / 2;
+  TORCH_CHECK(F % 16 == 0 && w.size(0) == 2 * F, "gemv_splitk_swiglu: w [2F, K], F % 16 == 0");
+  check_splitk("gemv_splitk_swiglu", x, w, out, part, tile_cnt, cfg, F, F / 16);
+  rfq::launch_gemv_splitk_swiglu(bp(x), x.stride(0), bp(w), (int)F, x.size(1), bpm(out),
+                                 out.stride(0), x.size(0), (int)cfg, part.data_ptr<float>(),
+                                 reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), cur_stream());
+}
+
+// qkv = x w^T with NeoX RoPE on q / k and the paged KV append, split K (M <= 16);
+// only qkv's q columns are written (= gemv_splitk + rope_kv)
+void gemv_splitk_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
+                      const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
+                      const Tensor& v_cache, int64_t Hq, int64_t Hkv, const Tensor& part,
+                      const Tensor& tile_cnt, int64_t cfg) {
+  const int64_t N = w.size(0);
+  check_splitk("gemv_splitk_rope", x, w, qkv, part, tile_cnt, cfg, N, N / 32);
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "gemv_splitk_rope: w must be [(Hq + 2 Hkv) * 128, K]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == 128,
+              "gemv_splitk_rope: cos_sin must be fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == 128 &&
+                  k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  v_cache.sizes() == k_cache.sizes(),
+              "gemv_splitk_rope: cache must be [blocks, Hkv, BS, 128]");
+  TORCH_CHECK(positions.numel() >= x.size(0) && slot_mapping.numel() >= x.size(0),
+              "gemv_splitk_rope: metadata");
+  rfq::launch_gemv_splitk_rope(bp(x), x.stride(0), bp(w), (int)N, x.size(1), bpm(qkv),
+                               qkv.stride(0), x.size(0), (int)cfg, part.data_ptr<float>(),
+                               reinterpret_cast<unsigned*>(tile_cnt.data_ptr()),
+                               positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
+                               slot_mapping.data_ptr<int32_t>(), bpm(k_cache), bpm(v_cache),
+                               (int)Hq, (int)Hkv, k_cache.size(2), cur_stream());
 }
 
 // y = x . w^T, split-K over (N/16) x KS workgroups with the in-launch per-tile
@@ -332,7 +380,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
                  const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
                  int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item,
-                 const std::optional<Tensor>& tickets) {
+                 const std::optional<Tensor>& tickets, int64_t waves) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode: tiles_per_item in {1, 2}");
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
@@ -349,6 +397,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   && seq_q_start.numel() >= seq_q_len.numel(),
               "attn_decode: per-sequence arrays mismatch");
   TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "attn_decode: num_splits in [1, 32]");
+  TORCH_CHECK(waves == 1 || (waves == 4 && num_splits % 4 == 0),
+              "attn_decode: waves 1, or 4 with num_splits % 4 == 0");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
@@ -361,7 +411,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     // zero-initialised once by the caller; the merging wave resets its entry
     CHECK_DEV(*tickets); CHECK_I32(*tickets);
     TORCH_CHECK(tickets->numel() >= work_seq.numel() * Hkv, "attn_decode: ticket buffer too small");
-    TORCH_CHECK(num_splits <= 16, "attn_decode: the in-kernel merge takes at most 16 splits");
+    TORCH_CHECK(num_splits / waves <= 16, "attn_decode: the in-kernel merge takes at most 16 splits");
     tk = tickets->data_ptr<int32_t>();
   }
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
@@ -371,7 +421,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
-                          (float)scale, num_splits, tiles_per_item, tk, cur_stream());
+                          (float)scale, num_splits, tiles_per_item, tk, (int)waves, cur_stream());
 }
 
 // Shared-prefix (cascade) decode attention, num_splits == 1; see attn_decode.hip.
@@ -780,6 +830,11 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("gemv_splitk_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
         "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) part, Tensor(f!) tile_cnt, "
         "int cfg) -> ()");
+  m.def("gemv_splitk_swiglu(Tensor x, Tensor w, Tensor(a!) out, Tensor(b!) part, "
+        "Tensor(c!) tile_cnt, int cfg) -> ()");
+  m.def("gemv_splitk_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
+        "Tensor(d!) part, Tensor(e!) tile_cnt, int cfg) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
@@ -803,7 +858,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
-        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None) -> ()");
+        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None, int waves=1) -> ()");
   m.def("attn_decode_shared(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_ct, Tensor(a!) out, Tensor(b!) ws_i32, Tensor(c!) pre_o, Tensor(d!) pre_ml, "
@@ -845,6 +900,8 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("skinny_gemm_swiglu", &skinny_gemm_swiglu);
   m.impl("gemv_splitk", &gemv_splitk);
   m.impl("gemv_splitk_norm", &gemv_splitk_norm);
+  m.impl("gemv_splitk_swiglu", &gemv_splitk_swiglu);
+  m.impl("gemv_splitk_rope", &gemv_splitk_rope);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);

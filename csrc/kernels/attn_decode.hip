@@ -97,9 +97,29 @@ __global__ __launch_bounds__(1024) void attn_prefix_meta_kernel(
   if (tid == 0) { meta[0] = P * kPage; meta[1] = s_cnt; }
 }
 
-// (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over
-template <int NT, int MODE = 0>
-__global__ __launch_bounds__(64, 2) void attn_decode_kernel(
+// LDS hand-off inside one wave's V tile buffer.  One wave per workgroup: the block
+// barrier (as before).  Several waves with independent split loops (different page
+// counts): a barrier would mismatch, and the tile buffer is the wave's own, so draining
+// this wave's LDS operations (in-order per wave) and fencing the compiler suffices.
+template <int NWV>
+__device__ __forceinline__ void wave_lds_sync() {
+  if constexpr (NWV == 1) {
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over.
+// NWV > 1 (small decode batches): a workgroup of NWV waves, one KV split per wave,
+// merged through LDS before the workgroup's single partial (or, with one workgroup per
+// item, the bf16 output) leaves the CU.  16 splits of one (work item, kv head) then
+// cost 4 workgroups + a 4-way in-kernel merge instead of 16 waves whose partials a
+// second launch (attn_decode_reduce) or a 16-way single-wave merge combines: the
+// decode step of a batch-1 request runs one attention launch per layer.
+template <int NT, int MODE = 0, int NWV = 1>
+__global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     int bt_stride, const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
@@ -107,9 +127,14 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
     int num_splits, PrefixArgs px = PrefixArgs{}, int32_t* __restrict__ tickets = nullptr) {
-  __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
+  __shared__ __attribute__((aligned(16))) bf16_t v_lds_all[NWV * kPage * kD];
+  const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;   // wave = inner split
+  bf16_t* v_lds = v_lds_all + wv * kPage * kD;
+  // split: the workgroup's (outer) split, which the partial / merge epilogue indexes;
+  // gsplit / nsplit: this wave's KV range among all NWV * num_splits
   const int split = blockIdx.x, kvh = blockIdx.y, w = blockIdx.z;
-  const int lane = threadIdx.x;
+  const int gsplit = split * NWV + wv, nsplit = num_splits * NWV;
+  const int lane = threadIdx.x & 63;
   const int g = lane >> 4;   // 16-lane group
   const int c = lane & 15;   // MFMA column
   const int G = Hq / Hkv;
@@ -150,9 +175,9 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     }
   }
 
-  int tps = (kvl - base + num_splits - 1) / num_splits;
+  int tps = (kvl - base + nsplit - 1) / nsplit;
   tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = base + split * tps;
+  const int start = base + gsplit * tps;
   const int end = min(kvl, start + tps);
 
   float m_run[NT], l_run[NT];
@@ -257,7 +282,7 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
         pb[t] = pack8(p);
       }
 
-      __syncthreads();  // V tile visible (single wave: orders the LDS writes)
+      wave_lds_sync<NWV>();  // V tile visible (one wave per tile buffer)
 
       // ---- O^T += V^T P^T (one transposed V read feeds every tile) ----
       const int q4 = c >> 2, p4 = c & 3;
@@ -274,7 +299,7 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
             o[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb[t]),
                                                               o[t][m], 0, 0, 0);
       }
-      __syncthreads();  // before the next tile overwrites v_lds
+      wave_lds_sync<NWV>();  // before the next tile overwrites v_lds
     };
 
     s16x8 kA[2][4], vA[8];
@@ -303,6 +328,74 @@ __global__ __launch_bounds__(64, 2) void attn_decode_kernel(
         fetch(j, kA, vA);
         process(j, kA, vA);
       }
+    }
+  }
+
+  if constexpr (NWV > 1) {
+    // ---- merge the NWV waves' splits through LDS (the V tile buffers are reused) ----
+    __shared__ float ml_lds[NWV][NT][16][2];
+    float* obuf = reinterpret_cast<float*>(v_lds_all);   // (NWV-1) x 8 x 64 f32x4 <= v_lds
+    static_assert((NWV - 1) * 8 * 64 * 16 <= NWV * kPage * kD * 2, "merge buffer");
+    float lt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      lt[t] = l_run[t];
+      lt[t] += __shfl_xor(lt[t], 16, 64);
+      lt[t] += __shfl_xor(lt[t], 32, 64);
+    }
+    __syncthreads();                                   // every wave is done with v_lds
+    if (g == 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        ml_lds[wv][t][c][0] = m_run[t];
+        ml_lds[wv][t][c][1] = lt[t];
+      }
+    }
+    __syncthreads();
+    float a_self[NT], l_all[NT], m_all[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float ms = -INFINITY;
+#pragma unroll
+      for (int v2 = 0; v2 < NWV; ++v2) ms = fmaxf(ms, ml_lds[v2][t][c][0]);
+      const float mu = ms == -INFINITY ? 0.f : ms;
+      float l = 0.f;
+#pragma unroll
+      for (int v2 = 0; v2 < NWV; ++v2) {
+        const float mw = ml_lds[v2][t][c][0];
+        l += (mw == -INFINITY ? 0.f : fast_exp2(mw - mu)) * ml_lds[v2][t][c][1];
+      }
+      a_self[t] = m_run[t] == -INFINITY ? 0.f : fast_exp2(m_run[t] - mu);
+      m_all[t] = ms;
+      l_all[t] = l;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (wv > 0) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          reinterpret_cast<f32x4*>(obuf)[((wv - 1) * 8 + m) * 64 + lane] = o[t][m] * a_self[t];
+      }
+      __syncthreads();
+      if (wv == 0) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          f32x4 acc = o[t][m] * a_self[t];
+#pragma unroll
+          for (int v2 = 1; v2 < NWV; ++v2)
+            acc += reinterpret_cast<const f32x4*>(obuf)[((v2 - 1) * 8 + m) * 64 + lane];
+          o[t][m] = acc;
+        }
+      }
+      __syncthreads();
+    }
+    if (wv != 0) return;
+    // wave 0 carries the workgroup's merged state into the epilogue below: the
+    // per-lane partial sums must add up to the merged denominator over the 4 groups
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      m_run[t] = m_all[t];
+      l_run[t] = g == 0 ? l_all[t] : 0.f;
     }
   }
 
@@ -487,9 +580,31 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
                         const int32_t* seq_kv_len, const int32_t* work_seq,
                         const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
                         float* part_o, float* part_ml, int Hq, int Hkv, float scale,
-                        int num_splits, int tiles_per_item, int32_t* tickets, hipStream_t s) {
+                        int num_splits, int tiles_per_item, int32_t* tickets, int waves,
+                        hipStream_t s) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
+  if (waves == 4 && num_splits % 4 == 0) {
+    // 4 splits per workgroup merged in LDS; the workgroups' partials merged in-kernel
+    // by the last to finish (tickets) or, without tickets, by the reduce launch
+    const int outer = num_splits / 4;
+    const dim3 grid4(outer, Hkv, W);
+    int32_t* tk4 = outer > 1 ? tickets : nullptr;
+    if (tiles_per_item == 2)
+      attn_decode_kernel<2, 0, 4><<<grid4, 256, 0, s>>>(
+          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
+          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
+          outer, PrefixArgs{}, tk4);
+    else
+      attn_decode_kernel<1, 0, 4><<<grid4, 256, 0, s>>>(
+          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
+          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
+          outer, PrefixArgs{}, tk4);
+    if (outer > 1 && tk4 == nullptr)
+      attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
+                                                          outer);
+    return;
+  }
   dim3 grid(num_splits, Hkv, W);
   int32_t* tk = num_splits > 1 ? tickets : nullptr;
   if (tiles_per_item == 2)

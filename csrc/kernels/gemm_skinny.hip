@@ -239,26 +239,38 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
             acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 as_bf16x8(w[u][a][j]), as_bf16x8(x[u][t][j]), acc[a][t], 0, 0, 0);
   }
-  for (; ks < ks1; ++ks) {
-    s16x8 w[NT][4], x[MT][4];
+  // tail (< U k-steps): every load is issued before the first MFMA, so a short K
+  // range (e.g. the TP=8 o projection, K = 1024: 2 steps per wave) costs one HBM
+  // round trip instead of one per step
+  if (ks < ks1) {
+    const int rem = ks1 - ks;
+    s16x8 w[U][NT][4], x[U][MT][4];
 #pragma unroll
-    for (int a = 0; a < NT; ++a)
+    for (int u = 0; u < U; ++u)
+      if (u < rem) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w[a][j] = ldw<NTL>(wp[a] + (int64_t)ks * 128 + j * JS);
+        for (int a = 0; a < NT; ++a)
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        x[t][j] = xv[t] ? ldx8<GX>(xp[t] + ks * 128 + j * JS, K) : zero;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int a = 0; a < NT; ++a)
+          for (int j = 0; j < 4; ++j)
+            w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * 128 + j * JS);
 #pragma unroll
         for (int t = 0; t < MT; ++t)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              as_bf16x8(w[a][j]), as_bf16x8(x[t][j]), acc[a][t], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            x[u][t][j] = xv[t] ? ldx8<GX>(xp[t] + (ks + u) * 128 + j * JS, K) : zero;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < rem) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int a = 0; a < NT; ++a)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+              acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  as_bf16x8(w[u][a][j]), as_bf16x8(x[u][t][j]), acc[a][t], 0, 0, 0);
+      }
   }
 
   if (NW > 1) {
@@ -517,41 +529,73 @@ void launch_skinny_gemm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, in
 // The o / down projections have only N/16 = 256 output tiles: one workgroup per CU
 // whose waves each stream a long K range as a few dependent load rounds, so the
 // kernel is bound by (rounds x HBM latency), not by bandwidth.  Here the grid is
-// tiles x KS: KS workgroups per 16-feature tile each stream K/KS (more, shorter
+// tiles x KS: KS workgroups per output tile each stream K/KS (more, shorter
 // streams in flight on every CU), publish their fp32 partial tile write-through,
 // and the last of a tile's KS arrivals (per-tile ticket) sums the slices in slice
-// order and writes the bf16 tile.  With NORM, finished tiles take a second ticket
-// and the grid's last one runs the residual-add RMSNorm (last_block_add_norm).
-// Every hand-off is the "every load sc1" form of cdna_hip_programming.md §6
-// Guideline 16: sc1 8-byte stores drained by vmcnt(0) + barrier, relaxed agent
-// tickets, sc1 loads of all handed-off bytes; counters are left at zero.
-template <int NW, int U, bool NORM>
+// order and runs the epilogue.  Every hand-off is the "every load sc1" form of
+// cdna_hip_programming.md §6 Guideline 16: sc1 8-byte stores drained by vmcnt(0) +
+// barrier, relaxed agent tickets, sc1 loads of all handed-off bytes; counters are
+// left at zero.
+//
+// Epilogues (EPI):
+//   kGvPlain  Y[M, N] bf16.
+//   kGvNorm   Y, then finished tiles take a second ticket and the grid's last one
+//             runs the residual-add RMSNorm (last_block_add_norm).
+//   kGvSwi    the tile is a (gate, up) pair of 16-row blocks [n0, +16) and
+//             [up_off + n0, +16) of the stacked gate|up weight; Y[M, F] = SwiGLU,
+//             rounded exactly like the skinny SWI epilogue / act.hip silu_mul.
+//             Small shards (TP = 8: F = 3,584 -> 224 tiles < 256 CUs) get KS x more
+//             workgroups than the one-tile-per-workgroup skinny kernel.
+//   kGvRope   the tile is a rotate-half pair [h*128 + 16j, +16), [h*128 + 64 + 16j,
+//             +16) of one head (RopeEpi): NeoX RoPE on q / k, q to Y, k / v appended
+//             to the paged cache.  The TP = 8 QKV shard (N = 1,280) has only 40 such
+//             pairs: split K is what lets it use more than 40 CUs.
+enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
+
+template <int NW, int U, int EPI>
 __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
-    bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part,
-    unsigned* __restrict__ tile_cnt, NormEpi ep) {
-  __shared__ f32x4 red[NW][64];
+    bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part, int Nn,
+    unsigned* __restrict__ tile_cnt, NormEpi ep, RopeEpi re, int up_off) {
+  constexpr int NT = EPI >= kGvSwi ? 2 : 1;
+  __shared__ f32x4 red[NW][NT][64];
   __shared__ float nscratch[17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int ntile = gridDim.x / KS, N = ntile * 16;
+  const int ntile = gridDim.x / KS;
   const int bt = blockIdx.x / KS, slice = blockIdx.x - bt * KS;
-  const int n0 = bt * 16;
+  // GEMM rows of the tile's NT 16-row blocks
+  int row0[NT];
+  if constexpr (EPI == kGvRope) {
+    row0[0] = (bt >> 2) * 128 + (bt & 3) * 16;
+    row0[NT - 1] = row0[0] + 64;
+  } else if constexpr (EPI == kGvSwi) {
+    row0[0] = bt * 16;
+    row0[NT - 1] = up_off + bt * 16;
+  } else {
+    row0[0] = bt * 16;
+  }
   const int nks_all = K >> 7;
   const int sl0 = slice * nks_all / KS, nks = (slice + 1) * nks_all / KS - sl0;
   const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
-  const bf16_t* wp = W + (int64_t)(n0 + r) * K + g * 8;
+  const bf16_t* wp[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) wp[a] = W + (int64_t)(row0[a] + r) * K + g * 8;
   const bool xv = r < M;
   const bf16_t* xp = X + (int64_t)(xv ? r : 0) * ldx + g * 8;
   const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   int ks = ks0;
   for (; ks + U <= ks1; ks += U) {
-    s16x8 w[U][4], x[U][4];
+    s16x8 w[U][NT][4], x[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[u][j] = ldw<false>(wp + (int64_t)(ks + u) * 128 + j * 32);
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * 128 + j * 32);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -561,30 +605,48 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[u][j]), as_bf16x8(x[u][j]), acc,
-                                                      0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+          acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[u][a][j]), as_bf16x8(x[u][j]),
+                                                           acc[a], 0, 0, 0);
   }
-  for (; ks < ks1; ++ks) {
-    s16x8 w[4], x[4];
+  if (ks < ks1) {                       // tail: all loads before the first MFMA
+    const int rem = ks1 - ks;
+    s16x8 w[U][NT][4], x[U][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = ldw<false>(wp + (int64_t)ks * 128 + j * 32);
+    for (int u = 0; u < U; ++u)
+      if (u < rem) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      x[j] = xv ? *reinterpret_cast<const s16x8*>(xp + ks * 128 + j * 32) : zero;
+        for (int a = 0; a < NT; ++a)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[j]), as_bf16x8(x[j]), acc, 0, 0,
-                                                    0);
+          for (int j = 0; j < 4; ++j)
+            w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * 128 + j * 32);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          x[u][j] = xv ? *reinterpret_cast<const s16x8*>(xp + (ks + u) * 128 + j * 32) : zero;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < rem) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int a = 0; a < NT; ++a)
+            acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(w[u][a][j]),
+                                                             as_bf16x8(x[u][j]), acc[a], 0, 0, 0);
+      }
   }
-  red[wave][lane] = acc;
+#pragma unroll
+  for (int a = 0; a < NT; ++a) red[wave][a][lane] = acc[a];
   __syncthreads();
-  // D layout: lane holds output features n0 + g*4 + i for token r.
-  gu64* slab = (gu64*)(part + ((int64_t)slice * M + r) * N + n0 + g * 4);
-  if (wave == 0) {
-    f32x4 s = red[0][lane];
+  // D layout: lane holds GEMM rows row0[a] + g*4 + i for token r.
+  if (wave == 0 && xv) {
 #pragma unroll
-    for (int w2 = 1; w2 < NW; ++w2) s += red[w2][lane];
-    if (xv) {
+    for (int a = 0; a < NT; ++a) {
+      f32x4 s = red[0][a][lane];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) s += red[w2][a][lane];
+      gu64* slab = (gu64*)(part + ((int64_t)slice * M + r) * Nn + row0[a] + g * 4);
       __hip_atomic_store(slab, (unsigned long long)__float_as_uint(s[0]) |
                                    ((unsigned long long)__float_as_uint(s[1]) << 32),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -606,28 +668,88 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
   if (threadIdx.x == 0)
     __hip_atomic_store(tile_cnt + bt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (wave == 0 && xv) {
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < KS; ++sl) {
-      const gu64* q = (const gu64*)(part + ((int64_t)sl * M + r) * N + n0 + g * 4);
-      const unsigned long long u0 = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long u1 =
-          __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s[0] += __uint_as_float((uint32_t)u0);
-      s[1] += __uint_as_float((uint32_t)(u0 >> 32));
-      s[2] += __uint_as_float((uint32_t)u1);
-      s[3] += __uint_as_float((uint32_t)(u1 >> 32));
+    float s[NT][4];
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+      s[a][0] = s[a][1] = s[a][2] = s[a][3] = 0.f;
+      for (int sl = 0; sl < KS; ++sl) {
+        const gu64* q = (const gu64*)(part + ((int64_t)sl * M + r) * Nn + row0[a] + g * 4);
+        const unsigned long long u0 = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long u1 =
+            __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s[a][0] += __uint_as_float((uint32_t)u0);
+        s[a][1] += __uint_as_float((uint32_t)(u0 >> 32));
+        s[a][2] += __uint_as_float((uint32_t)u1);
+        s[a][3] += __uint_as_float((uint32_t)(u1 >> 32));
+      }
     }
-    uint2 v;
-    v.x = pack_bf16x2(s[0], s[1]);
-    v.y = pack_bf16x2(s[2], s[3]);
-    bf16_t* yp = Y + (int64_t)r * ldy + n0 + g * 4;
-    if constexpr (NORM)
-      __hip_atomic_store((gu64*)yp, (unsigned long long)v.x | ((unsigned long long)v.y << 32),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      *reinterpret_cast<uint2*>(yp) = v;
+    if constexpr (EPI == kGvSwi) {
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gf = bf2f(f2bf(s[0][i]));              // = the gate_up GEMM's bf16 output
+        const float sg = gf / (1.f + __expf(-gf));
+        o[i] = bf2f(f2bf(sg)) * bf2f(f2bf(s[NT - 1][i]));
+      }
+      uint2 v;
+      v.x = pack_bf16x2(o[0], o[1]);
+      v.y = pack_bf16x2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(Y + (int64_t)r * ldy + bt * 16 + g * 4) = v;
+    } else if constexpr (EPI == kGvRope) {
+      const int h = bt >> 2;                               // head in [q | k | v]
+      const int d0 = (bt & 3) * 16 + g * 4;                // rotary index of s[0][0]
+      float o1[4], o2[4];
+      if (h < re.Hq + re.Hkv) {
+        const float* cs = re.cos_sin + (int64_t)re.positions[r] * 128;
+        const float4 c = *reinterpret_cast<const float4*>(cs + d0);
+        const float4 sn = *reinterpret_cast<const float4*>(cs + 64 + d0);
+        const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o1[i] = s[0][i] * cc[i] - s[NT - 1][i] * ss[i];
+          o2[i] = s[NT - 1][i] * cc[i] + s[0][i] * ss[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o1[i] = s[0][i];
+          o2[i] = s[NT - 1][i];
+        }
+      }
+      uint2 v1, v2;
+      v1.x = pack_bf16x2(o1[0], o1[1]);
+      v1.y = pack_bf16x2(o1[2], o1[3]);
+      v2.x = pack_bf16x2(o2[0], o2[1]);
+      v2.y = pack_bf16x2(o2[2], o2[3]);
+      bf16_t* dst = nullptr;
+      if (h < re.Hq) {
+        dst = Y + (int64_t)r * ldy + h * 128;
+      } else {
+        const int slot = re.slots[r];
+        if (slot >= 0) {                                   // -1 = padding row: no KV write
+          const bool is_k = h < re.Hq + re.Hkv;
+          const int kvh = is_k ? h - re.Hq : h - re.Hq - re.Hkv;
+          dst = (is_k ? re.k_cache : re.v_cache) +
+                (((int64_t)(slot / re.BS) * re.Hkv + kvh) * re.BS + slot % re.BS) * 128;
+        }
+      }
+      if (dst != nullptr) {
+        *reinterpret_cast<uint2*>(dst + d0) = v1;
+        *reinterpret_cast<uint2*>(dst + 64 + d0) = v2;
+      }
+    } else {
+      uint2 v;
+      v.x = pack_bf16x2(s[0][0], s[0][1]);
+      v.y = pack_bf16x2(s[0][2], s[0][3]);
+      bf16_t* yp = Y + (int64_t)r * ldy + row0[0] + g * 4;
+      if constexpr (EPI == kGvNorm)
+        __hip_atomic_store((gu64*)yp, (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *reinterpret_cast<uint2*>(yp) = v;
+    }
   }
-  if constexpr (NORM) {
+  if constexpr (EPI == kGvNorm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -640,31 +762,29 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (threadIdx.x == 0)
       __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_block_add_norm<NW * 64, 1>(Y, ldy, N, M, ep, nscratch);
+    last_block_add_norm<NW * 64, 1>(Y, ldy, ntile * 16, M, ep, nscratch);
   }
 }
 
 // cfg bits: [1:0] KS = 2 << bits (2, 4, 8, 16); bit 2: 8 waves (else 4); bit 3: U = 2 (else 4;
 // U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones).
-// part: fp32 [KS][M][N]; tile_cnt: N/16 zeroed uint32 (left at zero).
-void launch_gemv_splitk(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
-                        int64_t ldy, int M, int cfg, float* part, unsigned* tile_cnt, bool norm,
-                        const NormEpi& ep, hipStream_t s) {
+// part: fp32 [KS][M][Nn] (Nn = GEMM rows); tile_cnt: one zeroed uint32 per output tile
+// (left at zero).  ntile: N/16 (plain, norm), F/16 (swiglu), N/32 (rope).
+template <int EPI>
+static void launch_gemv_splitk_epi(const bf16_t* X, int64_t ldx, const bf16_t* W, int ntile, int Nn,
+                                   int K, bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
+                                   unsigned* tile_cnt, const NormEpi& ep, const RopeEpi& re,
+                                   int up_off, hipStream_t s) {
   const int KS = 2 << (cfg & 3);
-  const dim3 grid((N / 16) * KS);
-#define GV_LAUNCH(nw, u, nm)                                                                \
-  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, nm>), grid, dim3(nw * 64), 0, s, X, ldx, W, K, \
-                     Y, ldy, M, KS, part, tile_cnt, ep)
-  const int sel = ((cfg >> 2) & 3) | (norm ? 4 : 0);
-  switch (sel) {
-    case 0: GV_LAUNCH(4, 4, false); break;
-    case 1: GV_LAUNCH(8, 4, false); break;
-    case 2: GV_LAUNCH(4, 2, false); break;
-    case 3: GV_LAUNCH(8, 2, false); break;
-    case 4: GV_LAUNCH(4, 4, true); break;
-    case 5: GV_LAUNCH(8, 4, true); break;
-    case 6: GV_LAUNCH(4, 2, true); break;
-    default: GV_LAUNCH(8, 2, true); break;
+  const dim3 grid(ntile * KS);
+#define GV_LAUNCH(nw, u)                                                                        \
+  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI>), grid, dim3(nw * 64), 0, s, X, ldx, W, K, \
+                     Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
+  switch ((cfg >> 2) & 3) {
+    case 0: GV_LAUNCH(4, 4); break;
+    case 1: GV_LAUNCH(8, 4); break;
+    case 2: GV_LAUNCH(4, 2); break;
+    default: GV_LAUNCH(8, 2); break;
   }
 #undef GV_LAUNCH
 }
@@ -675,13 +795,34 @@ void launch_gemv_splitk_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
                              const bf16_t* norm_w, bf16_t* out, int64_t out_stride, float eps,
                              unsigned* counter, hipStream_t s) {
   const NormEpi ep{residual, res_stride, norm_w, out, out_stride, eps, counter, nullptr, 0};
-  launch_gemv_splitk(X, ldx, W, N, K, Y, ldy, M, cfg, part, tile_cnt, true, ep, s);
+  launch_gemv_splitk_epi<kGvNorm>(X, ldx, W, N / 16, N, K, Y, ldy, M, cfg, part, tile_cnt, ep,
+                                  RopeEpi{}, 0, s);
 }
 
 void launch_gemv_splitk_plain(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
                               bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
                               unsigned* tile_cnt, hipStream_t s) {
-  launch_gemv_splitk(X, ldx, W, N, K, Y, ldy, M, cfg, part, tile_cnt, false, NormEpi{}, s);
+  launch_gemv_splitk_epi<kGvPlain>(X, ldx, W, N / 16, N, K, Y, ldy, M, cfg, part, tile_cnt,
+                                   NormEpi{}, RopeEpi{}, 0, s);
+}
+
+// Y[M, F] = silu(x Wg^T) * (x Wu^T), w = [Wg; Wu] [2F, K]
+void launch_gemv_splitk_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, int F, int K,
+                               bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
+                               unsigned* tile_cnt, hipStream_t s) {
+  launch_gemv_splitk_epi<kGvSwi>(X, ldx, W, F / 16, 2 * F, K, Y, ldy, M, cfg, part, tile_cnt,
+                                 NormEpi{}, RopeEpi{}, F, s);
+}
+
+// qkv = x w^T with RoPE + KV append (N = (Hq + 2 Hkv) * 128); only q columns of Y written
+void launch_gemv_splitk_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                             bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
+                             unsigned* tile_cnt, const int32_t* positions, const float* cos_sin,
+                             const int32_t* slots, bf16_t* k_cache, bf16_t* v_cache, int Hq,
+                             int Hkv, int BS, hipStream_t s) {
+  const RopeEpi re{positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, BS};
+  launch_gemv_splitk_epi<kGvRope>(X, ldx, W, N / 32, N, K, Y, ldy, M, cfg, part, tile_cnt,
+                                  NormEpi{}, re, 0, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -42,6 +42,11 @@ from .weights import init_weights
 # two launches at batch 1 (profiles/r2_decode_attention_single_pass.md) -- one wave
 # merging 16 splits x 16 columns is slower than the 32-workgroup reduce kernel.
 SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "0") == "1"
+# RFQ_DECODE_WG_MERGE=1: with >= 4 splits, four splits share a workgroup and merge
+# through LDS (attn_decode.hip NWV = 4) and the workgroups' partials merge in-kernel:
+# one launch per layer.  Off by default: measured 1-2 us per layer SLOWER than one wave
+# per split + the reduce launch at batch 1 (profiles/r3_decode_attention_wg_merge.md).
+DECODE_WG_MERGE = os.environ.get("RFQ_DECODE_WG_MERGE", "0") == "1"
 
 
 @dataclass
@@ -221,12 +226,14 @@ class DecoderLM:
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
 
-    def _dec_tickets(self, work_items: int):
+    def _dec_tickets(self, work_items: int, waves: int = 1):
         """Zeroed int32 tickets for single-pass split decode attention (the kernel resets
         each entry it uses, so one persistent buffer serves every layer and graph replay).
         Sized once, before any capture: split decode only runs below 1024 (work item, kv
-        head) waves (engine/runner.py _decode_splits), extend rows at most 4x that."""
-        if self.device.type != "cuda" or not SINGLE_PASS_DECODE:
+        head) waves (engine/runner.py _decode_splits), extend rows at most 4x that.
+        Used by the 4-wave workgroup form (its few partials merge in-kernel) and, with
+        RFQ_SINGLE_PASS_DECODE, by the one-wave form."""
+        if self.device.type != "cuda" or not (SINGLE_PASS_DECODE or waves > 1):
             return None
         if self._tickets is None:
             self._tickets = torch.zeros(4096 * self.hkv, dtype=torch.int32, device=self.device)
@@ -265,11 +272,12 @@ class DecoderLM:
                                    li == 0)
         elif D > 0:
             po, pm = dec_parts if dec_parts is not None else (attn, attn)
+            ns = m.decode_splits if dec_parts is not None else 1
+            waves = 4 if (DECODE_WG_MERGE and ns >= 4 and ns % 4 == 0) else 1
             ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                             m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
-                            hq, hkv, self.scale,
-                            m.decode_splits if dec_parts is not None else 1,
-                            m.decode_tiles, self._dec_tickets(m.dec_work_seq.numel()))
+                            hq, hkv, self.scale, ns, m.decode_tiles,
+                            self._dec_tickets(m.dec_work_seq.numel(), waves), waves)
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,

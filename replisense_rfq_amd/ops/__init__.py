@@ -65,7 +65,7 @@ def linear_plan(M: int, N: int, K: int) -> int:
             if m >= M:
                 c = _LINEAR_PLAN.get((m, N, K))
                 if c is not None:
-                    return c if (c < 0 or c & 1 == 0 or N % 32 == 0) else -1
+                    return c if (c < 0 or c >= SPLITK_BIT or c & 1 == 0 or N % 32 == 0) else -1
                 break
     return _default_plan(M, N, K)
 
@@ -143,18 +143,28 @@ def norm_plan(M: int, N: int, K: int, gated: bool) -> int:
 
 def splitk_ws(device):
     """(fp32 partial slabs [16 slices x 16 rows x 16384], zeroed int32 tile tickets
-    [1024]) of the split-K GEMV (gemm_skinny.hip gemv_splitk); allocated before any
+    [16384]) of the split-K GEMV (gemm_skinny.hip gemv_splitk); allocated before any
     graph capture so captured graphs bake in stable pointers; tickets left at zero."""
     d = torch.device(device)
     key = ("splitk", d)
     ws = _NORM_COUNTERS.get(key)
     if ws is None:
         ws = _NORM_COUNTERS[key] = (torch.empty(16 * 16 * 16384, dtype=torch.float32, device=d),
-                                    torch.zeros(1024, dtype=torch.int32, device=d))
+                                    torch.zeros(16384, dtype=torch.int32, device=d))
     return ws
 
 
 SPLITK_BIT = 128          # plan cfg bit: the split-K GEMV kernel (low bits = its cfg)
+# split-K GEMV cfgs timed by the start-up plans: KS = 2 << (c & 3), bit 2 = 8 waves,
+# bit 3 = U 2 (gemm_skinny.hip launch_gemv_splitk_epi)
+SPLITK_CFGS = (0, 1, 2, 8, 9, 10, 12, 13, 14)
+
+
+def splitk_fits(device, cfg: int, M: int, n_rows: int, tiles: int) -> bool:
+    """Whether the shared split-K workspace holds a launch (KS*M*n_rows partial floats,
+    ``tiles`` ticket counters)."""
+    part, cnt = splitk_ws(device)
+    return (2 << (cfg & 3)) * M * n_rows <= part.numel() and tiles <= cnt.numel()
 
 
 def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bool:
@@ -204,7 +214,11 @@ def linear_swiglu(x, w):
             if cfg < 0:
                 return None
             out = torch.empty((M, F), dtype=x.dtype, device=x.device)
-            _native.ops().skinny_gemm_swiglu(x, w, out, cfg)
+            if cfg & SPLITK_BIT:
+                part, tiles = splitk_ws(x.device)
+                _native.ops().gemv_splitk_swiglu(x, w, out, part, tiles, cfg & 127)
+            else:
+                _native.ops().skinny_gemm_swiglu(x, w, out, cfg)
             return out
     return None
 
@@ -237,8 +251,13 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
         cfg = rope_plan(x.shape[0], w.shape[0], x.shape[1])
         if cfg >= 0:
             qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-            _native.ops().skinny_gemm_rope(x, w, qkv, positions, cos_sin, slot_mapping, k_cache,
-                                           v_cache, Hq, Hkv, cfg)
+            if cfg & SPLITK_BIT:
+                part, tiles = splitk_ws(x.device)
+                _native.ops().gemv_splitk_rope(x, w, qkv, positions, cos_sin, slot_mapping,
+                                               k_cache, v_cache, Hq, Hkv, part, tiles, cfg & 127)
+            else:
+                _native.ops().skinny_gemm_rope(x, w, qkv, positions, cos_sin, slot_mapping,
+                                               k_cache, v_cache, Hq, Hkv, cfg)
             return qkv
     qkv = linear(x, w)
     rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
@@ -337,6 +356,10 @@ def linear(x, w, out=None, plan: int | None = None):
         if cfg >= 0:
             if out is None:
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            if cfg & SPLITK_BIT:
+                part, tiles = splitk_ws(x.device)
+                _native.ops().gemv_splitk(x, w, out, part, tiles, cfg & 127)
+                return out
             _native.ops().skinny_gemm(x, w, out, cfg)
             return out
         if _SPLIT_PLAN and M > SKINNY_MAX_M and (N, K) in _SPLIT_PLAN:
@@ -430,16 +453,18 @@ def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
 
 def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq, work_ct,
                 out, part_o, part_ml, Hq, Hkv, scale, num_splits=1, tiles_per_item=1,
-                tickets=None):
+                tickets=None, waves: int = 1):
     """Paged attention for decode / short-extend rows (see csrc/kernels/attn_decode.hip).
     A work item (work_seq[w], work_ct[w]) covers column tiles
     [work_ct*tiles_per_item, +tiles_per_item) of its sequence's q_len*G (query, head) pairs.
     With num_splits > 1, ``tickets`` (int32 zeros, >= work items * Hkv, reset by the kernel)
-    makes it single-pass: the last split to finish merges the partials in-kernel."""
+    makes it single-pass: the last split to finish merges the partials in-kernel.
+    ``waves`` = 4 (num_splits % 4 == 0): four splits per workgroup merged through LDS,
+    so only num_splits / 4 partials reach the in-kernel (or reduce-launch) merge."""
     if _gpu(q):
         _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
                                   work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
-                                  num_splits, tiles_per_item, tickets)
+                                  num_splits, tiles_per_item, tickets, waves)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
                          out, Hq, Hkv, scale)

@@ -155,6 +155,50 @@ def test_attn_decode(gpu, Hq, Hkv, splits, single, tiles):
     _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits} tiles={tiles}")
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("splits", [4, 8, 16])
+@pytest.mark.parametrize("tiles", [1, 2])
+@pytest.mark.parametrize("tickets_on", [True, False])
+def test_attn_decode_wg_merge(gpu, Hq, Hkv, splits, tiles, tickets_on):
+    """4-wave workgroups (one split per wave, LDS merge): vs the fp32 oracle, decode and
+    extend rows, contexts shorter than the split count (empty splits), a padding work
+    item; the workgroups' partials merged in-kernel (tickets, reset after every launch)
+    or by the reduce launch."""
+    torch.manual_seed(7 + splits)
+    G = Hq // Hkv
+    cases = [(1, 1), (1, 31), (1, 33), (1, 700), (5, 129), (9, 2049), (3, 3), (1, 1100)]
+    qlens = [c[0] for c in cases]
+    kvlens = [c[1] for c in cases]
+    k, v = _paged_cache(512, Hkv, gpu, seed=9)
+    bt = _block_tables(kvlens, 512, gpu)
+    T = sum(qlens)
+    qs = [sum(qlens[:i]) for i in range(len(qlens))]
+    ws, wct = [], []
+    for i, ql in enumerate(qlens):
+        for ct in range(((ql * G + 15) // 16 + tiles - 1) // tiles):
+            ws.append(i)
+            wct.append(ct)
+    ws.append(-1)
+    wct.append(0)
+    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
+    q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
+    po = torch.empty(T * Hq * splits * 128, device=gpu)
+    pm = torch.empty(T * Hq * splits * 2, device=gpu)
+    scale = 1 / math.sqrt(128)
+    tickets = torch.zeros(len(ws) * Hkv, dtype=torch.int32, device=gpu) if tickets_on else None
+    exp = torch.zeros(T, Hq * 128, dtype=BF)
+    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
+                     torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
+    for it in range(3):
+        out = torch.full((T, Hq * 128), float("nan"), device=gpu, dtype=BF)
+        ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct), out,
+                        po, pm, Hq, Hkv, scale, splits, tiles, tickets, 4)
+        torch.cuda.synchronize()
+        if tickets is not None:
+            assert int(tickets.abs().sum()) == 0, "tickets not reset"
+        _close(out, exp, 2e-2, 0, f"wg-merge Hq={Hq} splits={splits} tiles={tiles} it={it}")
+
+
 @pytest.mark.parametrize("Hq,Hkv,tiles", [(32, 8, 1), (32, 8, 2), (8, 1, 1)])
 @pytest.mark.parametrize("share", [True, False])
 def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
@@ -674,6 +718,78 @@ def test_gemv_splitk(gpu, M, cfg, N, K):
         _close(out, want, 3e-2, 2e-2, f"gemv_splitk_norm cfg={cfg} it={it}")
     torch.cuda.synchronize()
     assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("cfg", [0, 2, 9, 13, 14])
+@pytest.mark.parametrize("F,K", [(3584, 8192), (512, 1024)])
+def test_gemv_splitk_swiglu(gpu, M, cfg, F, K):
+    """Split-K gate|up GEMV with the SwiGLU epilogue (TP=8 70B shard shape: F 3584,
+    K 8192) vs the fp32 torch op rounded like the unfused path (GEMM -> bf16 ->
+    silu_mul); repeated launches leave the tile tickets at zero."""
+    torch.manual_seed(M * 11 + cfg + F)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(2 * F, K, device=gpu) / math.sqrt(K)).to(BF)
+    part, tiles = ops.splitk_ws(gpu)
+    out = torch.empty(M, F, device=gpu, dtype=BF)
+    r = x.float() @ w.float().t()
+    gg, u = r[:, :F].to(BF).float(), r[:, F:].to(BF).float()
+    want = (gg * torch.sigmoid(gg)).to(BF).float() * u
+    for it in range(3):
+        torch.ops.rfq_amd.gemv_splitk_swiglu(x, w, out, part, tiles, cfg)
+        _close(out, want, 2e-2, 1e-2, f"gemv_splitk_swiglu cfg={cfg} it={it}")
+    torch.cuda.synchronize()
+    assert int(tiles.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("cfg", [0, 2, 9, 13])
+@pytest.mark.parametrize("Hq,Hkv,K", [(8, 1, 8192), (8, 2, 1024)])
+def test_gemv_splitk_rope_kv(gpu, M, cfg, Hq, Hkv, K):
+    """Split-K QKV GEMV with the RoPE + paged-KV-append epilogue (TP=8 70B shard:
+    Hq 8, Hkv 1, K 8192) == fp32 GEMM followed by the rope_kv oracle; padding rows
+    (slot -1) write nothing; tickets left at zero."""
+    torch.manual_seed(M * 17 + cfg + Hkv)
+    N = (Hq + 2 * Hkv) * 128
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    cos_sin = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(4 * 32, device=gpu)[:M].to(torch.int32)
+    if M > 1:
+        slots[-1] = -1
+    kc = torch.zeros(4, Hkv, 32, 128, device=gpu, dtype=BF)
+    vc = torch.zeros_like(kc)
+    qkv = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    part, tiles = ops.splitk_ws(gpu)
+    torch.ops.rfq_amd.gemv_splitk_rope(x, w, qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, part,
+                                       tiles, cfg)
+    exp = (x.float() @ w.float().t()).cpu()
+    kc_e, vc_e = torch.zeros(kc.shape), torch.zeros(vc.shape)
+    ref.rope_kv(exp, pos.cpu(), cos_sin.cpu(), slots.cpu(), kc_e, vc_e, Hq, Hkv)
+    q = Hq * 128
+    _close(qkv[:, :q], exp[:, :q], 2e-2, 1e-2, f"splitk rope q M={M} cfg={cfg}")
+    _close(kc, kc_e, 2e-2, 1e-2, f"splitk rope k cache M={M} cfg={cfg}")
+    _close(vc, vc_e, 2e-2, 1e-2, f"splitk v cache M={M} cfg={cfg}")
+    torch.cuda.synchronize()
+    assert int(tiles.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 40])
+@pytest.mark.parametrize("cfg", [12, 13, 14, 15])
+@pytest.mark.parametrize("N,K", [(8192, 1024), (512, 384), (1024, 3584)])
+def test_skinny_gemm_short_k_tail(gpu, M, cfg, N, K):
+    """Skinny GEMM on K ranges shorter than one unrolled step per wave (the TP=8 o
+    projection, K = 1024) and ragged tails (K = 3584: 28 k-steps over 4 / 8 waves):
+    the tail path issues every load before its MFMAs; vs the fp32 torch matmul."""
+    if K % 128:
+        pytest.skip("K % 128")
+    torch.manual_seed(M + cfg + K)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.skinny_gemm(x, w, y, cfg)
+    _close(y, x.float() @ w.float().t(), 2e-2, 1e-2, f"skinny tail M={M} cfg={cfg} K={K}")
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])

@@ -62,7 +62,7 @@ def run(B, C, P, shared, Hq=32, Hkv=8, q=1, tiles=2, splits=2, iters=20):
     return us, kv_bytes / us / 1e6
 
 
-def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20):
+def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1):
     """Batch-1 decode attention as the latency path runs it: L layers with their own
     KV caches, the L (split kernel [+ reduce]) launches captured in one hipGraph;
     returns µs per layer."""
@@ -82,11 +82,12 @@ def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20):
     out = torch.empty_like(qt)
     po = torch.empty(Hq * splits * 128, device=dev)
     pm = torch.empty(Hq * splits * 2, device=dev)
+    tickets = torch.zeros(items * Hkv, dtype=torch.int32, device=dev) if waves > 1 else None
 
     def body():
         for k, v in zip(ks, vs):
             ops.attn_decode(qt, k, v, bt, qs, ql, kvl, ws, wct, out, po, pm, Hq, Hkv,
-                            1 / math.sqrt(128), splits, tiles)
+                            1 / math.sqrt(128), splits, tiles, tickets, waves)
 
     body()
     torch.cuda.synchronize()
@@ -129,6 +130,17 @@ def main():
             for sp in (8, 16, 32):
                 row[f"s{sp}_us"] = round(run_latency(C, 8, 1, sp, L=80), 2)
             print(json.dumps(row), flush=True)
+        return
+    if os.environ.get("LAT_WG"):
+        # one split per wave (+ reduce launch) vs 4-wave workgroups merged in LDS with the
+        # in-kernel merge of the workgroups' partials; batch-1, 8B / 70B-TP1 / 70B-TP8 heads
+        for Hq, Hkv, L in ((32, 8, 32), (64, 8, 80), (8, 1, 80)):
+            for C in (512, 1024, 2048):
+                row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
+                for sp in (8, 16, 32):
+                    row[f"s{sp}_w1_us"] = round(run_latency(C, Hq, Hkv, sp, L=L), 2)
+                    row[f"s{sp}_w4_us"] = round(run_latency(C, Hq, Hkv, sp, L=L, waves=4), 2)
+                print(json.dumps(row), flush=True)
         return
     if os.environ.get("TILES_AB"):
         # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
