@@ -51,7 +51,10 @@ void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16
                                bool, hipStream_t);
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                         const int32_t*, int, bf16_t*, int64_t, int, int, float, int, hipStream_t);
+                         const int32_t*, int, bf16_t*, int64_t, int, int, float, int, int,
+                         float*, int32_t*, hipStream_t);
+int prefill_split_ws_floats();
+int prefill_split_tickets();
 void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t*, int,
                            const int32_t*, const float*, const uint64_t*, float*, int32_t*, int,
                            hipStream_t);
@@ -465,7 +468,9 @@ void attn_decode_shared(const Tensor& q, const Tensor& k_cache, const Tensor& v_
 void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& block_tables, const Tensor& seq_q_start, const Tensor& seq_q_len,
                   const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_qblk,
-                  const Tensor& out, int64_t Hq, int64_t Hkv, double scale, int64_t qblk) {
+                  const Tensor& out, int64_t Hq, int64_t Hkv, double scale, int64_t qblk,
+                  int64_t hsplit_below, const std::optional<Tensor>& ws,
+                  const std::optional<Tensor>& tickets) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
   CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
@@ -478,12 +483,28 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   const int64_t nw = qblk * (Hq / Hkv) / 32;
   TORCH_CHECK((qblk == 32 || qblk == 64) && (nw == 4 || nw == 8),
               "attn_prefill: qblk * (Hq / Hkv) must be 128 or 256 (4 or 8 waves)");
+  float* split_ws = nullptr;
+  int32_t* split_tk = nullptr;
+  if (ws.has_value() && tickets.has_value()) {
+    CHECK_DEV(*ws); CHECK_DEV(*tickets); CHECK_I32(*tickets);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= rfq::prefill_split_ws_floats() &&
+                    tickets->numel() >= rfq::prefill_split_tickets(),
+                "attn_prefill: split-KV workspace too small (ops.prefill_split_ws)");
+    split_ws = ws->data_ptr<float>();
+    split_tk = tickets->data_ptr<int32_t>();
+  }
   rfq::launch_attn_prefill(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
                            block_tables.data_ptr<int32_t>(), block_tables.stride(0),
                            seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
                            seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(),
                            work_qblk.data_ptr<int32_t>(), work_seq.numel(), bpm(out),
-                           out.stride(0), Hq, Hkv, (float)scale, (int)qblk, cur_stream());
+                           out.stride(0), Hq, Hkv, (float)scale, (int)qblk, (int)hsplit_below,
+                           split_ws, split_tk, cur_stream());
+}
+
+// sizes of the split-KV prefill workspace: (fp32 floats, int32 zeroed tickets)
+std::vector<int64_t> prefill_split_ws_sizes() {
+  return {rfq::prefill_split_ws_floats(), rfq::prefill_split_tickets()};
 }
 
 void sample_partial(const Tensor& logits, int64_t v0, const Tensor& mask_table,
@@ -865,7 +886,9 @@ TORCH_LIBRARY(rfq_amd, m) {
         "int Hq, int Hkv, float scale, int tiles_per_item, bool run_meta) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
-        "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale, int qblk=32) -> ()");
+        "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale, int qblk=32, "
+        "int hsplit_below=0, Tensor(b!)? ws=None, Tensor(c!)? tickets=None) -> ()");
+  m.def("prefill_split_ws_sizes() -> int[]", &prefill_split_ws_sizes);
   m.def("sample_partial(Tensor logits, int v0, Tensor mask_table, Tensor mask_idx, Tensor temps, "
         "Tensor seeds, Tensor(a!) part_val, Tensor(b!) part_idx) -> ()");
   m.def("sample_final(Tensor part_val, Tensor part_idx, Tensor(a!) out) -> ()");

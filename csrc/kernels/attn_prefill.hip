@@ -47,6 +47,8 @@ constexpr float kRescale = 8.f;         // defer-max threshold (log2 units)
 // by LDS-DMA into the slot tile t-1 vacated, so ONE barrier per tile suffices and
 // each tile's DMA has two tiles of latency cover.
 constexpr int kSlots = 4;
+constexpr int kMinSplitTiles = 3;       // key tiles per split workgroup, at least
+constexpr int kMaxKvSplit = 4;          // split workgroups per work item, at most
 typedef __attribute__((address_space(3))) char lds_c;
 typedef __attribute__((address_space(3))) const s16x8 lds_s16x8;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -58,7 +60,8 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_qblk, bf16_t* __restrict__ out, int64_t out_stride, int Hq,
-    int Hkv, float scale_log2) {
+    int Hkv, float scale_log2, int hgroups, int kvsplit = 1, float* __restrict__ ws = nullptr,
+    int32_t* __restrict__ tickets = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
   constexpr int NT = NW * 64;
@@ -67,13 +70,22 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r = lane & 31, h2 = lane >> 5;
   const int G = Hq / Hkv;
-  const int QB = NW * kQB / G;
-  const int num_work = gridDim.x / Hkv;
-  const int kvh = blockIdx.x % Hkv;
-  const int wi = num_work - 1 - blockIdx.x / Hkv;
+  // hgroups > 1 (small grids, e.g. one sequence at the TP = 8 rank shape Hq 8 / Hkv 1):
+  // the G query heads of a kv head are split over hgroups workgroups of HPW heads, so
+  // twice the workgroups share the causal critical path and each SIMD runs one wave
+  const int HPW = G / hgroups;
+  const int QB = NW / HPW * kQB;
+  // kvsplit = 2: the two workgroups of a (work item, kv head, head group) take the two
+  // halves of its key tiles and merge (below); adjacent in the grid, heaviest first
+  const int kvs = blockIdx.x % kvsplit;
+  const int bid = blockIdx.x / kvsplit;
+  const int num_work = gridDim.x / (Hkv * hgroups * kvsplit);
+  const int kvh = bid % Hkv;
+  const int hg = (bid / Hkv) % hgroups;
+  const int wi = num_work - 1 - bid / (Hkv * hgroups);
   const int seq = work_seq[wi];
-  const int head = kvh * G + wid % G;
-  const int qs = work_qblk[wi] * QB + (wid / G) * kQB;
+  const int head = kvh * G + hg * HPW + wid % HPW;
+  const int qs = work_qblk[wi] * QB + (wid / HPW) * kQB;
   const int q_len = seq_q_len[seq], kv_len = seq_kv_len[seq];
   const int ctx0 = kv_len - q_len;
   const int tok0 = seq_q_start[seq];
@@ -94,6 +106,15 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   const int w_kv_end = w_last_q < qs ? 0 : min(kv_len, ctx0 + w_last_q + 1);
   const int ntiles = (kv_end + kKT - 1) / kKT;
   const int wt = (w_kv_end + kKT - 1) / kKT;   // tiles this wave computes
+  // key tiles [t0, t1) of this workgroup: an item's tiles go to nact <= kvsplit
+  // workgroups of >= kMinSplitTiles tiles each; the others leave at once, and an
+  // unsplit item's first workgroup writes the output directly
+  const int nact = max(1, min(kvsplit, ntiles / kMinSplitTiles));
+  if (kvs >= nact) return;
+  const bool split = nact > 1;
+  const int t0 = kvs * ntiles / nact;
+  const int t1 = (kvs + 1) * ntiles / nact;
+  const int wend = min(wt, t1);
 
   lds_c* const lbase = (lds_c*)smem;
   // K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
@@ -300,23 +321,23 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   };
-  load(0);
-  if (ntiles > 1) load(1);
-  if (ntiles > 2) load(2);
-  wait_dma(ntiles > 2);
+  load(t0);
+  if (t0 + 1 < t1) load(t0 + 1);
+  if (t0 + 2 < t1) load(t0 + 2);
+  wait_dma(t0 + 2 < t1);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (wt > 0) {
-    qk(0);
+  if (wend > t0) {
+    qk(t0);
     sm_max();
 #pragma unroll
     for (int c = 0; c < 4; ++c) sm_exp(c, pb);
     sm_done();
   }
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 3 < ntiles) load(t + 3);
-    if (t < wt) {
-      if (t + 1 < wt) {
+  for (int t = t0; t < t1; ++t) {
+    if (t + 3 < t1) load(t + 3);
+    if (t < wend) {
+      if (t + 1 < wend) {
         qk(t + 1);
         s16x8 pn[4];
         pv_mfma(t, true, pn);
@@ -333,13 +354,87 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
         pv_mfma(t, false, nullptr);
       }
     }
-    wait_dma(t + 3 < ntiles);                   // tile t+2 landed (tile t+3 may fly)
+    wait_dma(t + 3 < t1);                       // tile t+2 landed (tile t+3 may fly)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
 
   float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (split) {
+    // Hand-off of the unnormalised O, running max (raw score units) and row sum between
+    // the two halves (cdna_hip_programming.md §6 Guideline 16, "every load sc1"): sc1
+    // 8-byte stores drained by vmcnt(0) + barrier, a relaxed agent-scope ticket, sc1
+    // loads of the partner's partial by the second arriver, which merges and writes the
+    // output; it resets the ticket for the next launch.  No fences, no L2 writeback.
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    constexpr int kPart = 64 * 64 + 64 * 2;               // floats per wave
+    float* mine = ws + (((int64_t)bid * kMaxKvSplit + kvs) * NW + wid) * kPart;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {                        // o[m][2jj..2jj+1], j = 8m + jj
+      const float a = o[j >> 3][2 * (j & 7)], b = o[j >> 3][2 * (j & 7) + 1];
+      __hip_atomic_store((gu64*)(mine + (j * 64 + lane) * 2),
+                         (unsigned long long)__float_as_uint(a) |
+                             ((unsigned long long)__float_as_uint(b) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store((gu64*)(mine + 4096 + lane * 2),
+                       (unsigned long long)__float_as_uint(m_run) |
+                           ((unsigned long long)__float_as_uint(l_tot) << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int s_second;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(tickets + bid, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      s_second = prev == nact - 1;
+      if (prev == nact - 1)
+        __hip_atomic_store(tickets + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_second) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
+    // every partner's (max, sum) first, then one rescale per partial
+    float m_p[kMaxKvSplit], l_p[kMaxKvSplit];
+    float m_n = m_run;
+#pragma unroll
+    for (int j = 0; j < kMaxKvSplit; ++j) {
+      m_p[j] = -INFINITY;
+      l_p[j] = 0.f;
+      if (j < nact && j != kvs) {
+        const float* other = ws + (((int64_t)bid * kMaxKvSplit + j) * NW + wid) * kPart;
+        const unsigned long long ml =
+            __hip_atomic_load((const gu64*)(other + 4096 + lane * 2), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+        m_p[j] = __uint_as_float((unsigned)ml);
+        l_p[j] = __uint_as_float((unsigned)(ml >> 32));
+        m_n = fmaxf(m_n, m_p[j]);
+      }
+    }
+    const float a_s = m_run == -INFINITY ? 0.f : fast_exp2((m_run - m_n) * scale_log2);
+    l_tot *= a_s;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) o[m] *= a_s;
+#pragma unroll
+    for (int j = 0; j < kMaxKvSplit; ++j) {
+      if (j >= nact || j == kvs) continue;
+      const float a_o = m_p[j] == -INFINITY ? 0.f : fast_exp2((m_p[j] - m_n) * scale_log2);
+      l_tot += l_p[j] * a_o;
+      const float* other = ws + (((int64_t)bid * kMaxKvSplit + j) * NW + wid) * kPart;
+      unsigned long long u[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        u[i] = __hip_atomic_load((const gu64*)(other + (i * 64 + lane) * 2), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const int m = i >> 3, e = 2 * (i & 7);
+        o[m][e] += __uint_as_float((unsigned)u[i]) * a_o;
+        o[m][e + 1] += __uint_as_float((unsigned)(u[i] >> 32)) * a_o;
+      }
+    }
+  }
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   bf16_t* ol = lds + wid * (kQB * kPD);
 #pragma unroll
@@ -363,29 +458,58 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   }
 }
 
+// Split-KV workspace (ws, tickets): per (work item, kv head, head group) 2 halves x 4
+// waves x (64 x 64 + 128) floats and one zeroed ticket; kPrefillSplitMaxWg bounds the
+// split grid (ops.prefill_split_ws allocates for it).
+constexpr int kPrefillSplitMaxWg = 256;
+int prefill_split_ws_floats() {
+  return (kPrefillSplitMaxWg / 2) * kMaxKvSplit * 4 * (64 * 64 + 64 * 2);
+}
+int prefill_split_tickets() { return kPrefillSplitMaxWg / 2; }
+
 // qblk: queries per work item (the packer's prefill block): NW = qblk * G / 32 waves.
+// hsplit_below: when num_work * Hkv is below this many workgroups (the grid cannot
+// fill the CUs) and the 8 waves are one query block of 8 heads (G = 8, qblk 32), the
+// heads are split over 2 workgroups of 4 waves (0 = never).
 void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                          const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
                          const int32_t* seq_q_start, const int32_t* seq_q_len,
                          const int32_t* seq_kv_len, const int32_t* work_seq,
                          const int32_t* work_qblk, int num_work, bf16_t* out, int64_t out_stride,
-                         int Hq, int Hkv, float scale, int qblk, hipStream_t s) {
+                         int Hq, int Hkv, float scale, int qblk, int hsplit_below,
+                         float* ws, int32_t* tickets, hipStream_t s) {
   if (num_work == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
   const int nw = qblk * G / kQB;
-  dim3 grid(num_work * Hkv);
   const size_t lds = kSlots * kStage * sizeof(bf16_t);    // 128 KB ring
+  if (nw == 8 && G == 8 && num_work * Hkv < hsplit_below) {
+    // kv split on top when the workspace is given and the doubled grid still fits the
+    // CUs once (one 128 KB-LDS workgroup per CU)
+    // 4 splits while the split grid is at most two rounds of the CUs (items with fewer
+    // tiles activate fewer), else 2 while it fits once
+    const int wg2 = num_work * Hkv * 2;
+    const int kvsplit = (ws == nullptr || tickets == nullptr) ? 1
+                        : (wg2 * 4 <= 2 * kPrefillSplitMaxWg ? 4
+                           : (wg2 * 2 <= kPrefillSplitMaxWg ? 2 : 1));
+    const dim3 grid2(num_work * Hkv * 2 * kvsplit);
+    attn_prefill_kernel<4><<<grid2, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
+                                                   scale_log2, 2, kvsplit, ws, tickets);
+    return;
+  }
+  dim3 grid(num_work * Hkv);
   if (nw == 8)
     attn_prefill_kernel<8><<<grid, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                  scale_log2);
+                                                  scale_log2, 1);
   else
     attn_prefill_kernel<4><<<grid, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                  scale_log2);
+                                                  scale_log2, 1);
 }
 
 }  // namespace rfq

@@ -507,13 +507,43 @@ def prefill_qblk(Hq: int, Hkv: int) -> int:
     return PREFILL_GROUPS[g]
 
 
+# prefill grids with fewer (work item x kv head) workgroups than this split the 8 query
+# heads of a kv head over two 4-wave workgroups (GQA group 8, e.g. the TP = 8 rank shard
+# of Llama-3-70B: one kv head); 0 = never.  profiles/r3_prefill_head_split.md
+PREFILL_HSPLIT_BELOW = int(os.environ.get("RFQ_PREFILL_HSPLIT_BELOW", "256"))
+
+
+# RFQ_PREFILL_KVSPLIT=0: no split-KV on top of the head split
+PREFILL_KVSPLIT = os.environ.get("RFQ_PREFILL_KVSPLIT", "1") != "0"
+
+
+def prefill_split_ws(device):
+    """(fp32 workspace, zeroed int32 tickets) of the split-KV prefill attention (the
+    kernel leaves the tickets at zero); one per device, allocated on first use."""
+    d = torch.device(device)
+    key = ("prefill_split", d)
+    ws = _NORM_COUNTERS.get(key)
+    if ws is None:
+        nf, nt = _native.ops().prefill_split_ws_sizes()
+        ws = _NORM_COUNTERS[key] = (torch.empty(nf, dtype=torch.float32, device=d),
+                                    torch.zeros(nt, dtype=torch.int32, device=d))
+    return ws
+
+
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
-                 work_seq, work_qblk, out, Hq, Hkv, scale, qblk: int = 32):
+                 work_seq, work_qblk, out, Hq, Hkv, scale, qblk: int = 32,
+                 hsplit_below: int | None = None, kvsplit: bool | None = None):
     """Causal paged prefill attention; the work list holds (sequence, query block of
-    ``qblk`` queries) items (qblk * Hq / Hkv must be 128 or 256)."""
+    ``qblk`` queries) items (qblk * Hq / Hkv must be 128 or 256).  Small grids at GQA
+    group 8 split the heads over two workgroups (``hsplit_below``) and, with
+    ``kvsplit``, the key tiles of each item over two more (merged in-kernel)."""
     if _gpu(q):
+        hs = PREFILL_HSPLIT_BELOW if hsplit_below is None else hsplit_below
+        ws, tk = prefill_split_ws(q.device) if (PREFILL_KVSPLIT if kvsplit is None
+                                                 else kvsplit) else (None, None)
         _native.ops().attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len,
-                                   seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale, qblk)
+                                   seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale, qblk,
+                                   hs, ws, tk)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
                          work_seq, work_qblk, out, Hq, Hkv, scale)

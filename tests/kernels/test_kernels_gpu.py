@@ -293,12 +293,21 @@ def test_attn_prefill(gpu, Hq, Hkv, qblk, spike):
     args = [torch.tensor(a, dtype=torch.int32, device=gpu) for a in (qlens, kvlens, ws, wq)]
     out = torch.zeros(T, Hq * 128, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(128)
-    ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out, Hq,
-                     Hkv, scale, qblk)
     exp = torch.zeros(T, Hq * 128, dtype=BF)
     ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), starts, args[0].cpu(), args[1].cpu(),
                      None, None, exp, Hq, Hkv, scale)
-    _close(out, exp, 2e-2, 0, f"attn_prefill Hq={Hq} qblk={qblk}")
+    # hsplit_below 0: one workgroup per (item, kv head); 4096: GQA group 8 split over two
+    # 4-wave workgroups (the small-grid form)
+    # kvsplit: the head-split form's items of >= 4 key tiles split over two workgroups
+    # (merged in-kernel; run twice, so the tickets must have been reset)
+    for hs, kvs in ((0, False), (4096, False), (4096, True), (4096, True)):
+        out.zero_()
+        ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out,
+                         Hq, Hkv, scale, qblk, hsplit_below=hs, kvsplit=kvs)
+        _close(out, exp, 2e-2, 0, f"attn_prefill Hq={Hq} qblk={qblk} hsplit={hs} kvsplit={kvs}")
+    if ops.native_available():
+        torch.cuda.synchronize()
+        assert int(ops.prefill_split_ws(gpu)[1].abs().sum()) == 0, "split tickets not reset"
 
 
 def test_sampler_masks_and_gumbel(gpu):
@@ -605,7 +614,7 @@ def test_linear_m_split_plan(gpu):
     torch.manual_seed(11)
     w = (torch.randn(512, 1024, device=gpu) * 0.03).to(BF)
     plan, _ = tune_split({"t": [w]}, {"t": 1024}, quantum=128, reps=1)
-    q, table, algos = plan[(512, 1024)]
+    q, table, algos = plan[(512, 1024)][:3]
     assert q == 128 and len(table) == 9 and len(algos) == 9
     forced = plan_splits([0.0] + [1.0] * 8 + [100.0], margin=1.0, launch_us=0.0)
     try:

@@ -32,8 +32,10 @@ def run(B, S, Hq, Hkv, iters=10):
     nqb = (S + qblk - 1) // qblk
     ws = torch.arange(B, dtype=torch.int32, device=dev).repeat_interleave(nqb)
     wq = torch.arange(nqb, dtype=torch.int32, device=dev).repeat(B)
+    hs = int(os.environ["HSPLIT"]) if "HSPLIT" in os.environ else None
+    kvs = os.environ["KVSPLIT"] != "0" if "KVSPLIT" in os.environ else None
     f = lambda: ops.attn_prefill(q, k, v, bt, qs, ql, kvl, ws, wq, out, Hq, Hkv,  # noqa: E731
-                                 1 / math.sqrt(128), qblk)
+                                 1 / math.sqrt(128), qblk, hsplit_below=hs, kvsplit=kvs)
     f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
