@@ -486,11 +486,13 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
   if (nw == 8 && G == 8 && num_work * Hkv < hsplit_below) {
     // kv split on top when the workspace is given and the doubled grid still fits the
     // CUs once (one 128 KB-LDS workgroup per CU)
-    // 4 splits while the split grid is at most two rounds of the CUs (items with fewer
-    // tiles activate fewer), else 2 while it fits once
+    // the most splits (4 or 2; items with fewer tiles activate fewer) whose grid still
+    // fits the CUs in one round: a second round of workgroups costs more than the
+    // shorter critical path saves (B1 S2048 Hq8/Hkv1: 4 splits over 512 workgroups
+    // 38-40 us vs 2 splits over 256: 34 us; profiles/r3_prefill_head_split.md)
     const int wg2 = num_work * Hkv * 2;
     const int kvsplit = (ws == nullptr || tickets == nullptr) ? 1
-                        : (wg2 * 4 <= 2 * kPrefillSplitMaxWg ? 4
+                        : (wg2 * 4 <= kPrefillSplitMaxWg ? 4
                            : (wg2 * 2 <= kPrefillSplitMaxWg ? 2 : 1));
     const dim3 grid2(num_work * Hkv * 2 * kvsplit);
     attn_prefill_kernel<4><<<grid2, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,

@@ -60,7 +60,8 @@ def run(B, S, Hq, Hkv, iters=10):
 
 def main():
     for B, S, Hq, Hkv in [(1, 2048, 32, 8), (4, 2048, 32, 8), (1, 2048, 8, 1), (8, 2048, 8, 1),
-                          (16, 512, 32, 8), (1, 8192, 32, 8)]:
+                          (16, 512, 32, 8), (1, 8192, 32, 8), (1, 1024, 8, 1), (1, 4096, 8, 1),
+                          (2, 2048, 8, 1)]:
         us, tf = run(B, S, Hq, Hkv)
         print(json.dumps({"B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "us": round(us, 1),
                           "TFLOPs": round(tf, 1), "pct_of_2.5PF": round(tf / 25.0, 1)}),
