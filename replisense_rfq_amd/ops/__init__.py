@@ -157,7 +157,7 @@ def splitk_ws(device):
 SPLITK_BIT = 128          # plan cfg bit: the split-K GEMV kernel (low bits = its cfg)
 # split-K GEMV cfgs timed by the start-up plans: KS = 2 << (c & 3), bit 2 = 8 waves,
 # bit 3 = U 2 (gemm_skinny.hip launch_gemv_splitk_epi)
-SPLITK_CFGS = (0, 1, 2, 8, 9, 10, 12, 13, 14)
+SPLITK_CFGS = (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14)
 
 
 def splitk_fits(device, cfg: int, M: int, n_rows: int, tiles: int) -> bool:

@@ -64,12 +64,16 @@ def _time(fn, ws, reps: int, graph: bool = True) -> float:
     return best
 
 
+LATENCY_MARGIN = float(os.environ.get("RFQ_LATENCY_LIB_MARGIN", "1.05"))
+
+
 def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, list[int]],
                 reps: int = 2, margin: float = 1.03) -> dict:
     """groups: name -> per-layer weights [N, K]; ms_by_group: name -> token counts.
     ``margin`` > 1: a hand-written kernel within 3 % of hipBLASLt is kept (at M <= 64
     the library's small-M tiles measured at parity at best, and the latency-path graphs
-    then launch only kernels this tree can tune and fuse)."""
+    then launch only kernels this tree can tune and fuse); at M <= 16 (the decode /
+    jump-forward steps of single requests) the tolerance is LATENCY_MARGIN."""
     ops = _native.ops()
     plan, report = {}, []
     for name, ws in groups.items():
@@ -82,7 +86,7 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
             x = torch.randn(M, K, device=ws[0].device, dtype=ws[0].dtype)
             out = torch.empty(M, N, device=x.device, dtype=x.dtype)
             t_lib = _time(lambda w: torch.matmul(x, w.t(), out=out), ws, reps)
-            best, t_best = -1, t_lib * margin
+            best, t_best = -1, t_lib * (LATENCY_MARGIN if M <= 16 else margin)
             for c in CANDIDATES:
                 if c & 1 and N % 32:
                     continue
@@ -133,10 +137,12 @@ def tune_silu_down(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin:
 
 
 def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated: bool,
-              reps: int = 2, margin: float = 0.97, eps: float = 1e-5):
+              reps: int = 2, margin: float = 1.02, eps: float = 1e-5):
     """o / down projection followed by the residual-add RMSNorm: the planned GEMM path
     (linear or silu_linear) + fused_add_rms_norm vs the skinny kernel that runs the
-    norm in its last workgroup (one launch instead of two)."""
+    norm in its last workgroup (one launch instead of two).  ``margin`` > 1: a fused
+    kernel within 2 % of the two-launch path is kept (one launch fewer per layer in
+    the captured graph, and no library GEMM on the latency path)."""
     from . import (NORM_FUSE_MAX_M, SPLITK_BIT, fused_add_rms_norm, linear, norm_counter,
                    norm_partials, splitk_ws)
 
@@ -172,7 +178,7 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
                 best, t_best = c, t
         # the split-K GEMV with the in-launch per-tile reduction + norm (plain x only;
         # tools/bench_gemv.py: KS 2-4, 4 waves, U 2-4 are its useful corner)
-        for c in ((8, 9, 12, 0) if not gated else ()):
+        for c in ((8, 9, 12, 13, 4, 5, 0) if not gated else ()):
             if (K // 128) < (2 << (c & 3)):
                 continue
             t = _time(lambda w, c=c: ops.gemv_splitk_norm(x, w, y, res, norm_w, eps, out,
