@@ -155,6 +155,13 @@ def _gemm_plan_summary() -> dict:
             if r[0].startswith("dense:") and isinstance(r[5], str) and "buckets" in r[5]}
 
 
+def _host_timers(engine) -> dict:
+    st = engine.runner.stats
+    return {"pack_s": st.get("pack_s", 0.0), "launch_s": st.get("launch_s", 0.0),
+            "wait_s": st.get("wait_s", 0.0), "post_s": engine.timers.get("post_s", 0.0),
+            "execute_s": engine.timers.get("execute_s", 0.0)}
+
+
 class _Heartbeat:
     """Rank 0 prints a progress line to stderr every ``period`` seconds, so a long
     silent phase (engine init, the timed window, the TP phase) never looks hung to
@@ -327,6 +334,7 @@ def main():
     if stream is not None:
         stream.finished.clear()
     steps0 = engine.num_steps
+    host0 = _host_timers(engine)
     barrier()
     sync()
     mark("timed")
@@ -336,6 +344,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     steps_timed = engine.num_steps - steps0
+    host = {k: round(v - host0[k], 3) for k, v in _host_timers(engine).items()}
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=engine.device if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -411,6 +420,9 @@ def main():
                        "timed_engine_steps": steps_timed,
                        "docs_completed_in_window_rank0": done_in_window,
                        "graph_steps": stats.get("graph_steps"), "steps": stats.get("steps"),
+                       # host seconds inside the timed window (rank 0): scheduler pack,
+                       # forward launch, device wait, post-processing (grammar, retire)
+                       "host_s": host,
                        "kv_blocks": stats.get("blocks"), "preempted": stats.get("preempted"),
                        "wall_s": round(time.perf_counter() - t_start, 1)},
         }

@@ -89,8 +89,10 @@ class ModelRunner:
         self._nonfinite = torch.zeros(1, dtype=torch.int32, device=self.device)
         if tp.enabled:
             self._setup_control_plane()
+        # host-side split of a step: pack (scheduler), launch (upload + forward + sampler
+        # enqueue), wait (device drain + token readback); forward_s = launch + wait
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
-                      "pack_s": 0.0}
+                      "pack_s": 0.0, "launch_s": 0.0, "wait_s": 0.0}
 
     def _decode_splits(self, NA: int, max_ctx: int, graph: bool) -> int:
         if NA == 0 or not self.is_cuda:
@@ -259,7 +261,10 @@ class ModelRunner:
             v = self._views(buf, header)
             logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
+        t1 = time.perf_counter()
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
+        self.stats["launch_s"] += t1 - t0
+        self.stats["wait_s"] += time.perf_counter() - t1
         if self.check_finite:
             bad = int(self._nonfinite[0])
             if bad:

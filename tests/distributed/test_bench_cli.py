@@ -172,6 +172,11 @@ def test_bench_driver_flags_time_budget():
     assert out["latency_slo_s"] == 30.0 and isinstance(out["slo_met_p99"], bool)
     assert out["config"]["profile"] == "synthetic" and out["config"]["in_flight_per_replica"] == 4
     assert out["vs_baseline"] is None
+    # host-side split of the timed window (scheduler, launch, device wait, post)
+    host = out["engine"]["host_s"]
+    assert {"pack_s", "launch_s", "wait_s", "post_s", "execute_s"} <= set(host)
+    assert all(v >= 0 for v in host.values())
+    assert host["execute_s"] <= out["ms_per_step"] * 20 / 1e3 + 1.0
 
 
 def test_bench_extra_phases_cpu():
