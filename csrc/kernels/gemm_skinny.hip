@@ -552,7 +552,14 @@ void launch_skinny_gemm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, in
 //             pairs: split K is what lets it use more than 40 CUs.
 enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
 
-template <int NW, int U, int EPI>
+//
+// TL (cfg bit 4): W is stored in the decode-tiled layout (ops.tile_weight): for
+// every 16-row tile T and 128-wide k block B, the four 16x32 MFMA A-fragments in
+// lane order, i.e. element ((T * K/128 + B) * 4 + j) * 512 + lane * 8 + e holds
+// W[16 T + (lane & 15)][128 B + 32 j + 8 (lane >> 4) + e].  Every wave load is then
+// 1 KB contiguous (8 whole 128-B lines) instead of 16 half lines of 16 rows, and a
+// tile's k-blocks follow each other: one sequential 4 KB stream per k-step.
+template <int NW, int U, int EPI, bool TL = false>
 __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
     bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part, int Nn,
@@ -579,8 +586,12 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
   const int sl0 = slice * nks_all / KS, nks = (slice + 1) * nks_all / KS - sl0;
   const int ks0 = sl0 + wave * nks / NW, ks1 = sl0 + (wave + 1) * nks / NW;
   const bf16_t* wp[NT];
+  // element step between k-steps (128 k) and between the four 32-k MFMA slices
+  constexpr int KSTEP = TL ? 2048 : 128, JSTEP = TL ? 512 : 32;
 #pragma unroll
-  for (int a = 0; a < NT; ++a) wp[a] = W + (int64_t)(row0[a] + r) * K + g * 8;
+  for (int a = 0; a < NT; ++a)
+    wp[a] = TL ? W + (int64_t)(row0[a] >> 4) * (K >> 7) * 2048 + lane * 8
+               : W + (int64_t)(row0[a] + r) * K + g * 8;
   const bool xv = r < M;
   const bf16_t* xp = X + (int64_t)(xv ? r : 0) * ldx + g * 8;
   const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -595,7 +606,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
 #pragma unroll
       for (int a = 0; a < NT; ++a)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * 128 + j * 32);
+        for (int j = 0; j < 4; ++j)
+          w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -620,7 +632,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
         for (int a = 0; a < NT; ++a)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * 128 + j * 32);
+            w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           x[u][j] = xv ? *reinterpret_cast<const s16x8*>(xp + (ks + u) * 128 + j * 32) : zero;
@@ -767,7 +779,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
 }
 
 // cfg bits: [1:0] KS = 2 << bits (2, 4, 8, 16); bit 2: 8 waves (else 4); bit 3: U = 2 (else 4;
-// U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones).
+// U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones);
+// bit 4: W in the decode-tiled layout (TL above).
 // part: fp32 [KS][M][Nn] (Nn = GEMM rows); tile_cnt: one zeroed uint32 per output tile
 // (left at zero).  ntile: N/16 (plain, norm), F/16 (swiglu), N/32 (rope).
 template <int EPI>
@@ -778,8 +791,12 @@ static void launch_gemv_splitk_epi(const bf16_t* X, int64_t ldx, const bf16_t* W
   const int KS = 2 << (cfg & 3);
   const dim3 grid(ntile * KS);
 #define GV_LAUNCH(nw, u)                                                                        \
-  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI>), grid, dim3(nw * 64), 0, s, X, ldx, W, K, \
-                     Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
+  if (cfg & 16)                                                                                 \
+    hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI, true>), grid, dim3(nw * 64), 0, s, X,    \
+                       ldx, W, K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off);           \
+  else                                                                                          \
+    hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI>), grid, dim3(nw * 64), 0, s, X, ldx, W,  \
+                       K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
   switch ((cfg >> 2) & 3) {
     case 0: GV_LAUNCH(4, 4); break;
     case 1: GV_LAUNCH(8, 4); break;

@@ -58,6 +58,13 @@ def resolve_device(spec: str, tp: TPContext) -> torch.device:
 class LLMEngine:
     def __init__(self, cfg: EngineConfig | None = None, tp: TPContext = SINGLE,
                  model=None, capture: bool = True):
+        # The engine loop hands the GIL back and forth with the threads around it (HTTP
+        # event loop, prompt tokenisers): every native call of a step (schedule_and_pack,
+        # the token readback, post) releases it, and taking it back waits up to one
+        # switch interval while another thread runs Python.  At the default 5 ms that is
+        # several ms of idle GPU per step (bench: pack 5.2 ms of a 113 ms step with the
+        # tokenizer thread busy); 0.5 ms bounds it.
+        sys.setswitchinterval(float(os.environ.get("RFQ_GIL_SWITCH_MS", "0.5")) / 1e3)
         self.cfg = cfg or EngineConfig()
         self.tp = tp
         self.device = resolve_device(self.cfg.device, tp)
@@ -77,6 +84,8 @@ class LLMEngine:
                                        moe_ep=self.cfg.moe_parallel == "ep")
         self.model = model or DecoderLM(self.model_cfg, self.device, tp, seed=self.cfg.seed,
                                         weights=weights, moe_ep=self.cfg.moe_parallel == "ep")
+        # before the KV pool is sized from the free memory: the tiled copies take theirs
+        self.tiled_bytes = self.model.tile_decode_weights() if self.cfg.tune_gemm else 0
         self.init_weights_s = time.perf_counter() - t0
         self.kv = KVCache(self.model_cfg, self.model.hkv, self._num_blocks(), self.device,
                           prefix_cache=self.cfg.prefix_cache)
@@ -327,11 +336,7 @@ class AsyncEngine:
     """
 
     def __init__(self, engine: LLMEngine):
-
-        # The HTTP event loop and this engine thread share the GIL; a short switch
-        # interval keeps the engine from waiting up to 5 ms for it between GPU steps.
-        sys.setswitchinterval(float(os.environ.get("RFQ_GIL_SWITCH_MS", "0.5")) / 1e3)
-        self.engine = engine
+        self.engine = engine          # (LLMEngine set the short GIL switch interval)
         self._inbox: queue.Queue = queue.Queue()
         self._stop = threading.Event()
         self._wake = threading.Event()

@@ -110,6 +110,31 @@ class DecoderLM:
         # all-gather before the next column-parallel GEMM.  0 = off (SURVEY.md §2.3 SP).
         self.sp_min_tokens = int(os.environ.get("RFQ_SP_MIN_TOKENS", "0"))
 
+    # ------------------------------------------------------- decode weight layout
+    TILED_PROJ = ("qkv", "o", "gate_up", "down")
+
+    def tile_decode_weights(self, mode: str | None = None) -> int:
+        """Decode-tiled copies of the per-layer projections (ops.tile_weight) for the
+        split-K GEMVs of small-batch decode steps: each wave load is then 1 KB of
+        contiguous weight bytes.  The row-major originals stay for every large-M GEMM,
+        so this costs one more copy of the projection weights: ``auto`` (RFQ_TILED_WEIGHTS,
+        default) tiles when that copy is at most 15 % of the device's memory (8B, the
+        70B TP=4/8 shards; not 70B at TP 1-2) and the model is dense.  The start-up plan
+        (ops.autotune) then times the tiled cfgs against everything else.  Returns bytes."""
+        mode = (mode or os.environ.get("RFQ_TILED_WEIGHTS", "auto")).lower()
+        if mode in ("0", "off", "false") or self.cfg.is_moe or self.device.type != "cuda":
+            return 0
+        ws = [lw[k] for lw in self.w["layers"] for k in self.TILED_PROJ if k in lw]
+        nbytes = sum(t.numel() * t.element_size() for t in ws)
+        if mode == "auto":
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            if nbytes > 0.15 * total:
+                return 0
+        for t in ws:
+            if t.shape[0] % 16 == 0 and t.shape[1] % 128 == 0:
+                ops.register_tiled(t, ops.tile_weight(t))
+        return nbytes
+
     # ------------------------------------------------------------------ KV pool
     def attach_kv_cache(self, k_pool: torch.Tensor, v_pool: torch.Tensor) -> None:
         """Pools shaped [L, num_blocks, Hkv_local, 32, 128]."""

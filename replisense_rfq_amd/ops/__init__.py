@@ -21,7 +21,8 @@ __all__ = [
     "set_norm_plan", "norm_plan", "norm_counter", "norm_partials", "linear_add_norm",
     "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
-    "gemm_dense", "gemm_dense_ok", "swiglu_large",
+    "gemm_dense", "gemm_dense_ok", "swiglu_large", "tile_weight", "untile_weight",
+    "register_tiled", "tiled_of", "clear_tiled", "SPLITK_TILED",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -160,6 +161,64 @@ SPLITK_BIT = 128          # plan cfg bit: the split-K GEMV kernel (low bits = it
 SPLITK_CFGS = (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14)
 
 
+SPLITK_TILED = 16        # split-K GEMV cfg bit: W in the decode-tiled layout (tile_weight)
+
+
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """Decode-tiled copy of a [N, K] weight (gemm_skinny.hip gemv_splitk, TL): for each
+    16-row tile and 128-wide k block, the four 16x32 MFMA A-fragments in lane order, so
+    every wave-wide load of the split-K GEMV reads 1 KB of contiguous memory.  Same
+    shape and dtype as ``w``; only the element order differs."""
+    N, K = w.shape
+    if N % 16 or K % 128:
+        raise ValueError(f"tile_weight: N % 16 == 0 and K % 128 == 0 required, got {N}x{K}")
+    return (w.view(N // 16, 16, K // 128, 4, 4, 8).permute(0, 2, 3, 4, 1, 5)
+            .contiguous().view(N, K))
+
+
+# data_ptr of a row-major projection weight -> its decode-tiled copy.  Filled when the
+# model is built (DecoderLM.tile_decode_weights); split-K GEMV plan entries with the
+# SPLITK_TILED bit read the copy, everything else the row-major original.
+# Entries die with their weight (weakref finalizer), so an engine torn down in the
+# same process frees its copies and a later weight at a reused address never matches.
+_TILED: dict[int, tuple] = {}
+
+
+def register_tiled(w: torch.Tensor, wt: torch.Tensor) -> None:
+    import weakref
+
+    key = w.data_ptr()
+    _TILED[key] = (weakref.ref(w), wt)
+    weakref.finalize(w, _TILED.pop, key, None)
+
+
+def tiled_of(w: torch.Tensor) -> torch.Tensor | None:
+    e = _TILED.get(w.data_ptr())
+    return e[1] if e is not None and e[0]() is w else None
+
+
+def clear_tiled() -> None:
+    _TILED.clear()
+
+
+def _wsel(w: torch.Tensor, cfg: int) -> torch.Tensor:
+    """The weight a split-K GEMV cfg reads: the tiled copy under SPLITK_TILED."""
+    if cfg & SPLITK_TILED:
+        wt = tiled_of(w)
+        if wt is None:
+            raise RuntimeError("split-K plan selects the tiled layout but the weight has no "
+                               "tiled copy (ops.register_tiled)")
+        return wt
+    return w
+
+
+def untile_weight(wt: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`tile_weight`."""
+    N, K = wt.shape
+    return (wt.view(N // 16, K // 128, 4, 4, 16, 8).permute(0, 4, 1, 2, 3, 5)
+            .contiguous().view(N, K))
+
+
 def splitk_fits(device, cfg: int, M: int, n_rows: int, tiles: int) -> bool:
     """Whether the shared split-K workspace holds a launch (KS*M*n_rows partial floats,
     ``tiles`` ticket counters)."""
@@ -182,7 +241,7 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     if cfg & SPLITK_BIT:
         part, tiles = splitk_ws(x.device)
-        _native.ops().gemv_splitk_norm(x, w, y, residual, norm_w, eps, out,
+        _native.ops().gemv_splitk_norm(x, _wsel(w, cfg), y, residual, norm_w, eps, out,
                                        norm_counter(x.device), part, tiles, cfg & 127)
         return True
     _native.ops().skinny_gemm_norm(x, w, y, residual, norm_w, eps, out,
@@ -216,7 +275,7 @@ def linear_swiglu(x, w):
             out = torch.empty((M, F), dtype=x.dtype, device=x.device)
             if cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
-                _native.ops().gemv_splitk_swiglu(x, w, out, part, tiles, cfg & 127)
+                _native.ops().gemv_splitk_swiglu(x, _wsel(w, cfg), out, part, tiles, cfg & 127)
             else:
                 _native.ops().skinny_gemm_swiglu(x, w, out, cfg)
             return out
@@ -253,8 +312,9 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
             qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
             if cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
-                _native.ops().gemv_splitk_rope(x, w, qkv, positions, cos_sin, slot_mapping,
-                                               k_cache, v_cache, Hq, Hkv, part, tiles, cfg & 127)
+                _native.ops().gemv_splitk_rope(x, _wsel(w, cfg), qkv, positions, cos_sin,
+                                               slot_mapping, k_cache, v_cache, Hq, Hkv, part,
+                                               tiles, cfg & 127)
             else:
                 _native.ops().skinny_gemm_rope(x, w, qkv, positions, cos_sin, slot_mapping,
                                                k_cache, v_cache, Hq, Hkv, cfg)
@@ -358,7 +418,7 @@ def linear(x, w, out=None, plan: int | None = None):
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
             if cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
-                _native.ops().gemv_splitk(x, w, out, part, tiles, cfg & 127)
+                _native.ops().gemv_splitk(x, _wsel(w, cfg), out, part, tiles, cfg & 127)
                 return out
             _native.ops().skinny_gemm(x, w, out, cfg)
             return out

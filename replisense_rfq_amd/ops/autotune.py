@@ -14,9 +14,9 @@ import os
 
 import torch
 
-from . import (SPLITK_BIT, SPLITK_CFGS, _native, gemm_dense_ok, set_linear_plan, set_norm_plan,
-               set_rope_plan, set_silu_plan, set_split_plan, set_swiglu_plan, silu_linear,
-               silu_mul, splitk_fits, splitk_ws)
+from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
+               set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan, set_split_plan,
+               set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of)
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -67,6 +67,13 @@ def _time(fn, ws, reps: int, graph: bool = True) -> float:
 LATENCY_MARGIN = float(os.environ.get("RFQ_LATENCY_LIB_MARGIN", "1.05"))
 
 
+def _splitk_cands(ws: list[torch.Tensor], base=SPLITK_CFGS) -> tuple:
+    """Split-K GEMV cfgs to time: ``base`` on the row-major weights, and the same cfgs
+    on the decode-tiled copies (SPLITK_TILED) when every layer has one."""
+    tiled = all(tiled_of(w) is not None for w in ws)
+    return tuple(base) + (tuple(c | SPLITK_TILED for c in base) if tiled else ())
+
+
 def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, list[int]],
                 reps: int = 2, margin: float = 1.03) -> dict:
     """groups: name -> per-layer weights [N, K]; ms_by_group: name -> token counts.
@@ -97,10 +104,11 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
                 # split-K GEMV (KS workgroups per 16-row tile, in-launch reduction): short
                 # N or short K shapes that leave CUs idle with one workgroup per tile
                 part, tiles = splitk_ws(x.device)
-                for c in SPLITK_CFGS:
+                for c in _splitk_cands(ws):
                     if K // 128 < (2 << (c & 3)) or not splitk_fits(x.device, c, M, N, N // 16):
                         continue
-                    t = _time(lambda w, c=c: ops.gemv_splitk(x, w, out, part, tiles, c), ws, reps)
+                    t = _time(lambda w, c=c: ops.gemv_splitk(x, _wsel(w, c), out, part, tiles, c),
+                              ws, reps)
                     if t < t_best:
                         best, t_best = c | SPLITK_BIT, t
             plan[(M, N, K)] = best
@@ -178,11 +186,11 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
                 best, t_best = c, t
         # the split-K GEMV with the in-launch per-tile reduction + norm (plain x only;
         # tools/bench_gemv.py: KS 2-4, 4 waves, U 2-4 are its useful corner)
-        for c in ((8, 9, 12, 13, 4, 5, 0) if not gated else ()):
+        for c in (_splitk_cands(ws, (8, 9, 12, 13, 4, 5, 0)) if not gated else ()):
             if (K // 128) < (2 << (c & 3)):
                 continue
-            t = _time(lambda w, c=c: ops.gemv_splitk_norm(x, w, y, res, norm_w, eps, out,
-                                                          counter, part, tiles, c), ws, reps)
+            t = _time(lambda w, c=c: ops.gemv_splitk_norm(x, _wsel(w, c), y, res, norm_w, eps,
+                                                          out, counter, part, tiles, c), ws, reps)
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
         if best >= 0:
@@ -217,10 +225,11 @@ def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: fl
             if t < t_best:
                 best, t_best = c, t
         part, tiles = splitk_ws(dev)
-        for c in SPLITK_CFGS:
+        for c in _splitk_cands(ws):
             if K // 128 < (2 << (c & 3)) or not splitk_fits(dev, c, M, N2, F // 16):
                 continue
-            t = _time(lambda w, c=c: ops.gemv_splitk_swiglu(x, w, act, part, tiles, c), ws, reps)
+            t = _time(lambda w, c=c: ops.gemv_splitk_swiglu(x, _wsel(w, c), act, part, tiles, c),
+                      ws, reps)
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
         if best >= 0:
@@ -265,11 +274,12 @@ def tune_rope(ws: list[torch.Tensor], ms: list[int], cos_sin: torch.Tensor, hq: 
             if t < t_best:
                 best, t_best = c, t
         part, tiles = splitk_ws(dev)
-        for c in SPLITK_CFGS:
+        for c in _splitk_cands(ws):
             if K // 128 < (2 << (c & 3)) or not splitk_fits(dev, c, M, N, N // 32):
                 continue
-            t = _time(lambda w, c=c: ops.gemv_splitk_rope(x, w, qkv, pos, cos_sin, slots, kc, vc,
-                                                          hq, hkv, part, tiles, c), ws, reps)
+            t = _time(lambda w, c=c: ops.gemv_splitk_rope(x, _wsel(w, c), qkv, pos, cos_sin, slots,
+                                                          kc, vc, hq, hkv, part, tiles, c),
+                      ws, reps)
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
         if best >= 0:
@@ -451,7 +461,9 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
         for r in xreport:
             log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d lib %.1fus -> %s %.1fus", *r)
     for r in report:
-        sel = "lib" if r[5] < 0 else (f"splitk{r[5] & 127}" if r[5] & SPLITK_BIT else f"skinny{r[5]}")
+        sel = "lib" if r[5] < 0 else (
+            (f"splitk{r[5] & 15}" + ("t" if r[5] & SPLITK_TILED else ""))
+            if r[5] & SPLITK_BIT else f"skinny{r[5]}")
         log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
                  r[0], r[1], r[2], r[3], r[4], sel, r[6])
     return report

@@ -31,3 +31,20 @@ def test_engine_build_rejects_group16(monkeypatch):
     monkeypatch.setattr(E, "get_config", lambda name: bad if name == "tiny-g16" else get_config(name))
     with pytest.raises(ValueError, match="GQA groups"):
         LLMEngine(EngineConfig(model="tiny-g16", device="cpu", max_num_seqs=2))
+
+
+def test_tile_weight_layout():
+    """Decode-tiled weight layout of the split-K GEMV (gemm_skinny.hip TL): element
+    ((T * K/128 + B) * 4 + j) * 512 + lane * 8 + e = W[16T + lane%16][128B + 32j +
+    8(lane//16) + e]; untile_weight inverts it; shapes outside the tiling rejected."""
+    import torch
+
+    w = torch.randn(48, 384)
+    t = ops.tile_weight(w)
+    assert t.shape == w.shape and torch.equal(ops.untile_weight(t), w)
+    flat = t.reshape(-1)
+    for T, B, j, lane, e in [(0, 0, 0, 0, 0), (2, 1, 3, 37, 5), (1, 2, 1, 63, 7)]:
+        off = ((T * 3 + B) * 4 + j) * 512 + lane * 8 + e
+        assert flat[off] == w[16 * T + lane % 16, 128 * B + 32 * j + 8 * (lane // 16) + e]
+    with pytest.raises(ValueError):
+        ops.tile_weight(torch.randn(40, 384))

@@ -784,6 +784,61 @@ def test_gemv_splitk_rope_kv(gpu, M, cfg, Hq, Hkv, K):
     assert int(tiles.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("cfg", [0, 5, 10, 14])
+def test_gemv_splitk_tiled_layout(gpu, M, cfg):
+    """Split-K GEMV on the decode-tiled weight layout (ops.tile_weight, cfg bit 16):
+    the same loads in a different memory order, so every epilogue (plain, norm, SwiGLU,
+    RoPE + KV append) is bit-identical to the row-major kernel, which the fp32 oracles
+    above cover; plus the plain result vs fp32 torch."""
+    torch.manual_seed(M * 29 + cfg)
+    T = ops.SPLITK_TILED
+    part, tiles = ops.splitk_ws(gpu)
+    N, K = 1024, 2048
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    wt = ops.tile_weight(w)
+    assert torch.equal(ops.untile_weight(wt), w)
+    y0, y1 = (torch.empty(M, N, device=gpu, dtype=BF) for _ in range(2))
+    torch.ops.rfq_amd.gemv_splitk(x, w, y0, part, tiles, cfg)
+    torch.ops.rfq_amd.gemv_splitk(x, wt, y1, part, tiles, cfg | T)
+    assert torch.equal(y0, y1)
+    _close(y1, x.float() @ w.float().t(), 2e-2, 1e-2, f"tiled gemv cfg={cfg}")
+    # residual-add RMSNorm epilogue
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
+    res = torch.randn(M, N, device=gpu, dtype=BF)
+    outs = []
+    for ww, c in ((w, cfg), (wt, cfg | T)):
+        r = res.clone()
+        o = torch.empty(M, N, device=gpu, dtype=BF)
+        torch.ops.rfq_amd.gemv_splitk_norm(x, ww, y0, r, nw, 1e-5, o, ops.norm_counter(gpu),
+                                           part, tiles, c)
+        outs.append((r, o))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # SwiGLU epilogue (gate rows [0, F), up rows [F, 2F))
+    F = N // 2
+    a0, a1 = (torch.empty(M, F, device=gpu, dtype=BF) for _ in range(2))
+    torch.ops.rfq_amd.gemv_splitk_swiglu(x, w, a0, part, tiles, cfg)
+    torch.ops.rfq_amd.gemv_splitk_swiglu(x, wt, a1, part, tiles, cfg | T)
+    assert torch.equal(a0, a1)
+    # RoPE + paged KV append (Hq 6, Hkv 1: N = 1024)
+    cos_sin = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(4 * 32, device=gpu)[:M].to(torch.int32)
+    got = []
+    for ww, c in ((w, cfg), (wt, cfg | T)):
+        kc = torch.zeros(4, 1, 32, 128, device=gpu, dtype=BF)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros((M, N), device=gpu, dtype=BF)
+        torch.ops.rfq_amd.gemv_splitk_rope(x, ww, q, pos, cos_sin, slots, kc, vc, 6, 1, part,
+                                           tiles, c)
+        got.append((q[:, :768], kc, vc))
+    for u, v in zip(*got):
+        assert torch.equal(u, v)
+    torch.cuda.synchronize()
+    assert int(tiles.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 40])
 @pytest.mark.parametrize("cfg", [12, 13, 14, 15])
 @pytest.mark.parametrize("N,K", [(8192, 1024), (512, 384), (1024, 3584)])
