@@ -52,7 +52,7 @@ void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16
 void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                          const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                          const int32_t*, int, bf16_t*, int64_t, int, int, float, int, int,
-                         float*, int32_t*, hipStream_t);
+                         float*, int32_t*, int, hipStream_t);
 int prefill_split_ws_floats();
 int prefill_split_tickets();
 void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t*, int,
@@ -470,7 +470,7 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_qblk,
                   const Tensor& out, int64_t Hq, int64_t Hkv, double scale, int64_t qblk,
                   int64_t hsplit_below, const std::optional<Tensor>& ws,
-                  const std::optional<Tensor>& tickets) {
+                  const std::optional<Tensor>& tickets, int64_t small_mode) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
   CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
@@ -499,7 +499,7 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                            seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(),
                            work_qblk.data_ptr<int32_t>(), work_seq.numel(), bpm(out),
                            out.stride(0), Hq, Hkv, (float)scale, (int)qblk, (int)hsplit_below,
-                           split_ws, split_tk, cur_stream());
+                           split_ws, split_tk, (int)small_mode, cur_stream());
 }
 
 // sizes of the split-KV prefill workspace: (fp32 floats, int32 zeroed tickets)
@@ -791,6 +791,8 @@ void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   const int64_t n_out = swiglu ? N / 2 : N;
   TORCH_CHECK(w.size(1) == K && K % 64 == 0 && K >= 64, "gemm_dense: w [N, K], K % 64 == 0");
+  TORCH_CHECK(!(cfg & 4) || (K % 128 == 0 && w.size(0) % 16 == 0 && w.is_contiguous()),
+              "gemm_dense: the decode-tiled weight layout (cfg bit 2) needs K % 128 == 0");
   TORCH_CHECK(swiglu ? (N % 256 == 0) : (N % 256 == 0),
               "gemm_dense: N % 256 == 0 (2F with F % 128 == 0 for swiglu)");
   TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "gemm_dense: out shape");
@@ -887,7 +889,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale, int qblk=32, "
-        "int hsplit_below=0, Tensor(b!)? ws=None, Tensor(c!)? tickets=None) -> ()");
+        "int hsplit_below=0, Tensor(b!)? ws=None, Tensor(c!)? tickets=None, "
+        "int small_mode=0) -> ()");
   m.def("prefill_split_ws_sizes() -> int[]", &prefill_split_ws_sizes);
   m.def("sample_partial(Tensor logits, int v0, Tensor mask_table, Tensor mask_idx, Tensor temps, "
         "Tensor seeds, Tensor(a!) part_val, Tensor(b!) part_idx) -> ()");

@@ -458,12 +458,12 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   }
 }
 
-// Split-KV workspace (ws, tickets): per (work item, kv head, head group) 2 halves x 4
-// waves x (64 x 64 + 128) floats and one zeroed ticket; kPrefillSplitMaxWg bounds the
+// Split-KV workspace (ws, tickets): per (work item, kv head, head group) up to 4 splits
+// x up to 8 waves x (64 x 64 + 128) floats and one zeroed ticket; kPrefillSplitMaxWg bounds the
 // split grid (ops.prefill_split_ws allocates for it).
 constexpr int kPrefillSplitMaxWg = 256;
 int prefill_split_ws_floats() {
-  return (kPrefillSplitMaxWg / 2) * kMaxKvSplit * 4 * (64 * 64 + 64 * 2);
+  return (kPrefillSplitMaxWg / 2) * kMaxKvSplit * 8 * (64 * 64 + 64 * 2);   // <= 8 waves
 }
 int prefill_split_tickets() { return kPrefillSplitMaxWg / 2; }
 
@@ -477,12 +477,36 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
                          const int32_t* seq_kv_len, const int32_t* work_seq,
                          const int32_t* work_qblk, int num_work, bf16_t* out, int64_t out_stride,
                          int Hq, int Hkv, float scale, int qblk, int hsplit_below,
-                         float* ws, int32_t* tickets, hipStream_t s) {
+                         float* ws, int32_t* tickets, int small_mode, hipStream_t s) {
   if (num_work == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
   const int nw = qblk * G / kQB;
   const size_t lds = kSlots * kStage * sizeof(bf16_t);    // 128 KB ring
+  // Small grids (num_work * Hkv < hsplit_below), two forms:
+  //   head split (small_mode 1): G = 8 heads over two 4-wave workgroups, split-KV 2-4 on
+  //     top while the grid fits the CUs once;
+  //   8-wave split-KV (small_mode 2): all G heads in one 8-wave workgroup (two waves per
+  //     SIMD), the key tiles split 2-4 ways.
+  // small_mode 0 (auto) takes the head split while it can also split the keys (grids up
+  // to 64 workgroups) and the 8-wave split-KV above that: B1 S4096 Hq8/Hkv1 98 -> 76 us,
+  // B2 S2048 54 -> 46 us, B1 S2048 34 either way, B1 S1024 19 vs 25 us
+  // (profiles/r3_prefill_kv8.md).
+  const int wg0 = num_work * Hkv;
+  const bool small = nw == 8 && wg0 < hsplit_below && ws != nullptr && tickets != nullptr;
+  const bool kv8 = small && (small_mode == 2 ||
+                             (small_mode == 0 && wg0 * 4 > kPrefillSplitMaxWg &&
+                              wg0 * 2 <= kPrefillSplitMaxWg));
+  if (kv8) {
+    const int wg = wg0;
+    const int kvsplit = wg * 4 <= kPrefillSplitMaxWg ? 4 : (wg * 2 <= kPrefillSplitMaxWg ? 2 : 1);
+    const dim3 grid8(wg * kvsplit);
+    attn_prefill_kernel<8><<<grid8, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
+                                                   scale_log2, 1, kvsplit, ws, tickets);
+    return;
+  }
   if (nw == 8 && G == 8 && num_work * Hkv < hsplit_below) {
     // kv split on top when the workspace is given and the doubled grid still fits the
     // CUs once (one 128 KB-LDS workgroup per CU)

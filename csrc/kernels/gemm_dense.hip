@@ -62,7 +62,14 @@ __device__ __forceinline__ void gbar() {
 // of ONE expert (the second absent when the expert has an odd block count: its rows
 // are neither loaded past the buffer nor stored); live tiles are enumerated
 // expert-major from the device-side offsets, so no host sync and a fixed grid.
-template <int EPI, int MF, int PH, int ABL = 0, bool GROUPED = false>
+// TLW: w is stored in the decode-tiled layout of the split-K GEMVs (ops.tile_weight;
+// gemm_skinny.hip TL), for models that keep only that copy of a projection.  A 16-byte
+// chunk (row, k0 + 8 gch) of a 64-deep K-tile then sits at
+//   (row >> 4) K/128 2048 + (row & 15) 8 + (gch >> 2) 512 + (gch & 3) 128
+//   + (k0 >> 7) 2048 + ((k0 >> 6) & 1) 1024,
+// i.e. a per-lane base plus a K-tile term; the LDS image and everything after the DMA
+// are unchanged, so the result is bit-identical to the row-major kernel.
+template <int EPI, int MF, int PH, int ABL = 0, bool GROUPED = false, bool TLW = false>
 __global__ __launch_bounds__(512) void gemm_dense_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
     bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off, int tiles_m, int tiles_n,
@@ -179,7 +186,9 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
       } else {
         wrow = tn * kGN + j;
       }
-      src_off[i] = wrow * (int)ldw + 8 * gch;                   // from w (this expert's)
+      src_off[i] = TLW ? (wrow >> 4) * (K >> 7) * 2048 + (wrow & 15) * 8 + (gch >> 2) * 512 +
+                             (gch & 3) * 128
+                       : wrow * (int)ldw + 8 * gch;             // from w (this expert's)
       dst_off[i] = (2 + (piece >> 4)) * kGHalf + (piece & 15) * 512;
       src_is_w[i] = true;
     }
@@ -190,7 +199,8 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
 #pragma unroll
     for (int pp = 0; pp < PPS; ++pp) {
       const int i = PPS * slot + pp;
-      const bf16_t* src = (src_is_w[i] ? wt : xt) + src_off[i] + k0;
+      const int kk = (TLW && src_is_w[i]) ? (k0 >> 7) * 2048 + ((k0 >> 6) & 1) * 1024 : k0;
+      const bf16_t* src = (src_is_w[i] ? wt : xt) + src_off[i] + kk;
       __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(st + dst_off[i]), 16, 0, 0);
     }
   };
@@ -440,7 +450,8 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   const int tiles_m = (M + kGM - 1) / kGM;
   const int tiles_n = swiglu ? n_out / 128 : n_out / kGN;
   const int grid = tiles_m * tiles_n;
-  // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile
+  // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile;
+  // bit 2: w in the decode-tiled layout (16x16x32, 2 phases)
 #define RFQ_GD_LAUNCH(E, F, P) \
   gemm_dense_kernel<E, F, P><<<grid, 512, kGLds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off, \
                                                       tiles_m, tiles_n, nullptr, 0, 0)
@@ -467,6 +478,15 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
       default: RFQ_GD_ABL(6); break;
     }
 #undef RFQ_GD_ABL
+    return;
+  }
+  if (cfg & 4) {   // w in the decode-tiled layout (16x32 MFMA, 2 phases per K-tile)
+    if (swiglu)
+      gemm_dense_kernel<EPI_SWIGLU, 16, 2, 0, false, true><<<grid, 512, kGLds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, nullptr, 0, 0);
+    else
+      gemm_dense_kernel<EPI_STORE, 16, 2, 0, false, true><<<grid, 512, kGLds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, nullptr, 0, 0);
     return;
   }
   if (swiglu) { RFQ_GD_EPI(EPI_SWIGLU) } else { RFQ_GD_EPI(EPI_STORE) }

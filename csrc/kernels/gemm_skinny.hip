@@ -559,7 +559,9 @@ enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
 // W[16 T + (lane & 15)][128 B + 32 j + 8 (lane >> 4) + e].  Every wave load is then
 // 1 KB contiguous (8 whole 128-B lines) instead of 16 half lines of 16 rows, and a
 // tile's k-blocks follow each other: one sequential 4 KB stream per k-step.
-template <int NW, int U, int EPI, bool TL = false>
+// NTL (cfg bit 5): weight loads non-temporal (nt): each weight byte is read once per
+// step by one CU, so it need not displace the activations / partials in L2.
+template <int NW, int U, int EPI, bool TL = false, bool NTL = false>
 __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
     bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part, int Nn,
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
       for (int a = 0; a < NT; ++a)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
+          w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
         for (int a = 0; a < NT; ++a)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            w[u][a][j] = ldw<false>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
+            w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           x[u][j] = xv ? *reinterpret_cast<const s16x8*>(xp + (ks + u) * 128 + j * 32) : zero;
@@ -780,7 +782,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
 
 // cfg bits: [1:0] KS = 2 << bits (2, 4, 8, 16); bit 2: 8 waves (else 4); bit 3: U = 2 (else 4;
 // U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones);
-// bit 4: W in the decode-tiled layout (TL above).
+// bit 4: W in the decode-tiled layout (TL above); bit 5: non-temporal weight loads (NTL).
 // part: fp32 [KS][M][Nn] (Nn = GEMM rows); tile_cnt: one zeroed uint32 per output tile
 // (left at zero).  ntile: N/16 (plain, norm), F/16 (swiglu), N/32 (rope).
 template <int EPI>
@@ -790,13 +792,16 @@ static void launch_gemv_splitk_epi(const bf16_t* X, int64_t ldx, const bf16_t* W
                                    int up_off, hipStream_t s) {
   const int KS = 2 << (cfg & 3);
   const dim3 grid(ntile * KS);
+#define GV_LAUNCH1(nw, u, tl, nt)                                                               \
+  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI, tl, nt>), grid, dim3(nw * 64), 0, s, X, ldx, \
+                     W, K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
 #define GV_LAUNCH(nw, u)                                                                        \
-  if (cfg & 16)                                                                                 \
-    hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI, true>), grid, dim3(nw * 64), 0, s, X,    \
-                       ldx, W, K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off);           \
-  else                                                                                          \
-    hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI>), grid, dim3(nw * 64), 0, s, X, ldx, W,  \
-                       K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
+  switch ((cfg >> 4) & 3) {                                                                     \
+    case 0: GV_LAUNCH1(nw, u, false, false); break;                                             \
+    case 1: GV_LAUNCH1(nw, u, true, false); break;                                              \
+    case 2: GV_LAUNCH1(nw, u, false, true); break;                                              \
+    default: GV_LAUNCH1(nw, u, true, true); break;                                              \
+  }
   switch ((cfg >> 2) & 3) {
     case 0: GV_LAUNCH(4, 4); break;
     case 1: GV_LAUNCH(8, 4); break;
@@ -804,6 +809,7 @@ static void launch_gemv_splitk_epi(const bf16_t* X, int64_t ldx, const bf16_t* W
     default: GV_LAUNCH(8, 2); break;
   }
 #undef GV_LAUNCH
+#undef GV_LAUNCH1
 }
 
 void launch_gemv_splitk_norm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,

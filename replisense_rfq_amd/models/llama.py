@@ -127,8 +127,10 @@ class DecoderLM:
         ws = [lw[k] for lw in self.w["layers"] for k in self.TILED_PROJ if k in lw]
         nbytes = sum(t.numel() * t.element_size() for t in ws)
         if mode == "auto":
-            total = torch.cuda.get_device_properties(self.device).total_memory
-            if nbytes > 0.15 * total:
+            # one process per GPU: at most 15 % of the device, and of what is still free
+            # (ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0)
+            free, total = torch.cuda.mem_get_info(self.device)
+            if nbytes > 0.15 * total or nbytes > 0.25 * free:
                 return 0
         for t in ws:
             if t.shape[0] % 16 == 0 and t.shape[1] % 128 == 0:

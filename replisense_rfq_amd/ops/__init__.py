@@ -162,6 +162,7 @@ SPLITK_CFGS = (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14)
 
 
 SPLITK_TILED = 16        # split-K GEMV cfg bit: W in the decode-tiled layout (tile_weight)
+SPLITK_NT = 32           # split-K GEMV cfg bit: non-temporal weight loads
 
 
 def tile_weight(w: torch.Tensor) -> torch.Tensor:
@@ -590,9 +591,14 @@ def prefill_split_ws(device):
     return ws
 
 
+# RFQ_PREFILL_SMALL: small-grid prefill form, 0 = auto, 1 = head split, 2 = 8-wave split-KV
+PREFILL_SMALL_MODE = int(os.environ.get("RFQ_PREFILL_SMALL", "0"))
+
+
 def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
                  work_seq, work_qblk, out, Hq, Hkv, scale, qblk: int = 32,
-                 hsplit_below: int | None = None, kvsplit: bool | None = None):
+                 hsplit_below: int | None = None, kvsplit: bool | None = None,
+                 small_mode: int | None = None):
     """Causal paged prefill attention; the work list holds (sequence, query block of
     ``qblk`` queries) items (qblk * Hq / Hkv must be 128 or 256).  Small grids at GQA
     group 8 split the heads over two workgroups (``hsplit_below``) and, with
@@ -603,7 +609,8 @@ def attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_
                                                  else kvsplit) else (None, None)
         _native.ops().attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len,
                                    seq_kv_len, work_seq, work_qblk, out, Hq, Hkv, scale, qblk,
-                                   hs, ws, tk)
+                                   hs, ws, tk,
+                                   PREFILL_SMALL_MODE if small_mode is None else small_mode)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, seq_q_start, seq_q_len, seq_kv_len,
                          work_seq, work_qblk, out, Hq, Hkv, scale)

@@ -14,7 +14,7 @@ import os
 
 import torch
 
-from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
+from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_NT, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
                set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan, set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of)
 
@@ -68,10 +68,17 @@ LATENCY_MARGIN = float(os.environ.get("RFQ_LATENCY_LIB_MARGIN", "1.05"))
 
 
 def _splitk_cands(ws: list[torch.Tensor], base=SPLITK_CFGS) -> tuple:
-    """Split-K GEMV cfgs to time: ``base`` on the row-major weights, and the same cfgs
-    on the decode-tiled copies (SPLITK_TILED) when every layer has one."""
+    """Split-K GEMV cfgs to time: ``base`` on the row-major weights, or, when every layer
+    has a decode-tiled copy (SPLITK_TILED), on the tiled copies with plain and with
+    non-temporal weight loads (SPLITK_NT: +5-15 % on the tiled stream, a loss on the
+    row-major one's half lines; profiles/r3_host_gaps_and_mall.md §3)."""
     tiled = all(tiled_of(w) is not None for w in ws)
-    return tuple(base) + (tuple(c | SPLITK_TILED for c in base) if tiled else ())
+    if not tiled:
+        return tuple(base)
+    # the row-major split-K cfgs are left out: the tiled stream beat them on every
+    # 8B / 70B / TP=8 shape measured (start-up time stays ~2x, not 3x)
+    return tuple(c | SPLITK_TILED for c in base) + tuple(c | SPLITK_TILED | SPLITK_NT
+                                                         for c in base)
 
 
 def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, list[int]],
@@ -462,7 +469,8 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
             log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d lib %.1fus -> %s %.1fus", *r)
     for r in report:
         sel = "lib" if r[5] < 0 else (
-            (f"splitk{r[5] & 15}" + ("t" if r[5] & SPLITK_TILED else ""))
+            (f"splitk{r[5] & 15}" + ("t" if r[5] & SPLITK_TILED else "")
+             + ("n" if r[5] & SPLITK_NT else ""))
             if r[5] & SPLITK_BIT else f"skinny{r[5]}")
         log.info("gemm plan %-8s M=%-3d N=%-6d K=%-6d hipblaslt %.1fus -> %s %.1fus",
                  r[0], r[1], r[2], r[3], r[4], sel, r[6])

@@ -299,12 +299,15 @@ def test_attn_prefill(gpu, Hq, Hkv, qblk, spike):
     # hsplit_below 0: one workgroup per (item, kv head); 4096: GQA group 8 split over two
     # 4-wave workgroups (the small-grid form)
     # kvsplit: the head-split form's items of >= 4 key tiles split over two workgroups
-    # (merged in-kernel; run twice, so the tickets must have been reset)
-    for hs, kvs in ((0, False), (4096, False), (4096, True), (4096, True)):
+    # (merged in-kernel; run twice, so the tickets must have been reset); small_mode 2:
+    # the 8-wave form with the key tiles split 2-4 ways (8-wave shapes only)
+    for hs, kvs, sm in ((0, False, 0), (4096, False, 1), (4096, True, 1), (4096, True, 1),
+                        (4096, True, 2), (4096, True, 2), (4096, True, 0)):
         out.zero_()
         ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out,
-                         Hq, Hkv, scale, qblk, hsplit_below=hs, kvsplit=kvs)
-        _close(out, exp, 2e-2, 0, f"attn_prefill Hq={Hq} qblk={qblk} hsplit={hs} kvsplit={kvs}")
+                         Hq, Hkv, scale, qblk, hsplit_below=hs, kvsplit=kvs, small_mode=sm)
+        _close(out, exp, 2e-2, 0,
+               f"attn_prefill Hq={Hq} qblk={qblk} hsplit={hs} kvsplit={kvs} small_mode={sm}")
     if ops.native_available():
         torch.cuda.synchronize()
         assert int(ops.prefill_split_ws(gpu)[1].abs().sum()) == 0, "split tickets not reset"
@@ -884,6 +887,20 @@ def test_gemm_dense_identity_asymmetric(gpu, cfg):
     w = (torch.arange(512 * K, device="cuda", dtype=torch.float32).reshape(512, K) % 97 - 48).to(BF)
     out = ops.gemm_dense(x, w, cfg=cfg)
     assert torch.equal(out.float(), w.float().t()[:K])
+
+
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 128), (100, 512, 256), (513, 1280, 1024),
+                                   (300, 4096, 8192)])
+def test_gemm_dense_tiled_weight(gpu, M, N, K, swiglu):
+    """gemm_dense reading the decode-tiled weight layout (cfg bit 4 -> 2 | 4): same LDS
+    image, so bit-identical to the row-major kernel of the same schedule (cfg 2)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + swiglu)
+    x = ((torch.rand(M, K, device="cuda", generator=g) * 2 - 1)).to(BF)
+    w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(BF)
+    a = ops.gemm_dense(x, w, swiglu=swiglu, cfg=2)
+    b = ops.gemm_dense(x, ops.tile_weight(w), swiglu=swiglu, cfg=2 | 4)
+    assert torch.equal(a, b)
 
 
 def test_gemm_dense_strided_rows(gpu):

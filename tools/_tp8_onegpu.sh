@@ -3,7 +3,7 @@
 # layer all-reduces through IPC on the same GPU).  Functional rehearsal of the 8-GPU
 # node's TP phase (BASELINE config 4), not a performance number.
 set -e
-export RFQ_DIST_BACKEND=gloo
+export RFQ_DIST_BACKEND=gloo RFQ_TILED_WEIGHTS=0 RFQ_TUNE_GEMM=0
 start=$(date +%s)
 timeout -k 20 780 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
   --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 8 --model llama3-70b --tp 8 \

@@ -49,10 +49,10 @@ def main():
                 _native.ops().gemv_splitk(x, w, y, part, tiles, cfg)
 
         res = {"shape": name, "rows": rows, "K": K, "layers": L, "MB": round(rows * K * 2 / 1e6, 1)}
-        for tiled in (False, True):
+        for tiled, nt in ((False, False), (True, False), (False, True), (True, True)):
             best = None
             for c in ops.SPLITK_CFGS:
-                cfg = c | (ops.SPLITK_TILED if tiled else 0)
+                cfg = c | (ops.SPLITK_TILED if tiled else 0) | (ops.SPLITK_NT if nt else 0)
                 ntile = ncol // 16
                 if not ops.splitk_fits(dev, c, 1, rows, ntile) or K // 128 < (2 << (c & 3)):
                     continue
@@ -75,19 +75,20 @@ def main():
                     torch.cuda.synchronize()
                     ts.append(a.elapsed_time(b) * 1e3 / L)
                 t = statistics.median(ts)
-                if tiled:
+                if tiled or nt:
                     ref = torch.empty_like(ys[0])
                     call(ws[0], ref, c)
-                    call(wts[0], ys[0], cfg)
+                    call((wts if tiled else ws)[0], ys[0], cfg)
                     torch.cuda.synchronize()
                     assert torch.equal(ref, ys[0]), f"{name} cfg {cfg}: tiled != row-major"
                 if best is None or t < best[1]:
                     best = (cfg, t)
                 del g
-            key = "tiled" if tiled else "rowmajor"
+            key = ("tiled" if tiled else "rowmajor") + ("_nt" if nt else "")
             res[key] = {"cfg": best[0], "us": round(best[1], 2),
                         "TBps": round(rows * K * 2 / best[1] / 1e6, 2)}
         res["speedup"] = round(res["rowmajor"]["us"] / res["tiled"]["us"], 3)
+        res["speedup_nt"] = round(res["rowmajor"]["us"] / res["tiled_nt"]["us"], 3)
         print(json.dumps(res), flush=True)
         del ws, wts
 
