@@ -109,6 +109,7 @@ class DecoderLM:
         # reduce-scatter (then the residual-add RMSNorm runs on 1/W of the rows) and an
         # all-gather before the next column-parallel GEMM.  0 = off (SURVEY.md §2.3 SP).
         self.sp_min_tokens = int(os.environ.get("RFQ_SP_MIN_TOKENS", "0"))
+        self.tiled_inplace = False      # projections stored only in the decode-tiled layout
 
     # ------------------------------------------------------- decode weight layout
     TILED_PROJ = ("qkv", "o", "gate_up", "down")
@@ -118,20 +119,36 @@ class DecoderLM:
         split-K GEMVs of small-batch decode steps: each wave load is then 1 KB of
         contiguous weight bytes.  The row-major originals stay for every large-M GEMM,
         so this costs one more copy of the projection weights: ``auto`` (RFQ_TILED_WEIGHTS,
-        default) tiles when that copy is at most 15 % of the device's memory (8B, the
-        70B TP=4/8 shards; not 70B at TP 1-2) and the model is dense.  The start-up plan
-        (ops.autotune) then times the tiled cfgs against everything else.  Returns bytes."""
+        default) copies when that copy is at most 15 % of the device's memory (8B, the
+        70B TP=4/8 shards) and otherwise (70B at TP 1-2) tiles in place: the row-major
+        projections are replaced, small steps run the tiled split-K GEMVs and large ones
+        the hand-written dense GEMM on the tiled layout (no hipBLASLt).  ``copy`` /
+        ``inplace`` force a mode.  Dense models only.  The start-up plan (ops.autotune)
+        times the tiled cfgs.  Returns the bytes of the extra copy."""
         mode = (mode or os.environ.get("RFQ_TILED_WEIGHTS", "auto")).lower()
         if mode in ("0", "off", "false") or self.cfg.is_moe or self.device.type != "cuda":
             return 0
         ws = [lw[k] for lw in self.w["layers"] for k in self.TILED_PROJ if k in lw]
         nbytes = sum(t.numel() * t.element_size() for t in ws)
         if mode == "auto":
-            # one process per GPU: at most 15 % of the device, and of what is still free
-            # (ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0)
+            # one process per GPU: a copy of at most 15 % of the device, and of what is
+            # still free (ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0);
+            # a model whose copy does not fit (70B at TP 1-2) is tiled in place
             free, total = torch.cuda.mem_get_info(self.device)
-            if nbytes > 0.15 * total or nbytes > 0.25 * free:
+            mode = "copy" if (nbytes <= 0.15 * total and nbytes <= 0.25 * free) else "inplace"
+        if mode == "inplace":
+            # in place: every GEMM on these weights runs a tiled-layout kernel (split-K
+            # GEMV, gemm_dense cfg 2|4), which needs N % 256 and K % 128 everywhere
+            if not all(t.shape[0] % 256 == 0 and t.shape[1] % 128 == 0 for t in ws):
                 return 0
+            del ws                    # hold no reference: each original is freed as replaced
+            for lw in self.w["layers"]:
+                for k in self.TILED_PROJ:
+                    if k in lw:
+                        lw[k] = ops.tile_weight(lw[k])       # the row-major tensor is freed
+                        ops.register_tiled(lw[k], None)
+            self.tiled_inplace = True
+            return 0
         for t in ws:
             if t.shape[0] % 16 == 0 and t.shape[1] % 128 == 0:
                 ops.register_tiled(t, ops.tile_weight(t))

@@ -225,8 +225,13 @@ def export_hf(full: dict, cfg: ModelConfig) -> dict[str, torch.Tensor]:
     D, F, Hq, Hkv = cfg.head_dim, cfg.ffn, cfg.n_heads, cfg.n_kv_heads
     out = {"model.embed_tokens.weight": full["embed"], "model.norm.weight": full["final_norm"],
            "lm_head.weight": full["lm_head"]}
+    from .. import ops
+
     for li, lw in enumerate(full["layers"]):
         p = f"model.layers.{li}."
+        # an engine's in-place decode-tiled projections (DecoderLM.tile_decode_weights)
+        lw = {k: ops.untile_weight(v) if isinstance(v, torch.Tensor) and ops.tiled_only(v)
+              else v for k, v in lw.items()}
         out[p + "input_layernorm.weight"] = lw["attn_norm"]
         out[p + "post_attention_layernorm.weight"] = lw["mlp_norm"]
         out[p + "self_attn.q_proj.weight"] = lw["qkv"][: Hq * D]

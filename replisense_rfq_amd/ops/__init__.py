@@ -22,7 +22,7 @@ __all__ = [
     "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
     "gemm_dense", "gemm_dense_ok", "swiglu_large", "tile_weight", "untile_weight",
-    "register_tiled", "tiled_of", "clear_tiled", "SPLITK_TILED",
+    "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -85,7 +85,7 @@ def silu_linear(gu, w, out=None):
     the start-up plan found it faster; otherwise act.hip silu_mul + linear."""
     M, F2 = gu.shape
     F, N = F2 // 2, w.shape[0]
-    if _gpu(gu) and _TUNED_MS and M <= SKINNY_MAX_M and gu.stride(1) == 1:
+    if _gpu(gu) and _TUNED_MS and M <= SKINNY_MAX_M and gu.stride(1) == 1 and not tiled_only(w):
         for m in _TUNED_MS:
             if m >= M:
                 cfg = _SILU_PLAN.get((m, N, F), -1)
@@ -185,7 +185,9 @@ def tile_weight(w: torch.Tensor) -> torch.Tensor:
 _TILED: dict[int, tuple] = {}
 
 
-def register_tiled(w: torch.Tensor, wt: torch.Tensor) -> None:
+def register_tiled(w: torch.Tensor, wt: torch.Tensor | None) -> None:
+    """``wt``: the tiled copy of row-major ``w``; None: ``w`` itself is stored tiled
+    (in-place mode, no row-major copy: every GEMM on it runs a tiled-layout kernel)."""
     import weakref
 
     key = w.data_ptr()
@@ -195,7 +197,39 @@ def register_tiled(w: torch.Tensor, wt: torch.Tensor) -> None:
 
 def tiled_of(w: torch.Tensor) -> torch.Tensor | None:
     e = _TILED.get(w.data_ptr())
-    return e[1] if e is not None and e[0]() is w else None
+    if e is None or e[0]() is not w:
+        return None
+    return w if e[1] is None else e[1]
+
+
+def tiled_only(w: torch.Tensor) -> bool:
+    """``w`` is stored in the decode-tiled layout and has no row-major copy."""
+    e = _TILED.get(w.data_ptr())
+    return e is not None and e[1] is None and e[0]() is w
+
+
+TILED_GEMV_DEFAULT = 8 | 16 | 32        # KS 2, 4 waves, U 2, tiled, nt (untuned shapes)
+
+
+def _gemv_tiled(x, w, out, cfg: int | None = None):
+    """out = x w^T for an in-place tiled ``w``: split-K GEMV in 16-row chunks for
+    M <= SKINNY_MAX_M (the M = 16 plan entry), the dense MFMA GEMM on the tiled layout
+    (gemm_dense cfg 2 | 4) above."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if M > SKINNY_MAX_M:
+        _native.ops().gemm_dense(x, w, out, False, 2 | 4)
+        return out
+    part, tiles = splitk_ws(x.device)
+    for a in range(0, M, 16):
+        xm = x[a:a + 16]
+        c = cfg if cfg is not None else linear_plan(xm.shape[0], N, K)
+        if c < 0 or not (c & SPLITK_BIT) or not (c & SPLITK_TILED):
+            c = TILED_GEMV_DEFAULT
+        _native.ops().gemv_splitk(xm, w, out[a:a + 16], part, tiles, c & 127)
+    return out
 
 
 def clear_tiled() -> None:
@@ -237,7 +271,7 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     K = x.shape[1] // 2 if gated else x.shape[1]
     N = w.shape[0]
     cfg = norm_plan(M, N, K, gated)
-    if cfg < 0:
+    if cfg < 0 or (tiled_only(w) and not (cfg & SPLITK_BIT and cfg & SPLITK_TILED)):
         return False
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     if cfg & SPLITK_BIT:
@@ -271,7 +305,7 @@ def linear_swiglu(x, w):
     for m in _TUNED_MS:
         if m >= M:
             cfg = _SWI_PLAN.get((m, F, K), -1)
-            if cfg < 0:
+            if cfg < 0 or (tiled_only(w) and not (cfg & SPLITK_BIT and cfg & SPLITK_TILED)):
                 return None
             out = torch.empty((M, F), dtype=x.dtype, device=x.device)
             if cfg & SPLITK_BIT:
@@ -309,6 +343,8 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
     plan measured that faster (then only the q columns of the result are written)."""
     if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:
         cfg = rope_plan(x.shape[0], w.shape[0], x.shape[1])
+        if tiled_only(w) and not (cfg & SPLITK_BIT and cfg & SPLITK_TILED):
+            cfg = -1
         if cfg >= 0:
             qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
             if cfg & SPLITK_BIT:
@@ -381,6 +417,10 @@ def swiglu_large(x, w):
     N = w.shape[0]
     if M <= SKINNY_MAX_M:
         return None
+    if tiled_only(w):                 # no row-major copy: the tiled dense kernel, fused
+        out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
+        _native.ops().gemm_dense(x, w, out, True, 2 | 4)
+        return out
     cfg = _dense_cfg(M, N, K, swiglu=True)
     if cfg < 0:
         return None
@@ -412,6 +452,8 @@ def linear(x, w, out=None, plan: int | None = None):
     M-split plan measured that to be faster."""
     M, K = x.shape
     N = w.shape[0]
+    if _gpu(x) and tiled_only(w):
+        return _gemv_tiled(x, w, out, plan)
     if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:
         cfg = linear_plan(M, N, K) if plan is None else plan
         if cfg >= 0:

@@ -16,7 +16,8 @@ import torch
 
 from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_NT, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
                set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan, set_split_plan,
-               set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of)
+               set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
+               tiled_only)
 
 log = logging.getLogger("replisense_rfq_amd.ops")
 
@@ -67,6 +68,12 @@ def _time(fn, ws, reps: int, graph: bool = True) -> float:
 LATENCY_MARGIN = float(os.environ.get("RFQ_LATENCY_LIB_MARGIN", "1.05"))
 
 
+def _tiled_group(ws: list[torch.Tensor]) -> bool:
+    """Every layer's weight is stored in the decode-tiled layout only (in-place mode):
+    no hipBLASLt or skinny-kernel candidate can read it."""
+    return all(tiled_only(w) for w in ws)
+
+
 def _splitk_cands(ws: list[torch.Tensor], base=SPLITK_CFGS) -> tuple:
     """Split-K GEMV cfgs to time: ``base`` on the row-major weights, or, when every layer
     has a decode-tiled copy (SPLITK_TILED), on the tiled copies with plain and with
@@ -99,6 +106,22 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
                 continue
             x = torch.randn(M, K, device=ws[0].device, dtype=ws[0].dtype)
             out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+            if _tiled_group(ws):
+                # in-place tiled weights: only the tiled split-K GEMV reads them (M > 16
+                # runs in 16-row chunks of the M = 16 entry, ops._gemv_tiled)
+                if M > 16:
+                    continue
+                part, tiles = splitk_ws(x.device)
+                best, t_best = -1, float("inf")
+                for c in _splitk_cands(ws):
+                    if K // 128 < (2 << (c & 3)) or not splitk_fits(x.device, c, M, N, N // 16):
+                        continue
+                    t = _time(lambda w, c=c: ops.gemv_splitk(x, w, out, part, tiles, c), ws, reps)
+                    if t < t_best:
+                        best, t_best = c | SPLITK_BIT, t
+                plan[(M, N, K)] = best
+                report.append((name, M, N, K, 0.0, best, round(t_best, 1)))
+                continue
             t_lib = _time(lambda w: torch.matmul(x, w.t(), out=out), ws, reps)
             best, t_best = -1, t_lib * (LATENCY_MARGIN if M <= 16 else margin)
             for c in CANDIDATES:
@@ -131,7 +154,7 @@ def tune_silu_down(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin:
     ops = _native.ops()
     N, F = ws[0].shape
     plan, report = {}, []
-    if F % 128 or N % 16:
+    if F % 128 or N % 16 or _tiled_group(ws):
         return plan, report
     for M in ms:
         if M > 64:
@@ -183,7 +206,7 @@ def tune_norm(ws: list[torch.Tensor], ms: list[int], norm_w: torch.Tensor, gated
 
         t_ref = _time(ref, ws, reps)
         best, t_best = -1, t_ref * margin
-        base = (16, 17, 18, 19) if gated else CANDIDATES
+        base = () if _tiled_group(ws) else ((16, 17, 18, 19) if gated else CANDIDATES)
         for c in base + tuple(b | 64 for b in base):       # | 64: two K slices per tile
             if c & 1 and N % 32:
                 continue
@@ -227,7 +250,7 @@ def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: fl
         act = torch.empty(M, F, device=dev, dtype=dt)
         t_ref = _time(lambda w: silu_mul(linear(x, w, out=gu), out=act), ws, reps)
         best, t_best = -1, t_ref * margin
-        for c in (0, 2):
+        for c in (() if _tiled_group(ws) else (0, 2)):
             t = _time(lambda w, c=c: ops.skinny_gemm_swiglu(x, w, act, c), ws, reps)
             if t < t_best:
                 best, t_best = c, t
@@ -275,7 +298,7 @@ def tune_rope(ws: list[torch.Tensor], ms: list[int], cos_sin: torch.Tensor, hq: 
 
         t_ref = _time(ref, ws, reps)
         best, t_best = -1, t_ref * margin
-        for c in (13, 15):
+        for c in (() if _tiled_group(ws) else (13, 15)):
             t = _time(lambda w, c=c: ops.skinny_gemm_rope(x, w, qkv, pos, cos_sin, slots, kc, vc,
                                                           hq, hkv, c), ws, reps)
             if t < t_best:
@@ -343,8 +366,8 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
     for name, ws in groups.items():
         N, K = ws[0].shape
         J = max_m.get(name, 0) // quantum
-        if J < 2 or (N, K) in plan:
-            continue
+        if J < 2 or (N, K) in plan or _tiled_group(ws):
+            continue                 # in-place tiled weights: always the tiled dense GEMM
         w = ws[0]
         x = torch.randn(J * quantum, K, device=w.device, dtype=w.dtype)
         out = torch.empty(J * quantum, N, device=w.device, dtype=w.dtype)

@@ -163,3 +163,46 @@ def test_mixtral_engine(gpu):
     prompts = [tok.chat_ids(build_messages(synth.make_rfq(i).text)) for i in range(3)]
     for s in eng.generate(prompts):
         RFQResponse(**json.loads(eng.decode_text(s)))
+
+
+def test_inplace_tiled_forward_matches_cpu_oracle(gpu):
+    """In-place decode-tiled projections (the layout 70B at TP 1-2 keeps, no row-major
+    copy): every GEMM on them runs a tiled-layout kernel -- split-K GEMVs (M <= 16, in
+    16-row chunks up to 64) and the dense MFMA GEMM (larger M) -- vs the CPU oracle on
+    the row-major weights, at prefill, chunked and decode-sized batches."""
+    from replisense_rfq_amd import ops
+
+    cfg = get_config("tiny-llama")
+    m_gpu = DecoderLM(cfg, gpu, seed=5)
+    w_cpu = {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in m_gpu.w.items()}
+    w_cpu["layers"] = [type(l)({k: t.cpu() for k, t in l.items()}) for l in m_gpu.w["layers"]]
+    m_gpu.tile_decode_weights("inplace")
+    assert m_gpu.tiled_inplace
+    assert all(ops.tiled_only(m_gpu.w["layers"][0][k]) for k in DecoderLM.TILED_PROJ)
+    m_cpu = DecoderLM(cfg, "cpu", weights=w_cpu)
+    nb = 8
+    shape = (cfg.n_layers, nb, m_gpu.hkv, 32, 128)
+    for T in (150, 40, 5):
+        for m in (m_gpu, m_cpu):
+            dev = m.device
+            m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16, device=dev),
+                              torch.zeros(shape, dtype=torch.bfloat16, device=dev))
+        lg = m_gpu.forward(_meta(T, gpu, nb)).float().cpu()
+        lc = m_cpu.forward(_meta(T, "cpu", nb)).float()
+        rel = (lg - lc).norm() / lc.norm()
+        assert rel < 0.05, (T, rel)
+
+
+def test_engine_inplace_tiled_valid(gpu, monkeypatch):
+    """The engine with in-place tiled weights: start-up plans restricted to tiled
+    kernels, graph-captured decode, valid RFQ JSON."""
+    monkeypatch.setenv("RFQ_TILED_WEIGHTS", "inplace")
+    eng = _engine(True)
+    assert eng.model.tiled_inplace
+    tok = eng.tokenizer
+    prompts = [tok.chat_ids(build_messages(synth.make_rfq(30 + i).text)) for i in range(4)]
+    for s in eng.generate(prompts):
+        RFQResponse(**json.loads(eng.decode_text(s)))
+    assert eng.stats()["graph_steps"] > 0
+    del eng
+    torch.cuda.empty_cache()
