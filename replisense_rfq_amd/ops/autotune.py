@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 
 import torch
 
@@ -50,6 +51,16 @@ def _time(fn, ws, reps: int, graph: bool = True) -> float:
         except RuntimeError as e:       # capture refused: fall back to eager timing
             log.warning("autotune: graph capture failed (%s); timing eagerly", e)
             g = None
+    if g is None:
+        # eager timing of one large GEMM takes a few ms at most: after the host gap of
+        # the previous measurement the GPU clock is still ramping up, which read hipBLASLt
+        # and the hand-written GEMM alike ~3x slow (gate|up at M = 4096: 2.5 ms here vs
+        # 0.7 ms steady).  Keep the GPU busy for ~10 ms first.
+        t_end = time.perf_counter() + 0.010
+        while time.perf_counter() < t_end:
+            for w in ws:
+                fn(w)
+            torch.cuda.synchronize()
     best = float("inf")
     for _ in range(3 if g is not None else 1):     # min of 3 trials: one slow trial
         e0.record()                                # must not flip a plan entry
