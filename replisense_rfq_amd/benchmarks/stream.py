@@ -42,6 +42,33 @@ def _parsed_doc(args):
     return text, synth.decode_hints(d)
 
 
+def _produce_proc(base: int, flavor: str, path, out_q, stop_evt) -> None:
+    """Spawned producer process for the plain-text stream: synthesise each document,
+    build the byte-identical prompt and tokenise it, away from the engine's GIL (a
+    producer thread in the engine process took the GIL from the step loop every switch
+    interval: the scheduler pack waited 5.2 ms per step at the default 5 ms interval and
+    the forward launch +3 ms at 0.5 ms).  Imports no torch and never touches the GPU."""
+    import queue as _q
+
+    from ..engine.tokenizer import get_tokenizer
+    from ..service.prompt import build_messages, register_prompt_prefix
+    from ..utils import synth
+
+    tok = get_tokenizer(flavor, path)
+    register_prompt_prefix(tok)
+    i = 0
+    while not stop_evt.is_set():
+        d = synth.make_rfq(base + i)
+        item = (base + i, tok.chat_ids(build_messages(d.text)), synth.decode_hints(d))
+        while not stop_evt.is_set():
+            try:
+                out_q.put(item, timeout=0.1)
+                break
+            except _q.Full:
+                continue
+        i += 1
+
+
 class DocStream:
     """One replica's continuous document stream over an LLMEngine.
 
@@ -53,7 +80,8 @@ class DocStream:
     """
 
     def __init__(self, engine, dp_rank: int, seed: int, in_flight: int,
-                 formats: tuple | None = None, parse_procs: int = 4):
+                 formats: tuple | None = None, parse_procs: int = 4,
+                 producer: str | None = None):
         from ..service.extract import build_messages
         from ..service.prompt import register_prompt_prefix
         from ..utils import synth
@@ -77,8 +105,27 @@ class DocStream:
 
             # spawn, never fork: this process owns a GPU context
             self._pool = ProcessPoolExecutor(parse_procs, mp_context=mp.get_context("spawn"))
-        self.thread = threading.Thread(target=self._produce, name="bench-tokenize", daemon=True)
-        self.thread.start()
+        # plain-text stream: the prompts come from a spawned process (RFQ_BENCH_PRODUCER=
+        # process, default) or, as before, from a thread of this process (=thread)
+        import os
+
+        mode = producer or os.environ.get("RFQ_BENCH_PRODUCER", "process")
+        self._proc = None
+        self.thread = None
+        if self.formats is None and mode == "process":
+            import multiprocessing as mp
+
+            ctx = mp.get_context("spawn")            # never fork: this process owns a GPU
+            self.ready = ctx.Queue(maxsize=max(64, in_flight))
+            self._stop_evt = ctx.Event()
+            self._proc = ctx.Process(target=_produce_proc, name="bench-tokenize",
+                                     args=(self.base, self.tok.flavor, getattr(self.tok, "path", None),
+                                           self.ready, self._stop_evt), daemon=True)
+            self._proc.start()
+        else:
+            self.thread = threading.Thread(target=self._produce, name="bench-tokenize",
+                                           daemon=True)
+            self.thread.start()
 
     def _docs(self):
         i = 0
@@ -112,9 +159,14 @@ class DocStream:
         eng = self.engine
         while self.live < self.in_flight:
             try:
-                ids, params = self.ready.get(block=block and not eng.has_work(), timeout=1.0)
+                item = self.ready.get(block=block and not eng.has_work(), timeout=1.0)
             except queue.Empty:
                 return
+            if self._proc is not None:           # (doc seed, prompt ids, decode hints)
+                s, ids, hints = item
+                params = eng.default_params(seed=s & 0xFFFFFF, **hints)
+            else:
+                ids, params = item
             eng.add_request(ids, params)
             self.live += 1
 
@@ -136,12 +188,22 @@ class DocStream:
 
     def close(self):
         self.stop.set()
+        if self._proc is not None:
+            self._stop_evt.set()
         try:
             while True:
                 self.ready.get_nowait()
         except queue.Empty:
             pass
-        self.thread.join(timeout=10)
+        if self._proc is not None:
+            self._proc.join(timeout=10)
+            if self._proc.is_alive():
+                self._proc.terminate()
+                self._proc.join(timeout=5)
+            self.ready.cancel_join_thread()
+            self._proc = None
+        if self.thread is not None:
+            self.thread.join(timeout=10)
         if self._pool is not None:
             self._pool.shutdown(wait=False, cancel_futures=True)
         if self.engine.has_work():

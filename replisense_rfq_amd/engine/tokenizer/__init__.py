@@ -43,6 +43,7 @@ class Tokenizer:
             with gzip.open(_DIR / f"{flavor}_synth.json.gz", "rb") as f:
                 self._tok = _HFTok.from_str(f.read().decode())
         self.flavor = flavor
+        self.path = str(path) if path else None      # to rebuild it in another process
         self.vocab_size = self._tok.get_vocab_size()
         self._content_prefixes: list[str] = []
         self._raw_prefixes: dict[str, tuple[list[int], int]] = {}

@@ -1,0 +1,34 @@
+"""The bench's document stream: the spawned producer process (default) hands the
+engine exactly the prompts and sampling parameters the in-process producer thread
+builds (same documents, token-identical prompts, same seeds and hints)."""
+from replisense_rfq_amd.benchmarks.stream import DocStream
+from replisense_rfq_amd.engine.engine import LLMEngine
+from replisense_rfq_amd.utils.config import EngineConfig
+
+
+def _first(stream, n):
+    got = []
+    for _ in range(n):
+        item = stream.ready.get(timeout=60)
+        if stream._proc is not None:
+            s, ids, hints = item
+            item = (ids, stream.engine.default_params(seed=s & 0xFFFFFF, **hints))
+        got.append(item)
+    return got
+
+
+def test_process_producer_matches_thread():
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4,
+                                 decode_hints=True))
+    a = DocStream(eng, 0, 7, 4, producer="process")
+    b = DocStream(eng, 0, 7, 4, producer="thread")
+    try:
+        pa, pb = _first(a, 5), _first(b, 5)
+    finally:
+        a.close()
+        b.close()
+    assert a._proc is None and b.thread is not None
+    for (ia, sa), (ib, sb) in zip(pa, pb):
+        assert list(ia) == list(ib)
+        assert (sa.seed, sa.min_items, sa.profile, sa.temperature) == \
+            (sb.seed, sb.min_items, sb.profile, sb.temperature)
