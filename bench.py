@@ -399,7 +399,9 @@ def main():
                        "in_flight_per_replica": args.max_num_seqs,
                        "temperature": cfg.temperature, "grammar": cfg.grammar,
                        "profile": "synthetic", "decode_hints": True,
-                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs},
+                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
+                       # prompts built + tokenised in a spawned process (benchmarks.stream)
+                       "producer": os.environ.get("RFQ_BENCH_PRODUCER", "process")},
             # latency under load of the documents completed in the timed window
             # (submission -> last token, closed loop at in_flight_per_replica)
             "loaded_latency_s": loaded["e2e_s"],
@@ -417,6 +419,10 @@ def main():
             "engine": {"init_s": round(t_init, 1), "graph_capture_s": round(engine.capture_s, 1),
                        "gemm_tune_s": round(engine.tune_s, 1),
                        "gemm_plan": _gemm_plan_summary(),
+                       # decode-tiled projection weights: extra copy (bytes) or in place
+                       "tiled_weights": ("inplace" if getattr(engine.model, "tiled_inplace", False)
+                                         else ("copy" if getattr(engine, "tiled_bytes", 0)
+                                               else "off")),
                        "timed_engine_steps": steps_timed,
                        "docs_completed_in_window_rank0": done_in_window,
                        "graph_steps": stats.get("graph_steps"), "steps": stats.get("steps"),
