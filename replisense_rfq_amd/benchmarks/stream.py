@@ -161,6 +161,9 @@ class DocStream:
             try:
                 item = self.ready.get(block=block and not eng.has_work(), timeout=1.0)
             except queue.Empty:
+                if self._proc is not None and not self._proc.is_alive():
+                    raise RuntimeError(f"bench producer process exited "
+                                       f"(code {self._proc.exitcode}); no more documents")
                 return
             if self._proc is not None:           # (doc seed, prompt ids, decode hints)
                 s, ids, hints = item
