@@ -420,9 +420,7 @@ def main():
                        "gemm_tune_s": round(engine.tune_s, 1),
                        "gemm_plan": _gemm_plan_summary(),
                        # decode-tiled projection weights: extra copy (bytes) or in place
-                       "tiled_weights": ("inplace" if getattr(engine.model, "tiled_inplace", False)
-                                         else ("copy" if getattr(engine, "tiled_bytes", 0)
-                                               else "off")),
+                       "tiled_weights": getattr(engine.model, "tiled_plan", None) or "off",
                        "timed_engine_steps": steps_timed,
                        "docs_completed_in_window_rank0": done_in_window,
                        "graph_steps": stats.get("graph_steps"), "steps": stats.get("steps"),

@@ -109,50 +109,70 @@ class DecoderLM:
         # reduce-scatter (then the residual-add RMSNorm runs on 1/W of the rows) and an
         # all-gather before the next column-parallel GEMM.  0 = off (SURVEY.md §2.3 SP).
         self.sp_min_tokens = int(os.environ.get("RFQ_SP_MIN_TOKENS", "0"))
-        self.tiled_inplace = False      # projections stored only in the decode-tiled layout
+        self.tiled_inplace = False      # some projection stored only in the decode-tiled layout
+        self.tiled_plan: dict = {}      # projection -> copy | inplace | off
 
     # ------------------------------------------------------- decode weight layout
     TILED_PROJ = ("qkv", "o", "gate_up", "down")
 
     def tile_decode_weights(self, mode: str | None = None) -> int:
-        """Decode-tiled copies of the per-layer projections (ops.tile_weight) for the
+        """Decode-tiled layout (ops.tile_weight) of the per-layer projections for the
         split-K GEMVs of small-batch decode steps: each wave load is then 1 KB of
-        contiguous weight bytes.  The row-major originals stay for every large-M GEMM,
-        so this costs one more copy of the projection weights: ``auto`` (RFQ_TILED_WEIGHTS,
-        default) copies when that copy is at most 15 % of the device's memory (8B, the
-        70B TP=4/8 shards) and otherwise (70B at TP 1-2) tiles in place: the row-major
-        projections are replaced, small steps run the tiled split-K GEMVs and large ones
-        the hand-written dense GEMM on the tiled layout (no hipBLASLt).  ``copy`` /
-        ``inplace`` force a mode.  Dense models only.  The start-up plan (ops.autotune)
-        times the tiled cfgs.  Returns the bytes of the extra copy."""
+        contiguous weight bytes.  Per projection, one of:
+
+          copy     a tiled copy next to the row-major weight (large-M GEMMs keep
+                   hipBLASLt / the plan's kernels);
+          inplace  the row-major weight is replaced: small steps run the tiled split-K
+                   GEMVs, large ones the hand-written dense GEMM on the tiled layout
+                   (gemm_dense cfg 2|4; no library GEMM can read it).
+
+        ``auto`` (RFQ_TILED_WEIGHTS, default) copies projections, smallest first, while
+        the copies stay within 25 % of the device's memory (and 40 % of what is free;
+        ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0) and tiles the rest
+        in place: 8B and the 70B TP=8 shard copy all four, 70B at TP=1 copies qkv, o and
+        down and keeps only the tiled gate|up (whose 224-tile grid suits the dense GEMM
+        at prefill sizes).  ``copy`` / ``inplace`` force one mode for all.  Dense models
+        only.  The start-up plan (ops.autotune) times the tiled cfgs.  Returns the bytes
+        of the extra copies."""
         mode = (mode or os.environ.get("RFQ_TILED_WEIGHTS", "auto")).lower()
         if mode in ("0", "off", "false") or self.cfg.is_moe or self.device.type != "cuda":
             return 0
-        ws = [lw[k] for lw in self.w["layers"] for k in self.TILED_PROJ if k in lw]
-        nbytes = sum(t.numel() * t.element_size() for t in ws)
+        layers = self.w["layers"]
+        names = [k for k in self.TILED_PROJ if k in layers[0]]
+        size = {k: sum(lw[k].numel() * lw[k].element_size() for lw in layers) for k in names}
+
+        def inplace_ok(k):           # the tiled dense GEMM's shape constraints
+            t = layers[0][k]
+            return t.shape[0] % 256 == 0 and t.shape[1] % 128 == 0
+
         if mode == "auto":
-            # one process per GPU: a copy of at most 15 % of the device, and of what is
-            # still free (ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0);
-            # a model whose copy does not fit (70B at TP 1-2) is tiled in place
             free, total = torch.cuda.mem_get_info(self.device)
-            mode = "copy" if (nbytes <= 0.15 * total and nbytes <= 0.25 * free) else "inplace"
-        if mode == "inplace":
-            # in place: every GEMM on these weights runs a tiled-layout kernel (split-K
-            # GEMV, gemm_dense cfg 2|4), which needs N % 256 and K % 128 everywhere
-            if not all(t.shape[0] % 256 == 0 and t.shape[1] % 128 == 0 for t in ws):
-                return 0
-            del ws                    # hold no reference: each original is freed as replaced
-            for lw in self.w["layers"]:
-                for k in self.TILED_PROJ:
-                    if k in lw:
-                        lw[k] = ops.tile_weight(lw[k])       # the row-major tensor is freed
-                        ops.register_tiled(lw[k], None)
-            self.tiled_inplace = True
-            return 0
-        for t in ws:
-            if t.shape[0] % 16 == 0 and t.shape[1] % 128 == 0:
-                ops.register_tiled(t, ops.tile_weight(t))
-        return nbytes
+            budget = min(0.25 * total, 0.40 * free)
+            plan, used = {}, 0
+            for k in sorted(names, key=lambda n: size[n]):
+                if used + size[k] <= budget:
+                    plan[k], used = "copy", used + size[k]
+                else:
+                    plan[k] = "inplace" if inplace_ok(k) else "off"
+        elif mode == "inplace":
+            plan = {k: "inplace" if inplace_ok(k) else "off" for k in names}
+        else:
+            plan = {k: "copy" for k in names}
+        copied = 0
+        for k in names:
+            if plan[k] == "copy":
+                for lw in layers:
+                    t = lw[k]
+                    if t.shape[0] % 16 == 0 and t.shape[1] % 128 == 0:
+                        ops.register_tiled(t, ops.tile_weight(t))
+                copied += size[k]
+            elif plan[k] == "inplace":
+                for lw in layers:
+                    lw[k] = ops.tile_weight(lw[k])          # the row-major tensor is freed
+                    ops.register_tiled(lw[k], None)
+        self.tiled_plan = plan
+        self.tiled_inplace = any(v == "inplace" for v in plan.values())
+        return copied
 
     # ------------------------------------------------------------------ KV pool
     def attach_kv_cache(self, k_pool: torch.Tensor, v_pool: torch.Tensor) -> None:

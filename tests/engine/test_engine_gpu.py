@@ -206,3 +206,35 @@ def test_engine_inplace_tiled_valid(gpu, monkeypatch):
     assert eng.stats()["graph_steps"] > 0
     del eng
     torch.cuda.empty_cache()
+
+
+def test_mixed_tiled_plan_forward_matches_cpu_oracle(gpu, monkeypatch):
+    """auto with a copy budget that holds only the smallest projections: qkv and o get
+    tiled copies, down and gate|up are tiled in place; the mixed model still matches
+    the CPU oracle at prefill- and decode-sized batches."""
+    from replisense_rfq_amd import ops
+
+    cfg = get_config("tiny-llama")
+    m_gpu = DecoderLM(cfg, gpu, seed=9)
+    w_cpu = {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in m_gpu.w.items()}
+    w_cpu["layers"] = [type(l)({k: t.cpu() for k, t in l.items()}) for l in m_gpu.w["layers"]]
+    # budget = min(0.25 total, 0.40 free) = 2.7 MB: o (1.05 MB) + qkv (1.57 MB) fit
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a, **k: (6_750_000, 10_800_000))
+    m_gpu.tile_decode_weights("auto")
+    assert m_gpu.tiled_plan == {"qkv": "copy", "o": "copy", "gate_up": "inplace",
+                                "down": "inplace"}, m_gpu.tiled_plan
+    lw = m_gpu.w["layers"][0]
+    assert ops.tiled_of(lw["qkv"]) is not None and not ops.tiled_only(lw["qkv"])
+    assert ops.tiled_only(lw["down"]) and ops.tiled_only(lw["gate_up"])
+    m_cpu = DecoderLM(cfg, "cpu", weights=w_cpu)
+    nb = 8
+    shape = (cfg.n_layers, nb, m_gpu.hkv, 32, 128)
+    for T in (150, 40, 5):
+        for m in (m_gpu, m_cpu):
+            dev = m.device
+            m.attach_kv_cache(torch.zeros(shape, dtype=torch.bfloat16, device=dev),
+                              torch.zeros(shape, dtype=torch.bfloat16, device=dev))
+        lg = m_gpu.forward(_meta(T, gpu, nb)).float().cpu()
+        lc = m_cpu.forward(_meta(T, "cpu", nb)).float()
+        rel = (lg - lc).norm() / lc.norm()
+        assert rel < 0.05, (T, rel)
