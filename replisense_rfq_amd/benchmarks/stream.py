@@ -21,10 +21,28 @@ import threading
 import time
 
 
+_WORKER_TOK = {}
+
+
+def _worker_tokenizer(flavor: str, path):
+    """One tokenizer per parse worker process (prompt prefix registered, as in the
+    engine process: token-identical prompts)."""
+    key = (flavor, path)
+    if key not in _WORKER_TOK:
+        from ..engine.tokenizer import get_tokenizer
+        from ..service.prompt import register_prompt_prefix
+
+        tok = get_tokenizer(flavor, path)
+        register_prompt_prefix(tok)
+        _WORKER_TOK[key] = tok
+    return _WORKER_TOK[key]
+
+
 def _parsed_doc(args):
     """Worker: generate one synthetic attachment, parse it with the service parser,
-    return (raw_text, decode hints).  Module-level for the spawn pool."""
-    seed, fmt = args
+    build the prompt and tokenise it (off the engine process's GIL); return (prompt
+    ids, decode hints).  Module-level for the spawn pool."""
+    seed, fmt, flavor, tok_path = args
     import os
     import tempfile
     from pathlib import Path
@@ -39,7 +57,10 @@ def _parsed_doc(args):
         text = FileParser().parse_file(str(p))["raw_text"]       # file_parser.py:97-99
     finally:
         p.unlink(missing_ok=True)
-    return text, synth.decode_hints(d)
+    from ..service.prompt import build_messages
+
+    return _worker_tokenizer(flavor, tok_path).chat_ids(build_messages(text)), \
+        synth.decode_hints(d)
 
 
 def _produce_proc(base: int, flavor: str, path, out_q, stop_evt) -> None:
@@ -135,18 +156,19 @@ class DocStream:
                 yield self.base + i, d.text, self._synth.decode_hints(d)
                 i += 1
         chunk = 32
+        flavor, path = self.tok.flavor, getattr(self.tok, "path", None)
         while not self.stop.is_set():
-            args = [(self.base + i + k, self.formats[(i + k) % len(self.formats)])
+            args = [(self.base + i + k, self.formats[(i + k) % len(self.formats)], flavor, path)
                     for k in range(chunk)]
-            for (s, _), (text, hints) in zip(args, self._pool.map(_parsed_doc, args)):
-                yield s, text, hints
+            for a, (ids, hints) in zip(args, self._pool.map(_parsed_doc, args)):
+                yield a[0], ids, hints                  # already tokenised by the worker
             i += chunk
 
     def _produce(self):
-        for s, text, hints in self._docs():
+        for s, doc, hints in self._docs():
             if self.stop.is_set():
                 return
-            ids = self.tok.chat_ids(self._build(text))
+            ids = doc if self._pool is not None else self.tok.chat_ids(self._build(doc))
             params = self.engine.default_params(seed=s & 0xFFFFFF, **hints)
             while not self.stop.is_set():
                 try:
