@@ -48,3 +48,25 @@ def test_tile_weight_layout():
         assert flat[off] == w[16 * T + lane % 16, 128 * B + 32 * j + 8 * (lane // 16) + e]
     with pytest.raises(ValueError):
         ops.tile_weight(torch.randn(40, 384))
+
+
+def test_tiled_registry_lifetime():
+    """ops.register_tiled: a copy is found only for the exact tensor object it was
+    registered for (not a view at the same address), in-place entries (None) report
+    the tensor itself as tiled-only, and entries die with their weight."""
+    import gc
+
+    import torch
+
+    w = torch.randn(32, 256)
+    wt = ops.tile_weight(w)
+    ops.register_tiled(w, wt)
+    assert ops.tiled_of(w) is wt and not ops.tiled_only(w)
+    assert ops.tiled_of(w.view(32, 256)) is None
+    v = ops.tile_weight(torch.randn(16, 128))
+    ops.register_tiled(v, None)
+    assert ops.tiled_of(v) is v and ops.tiled_only(v)
+    n = len(ops._TILED)
+    del w, wt, v
+    gc.collect()
+    assert len(ops._TILED) == n - 2
