@@ -118,7 +118,19 @@ __device__ __forceinline__ void wave_lds_sync() {
 // cost 4 workgroups + a 4-way in-kernel merge instead of 16 waves whose partials a
 // second launch (attn_decode_reduce) or a 16-way single-wave merge combines: the
 // decode step of a batch-1 request runs one attention launch per layer.
-template <int NT, int MODE = 0, int NWV = 1>
+// NTK: K / V pages past the first kNtFromPage of a sequence are loaded non-temporal.
+// Those pages belong to one sequence and are read once per step per layer; the leading
+// pages hold the prompt prefix every request shares (prefix cache), which the other
+// sequences' waves re-read from L2 / MALL and keep the default policy.
+constexpr int kNtFromPage = 16;
+
+template <bool NTL>
+__device__ __forceinline__ s16x8 ld16(const bf16_t* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p));
+  else return *reinterpret_cast<const s16x8*>(p);
+}
+
+template <int NT, int MODE = 0, int NWV = 1, bool NTK = false>
 __global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -216,13 +228,23 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
       pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
+      if (NTK && pg0 + j >= kNtFromPage) {
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          kf[mt][ks] = reinterpret_cast<const s16x8*>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g)[0];
+          for (int ks = 0; ks < 4; ++ks)
+            kf[mt][ks] = ld16<true>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vr[i] = reinterpret_cast<const s16x8*>(vb + (g + 4 * i) * kD)[c];
+        for (int i = 0; i < 8; ++i) vr[i] = ld16<true>(vb + (g + 4 * i) * kD + 8 * c);
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+            kf[mt][ks] = ld16<false>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vr[i] = ld16<false>(vb + (g + 4 * i) * kD + 8 * c);
+      }
     };
     auto process = [&](int j, const s16x8 (&kf)[2][4], const s16x8 (&vr)[8]) {
       const int kt = start + j * kPage;
@@ -607,16 +629,22 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
   }
   dim3 grid(num_splits, Hkv, W);
   int32_t* tk = num_splits > 1 ? tickets : nullptr;
-  if (tiles_per_item == 2)
-    attn_decode_kernel<2><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
-                                              bt_stride, seq_q_start, seq_q_len, seq_kv_len,
-                                              work_seq, work_ct, out, out_stride, part_o, part_ml,
-                                              Hq, Hkv, scale_log2, num_splits, PrefixArgs{}, tk);
-  else
-    attn_decode_kernel<1><<<grid, 64, 0, s>>>(q, q_stride, k_cache, v_cache, block_tables,
-                                              bt_stride, seq_q_start, seq_q_len, seq_kv_len,
-                                              work_seq, work_ct, out, out_stride, part_o, part_ml,
-                                              Hq, Hkv, scale_log2, num_splits, PrefixArgs{}, tk);
+  // RFQ_ATTN_NT=1: non-temporal loads for the per-sequence KV pages (NTK above)
+  static const bool ntk = [] {
+    const char* v = getenv("RFQ_ATTN_NT");
+    return v != nullptr && v[0] == '1';
+  }();
+#define RFQ_AD_LAUNCH(T, N)                                                                     \
+  attn_decode_kernel<T, 0, 1, N><<<grid, 64, 0, s>>>(                                            \
+      q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,            \
+      seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,      \
+      num_splits, PrefixArgs{}, tk)
+  if (tiles_per_item == 2) {
+    if (ntk) RFQ_AD_LAUNCH(2, true); else RFQ_AD_LAUNCH(2, false);
+  } else {
+    if (ntk) RFQ_AD_LAUNCH(1, true); else RFQ_AD_LAUNCH(1, false);
+  }
+#undef RFQ_AD_LAUNCH
   // without a ticket buffer the split partials are merged by a second launch
   if (num_splits > 1 && tk == nullptr)
     attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,

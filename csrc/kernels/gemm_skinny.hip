@@ -561,18 +561,20 @@ enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
 // tile's k-blocks follow each other: one sequential 4 KB stream per k-step.
 // NTL (cfg bit 5): weight loads non-temporal (nt): each weight byte is read once per
 // step by one CU, so it need not displace the activations / partials in L2.
-template <int NW, int U, int EPI, bool TL = false, bool NTL = false>
-__global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
-    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
-    bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part, int Nn,
-    unsigned* __restrict__ tile_cnt, NormEpi ep, RopeEpi re, int up_off) {
+// One work unit (16-row tile bt = unit / KS, K slice unit % KS) of the split-K GEMV;
+// every early return below is workgroup-uniform.
+template <int NW, int U, int EPI, bool TL, bool NTL>
+__device__ __forceinline__ void gemv_splitk_unit(
+    int unit, int ntile, const bf16_t* __restrict__ X, int64_t ldx,
+    const bf16_t* __restrict__ W, int K, bf16_t* __restrict__ Y, int64_t ldy, int M, int KS,
+    float* __restrict__ part, int Nn, unsigned* __restrict__ tile_cnt, const NormEpi& ep,
+    const RopeEpi& re, int up_off) {
   constexpr int NT = EPI >= kGvSwi ? 2 : 1;
   __shared__ f32x4 red[NW][NT][64];
   __shared__ float nscratch[17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int ntile = gridDim.x / KS;
-  const int bt = blockIdx.x / KS, slice = blockIdx.x - bt * KS;
+  const int bt = unit / KS, slice = unit - bt * KS;
   // GEMM rows of the tile's NT 16-row blocks
   int row0[NT];
   if constexpr (EPI == kGvRope) {
@@ -780,9 +782,31 @@ __global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
   }
 }
 
+// PERSIST (cfg bit 6, tiled layout only): a grid of about four 4-wave (two 8-wave)
+// workgroups per CU walks the work units in strides of the grid, so a CU's waves stay
+// resident and one unit's reduction / hand-off overlaps the other workgroups' streams
+// instead of a workgroup being torn down and launched per unit.
+template <int NW, int U, int EPI, bool TL = false, bool NTL = false, bool PERSIST = false>
+__global__ __launch_bounds__(NW * 64) void gemv_splitk_kernel(
+    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int K,
+    bf16_t* __restrict__ Y, int64_t ldy, int M, int KS, float* __restrict__ part, int Nn,
+    unsigned* __restrict__ tile_cnt, NormEpi ep, RopeEpi re, int up_off, int units) {
+  if constexpr (!PERSIST) {
+    gemv_splitk_unit<NW, U, EPI, TL, NTL>(blockIdx.x, units / KS, X, ldx, W, K, Y, ldy, M, KS,
+                                          part, Nn, tile_cnt, ep, re, up_off);
+  } else {
+    for (int unit = blockIdx.x; unit < units; unit += gridDim.x) {
+      gemv_splitk_unit<NW, U, EPI, TL, NTL>(unit, units / KS, X, ldx, W, K, Y, ldy, M, KS,
+                                            part, Nn, tile_cnt, ep, re, up_off);
+      __syncthreads();                 // red / nscratch are reused by the next unit
+    }
+  }
+}
+
 // cfg bits: [1:0] KS = 2 << bits (2, 4, 8, 16); bit 2: 8 waves (else 4); bit 3: U = 2 (else 4;
 // U = 8 needs 256+ VGPRs: the X fragments take as many registers as the W ones);
-// bit 4: W in the decode-tiled layout (TL above); bit 5: non-temporal weight loads (NTL).
+// bit 4: W in the decode-tiled layout (TL above); bit 5: non-temporal weight loads (NTL);
+// bit 6: persistent grid (PERSIST, with bit 4 only).
 // part: fp32 [KS][M][Nn] (Nn = GEMM rows); tile_cnt: one zeroed uint32 per output tile
 // (left at zero).  ntile: N/16 (plain, norm), F/16 (swiglu), N/32 (rope).
 template <int EPI>
@@ -791,16 +815,21 @@ static void launch_gemv_splitk_epi(const bf16_t* X, int64_t ldx, const bf16_t* W
                                    unsigned* tile_cnt, const NormEpi& ep, const RopeEpi& re,
                                    int up_off, hipStream_t s) {
   const int KS = 2 << (cfg & 3);
-  const dim3 grid(ntile * KS);
-#define GV_LAUNCH1(nw, u, tl, nt)                                                               \
-  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI, tl, nt>), grid, dim3(nw * 64), 0, s, X, ldx, \
-                     W, K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off)
+  const int units = ntile * KS;
+  const bool persist = (cfg & 64) && (cfg & 16);          // tiled layout only
+  const int per_cu = (cfg & 4) ? 2 : 4;                   // 8-wave : 4-wave workgroups
+  const dim3 grid(persist ? min(units, 256 * per_cu) : units);
+#define GV_LAUNCH1(nw, u, tl, nt, pe)                                                           \
+  hipLaunchKernelGGL((gemv_splitk_kernel<nw, u, EPI, tl, nt, pe>), grid, dim3(nw * 64), 0, s, X, \
+                     ldx, W, K, Y, ldy, M, KS, part, Nn, tile_cnt, ep, re, up_off, units)
 #define GV_LAUNCH(nw, u)                                                                        \
-  switch ((cfg >> 4) & 3) {                                                                     \
-    case 0: GV_LAUNCH1(nw, u, false, false); break;                                             \
-    case 1: GV_LAUNCH1(nw, u, true, false); break;                                              \
-    case 2: GV_LAUNCH1(nw, u, false, true); break;                                              \
-    default: GV_LAUNCH1(nw, u, true, true); break;                                              \
+  switch (((cfg >> 4) & 3) | (persist ? 4 : 0)) {                                               \
+    case 0: GV_LAUNCH1(nw, u, false, false, false); break;                                      \
+    case 1: GV_LAUNCH1(nw, u, true, false, false); break;                                       \
+    case 2: GV_LAUNCH1(nw, u, false, true, false); break;                                       \
+    case 3: GV_LAUNCH1(nw, u, true, true, false); break;                                        \
+    case 5: GV_LAUNCH1(nw, u, true, false, true); break;                                        \
+    default: GV_LAUNCH1(nw, u, true, true, true); break;                                        \
   }
   switch ((cfg >> 2) & 3) {
     case 0: GV_LAUNCH(4, 4); break;

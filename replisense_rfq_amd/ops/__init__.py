@@ -22,7 +22,7 @@ __all__ = [
     "set_rope_plan", "set_swiglu_plan", "linear_swiglu", "splitk_ws",
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
     "gemm_dense", "gemm_dense_ok", "swiglu_large", "tile_weight", "untile_weight",
-    "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT",
+    "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT", "SPLITK_PERSIST",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -163,6 +163,7 @@ SPLITK_CFGS = (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14)
 
 SPLITK_TILED = 16        # split-K GEMV cfg bit: W in the decode-tiled layout (tile_weight)
 SPLITK_NT = 32           # split-K GEMV cfg bit: non-temporal weight loads
+SPLITK_PERSIST = 64      # split-K GEMV cfg bit: persistent grid (tiled layout only)
 
 
 def tile_weight(w: torch.Tensor) -> torch.Tensor:

@@ -788,12 +788,13 @@ def test_gemv_splitk_rope_kv(gpu, M, cfg, Hq, Hkv, K):
 
 
 @pytest.mark.parametrize("M", [1, 5, 16])
-@pytest.mark.parametrize("cfg", [0, 5, 10, 14])
+@pytest.mark.parametrize("cfg", [0, 5, 10, 14, 0 | 32 | 64, 5 | 64, 10 | 32 | 64, 14 | 64])
 def test_gemv_splitk_tiled_layout(gpu, M, cfg):
-    """Split-K GEMV on the decode-tiled weight layout (ops.tile_weight, cfg bit 16):
-    the same loads in a different memory order, so every epilogue (plain, norm, SwiGLU,
-    RoPE + KV append) is bit-identical to the row-major kernel, which the fp32 oracles
-    above cover; plus the plain result vs fp32 torch."""
+    """Split-K GEMV on the decode-tiled weight layout (ops.tile_weight, cfg bit 16), also
+    with non-temporal loads (32) and the persistent grid (64): the same loads in a
+    different memory order / work order, so every epilogue (plain, norm, SwiGLU, RoPE +
+    KV append) is bit-identical to the row-major kernel, which the fp32 oracles above
+    cover; plus the plain result vs fp32 torch."""
     torch.manual_seed(M * 29 + cfg)
     T = ops.SPLITK_TILED
     part, tiles = ops.splitk_ws(gpu)

@@ -10,6 +10,7 @@ Usage (GPU box): python tools/bench_gemv_tiled.py > gpurun_out/gemv_tiled.jsonl
 from __future__ import annotations
 
 import json
+import os
 import statistics
 import sys
 
@@ -49,10 +50,15 @@ def main():
                 _native.ops().gemv_splitk(x, w, y, part, tiles, cfg)
 
         res = {"shape": name, "rows": rows, "K": K, "layers": L, "MB": round(rows * K * 2 / 1e6, 1)}
-        for tiled, nt in ((False, False), (True, False), (False, True), (True, True)):
+        layouts = [(False, False, False), (True, False, False), (True, True, False),
+                   (True, True, True)]
+        if os.environ.get("GEMV_BENCH_ALL") == "1":
+            layouts.insert(2, (False, True, False))
+        for tiled, nt, pe in layouts:
             best = None
             for c in ops.SPLITK_CFGS:
-                cfg = c | (ops.SPLITK_TILED if tiled else 0) | (ops.SPLITK_NT if nt else 0)
+                cfg = (c | (ops.SPLITK_TILED if tiled else 0) | (ops.SPLITK_NT if nt else 0)
+                       | (ops.SPLITK_PERSIST if pe else 0))
                 ntile = ncol // 16
                 if not ops.splitk_fits(dev, c, 1, rows, ntile) or K // 128 < (2 << (c & 3)):
                     continue
@@ -84,11 +90,12 @@ def main():
                 if best is None or t < best[1]:
                     best = (cfg, t)
                 del g
-            key = ("tiled" if tiled else "rowmajor") + ("_nt" if nt else "")
+            key = ("tiled" if tiled else "rowmajor") + ("_nt" if nt else "") + ("_p" if pe else "")
             res[key] = {"cfg": best[0], "us": round(best[1], 2),
                         "TBps": round(rows * K * 2 / best[1] / 1e6, 2)}
         res["speedup"] = round(res["rowmajor"]["us"] / res["tiled"]["us"], 3)
         res["speedup_nt"] = round(res["rowmajor"]["us"] / res["tiled_nt"]["us"], 3)
+        res["speedup_nt_p"] = round(res["rowmajor"]["us"] / res["tiled_nt_p"]["us"], 3)
         print(json.dumps(res), flush=True)
         del ws, wts
 
