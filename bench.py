@@ -158,6 +158,7 @@ def _gemm_plan_summary() -> dict:
 def _host_timers(engine) -> dict:
     st = engine.runner.stats
     return {"pack_s": st.get("pack_s", 0.0), "launch_s": st.get("launch_s", 0.0),
+            "overlap_s": st.get("overlap_s", 0.0),
             "wait_s": st.get("wait_s", 0.0), "post_s": engine.timers.get("post_s", 0.0),
             "execute_s": engine.timers.get("execute_s", 0.0)}
 
@@ -401,7 +402,9 @@ def main():
                        "profile": "synthetic", "decode_hints": True,
                        "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
                        # prompts built + tokenised in a spawned process (benchmarks.stream)
-                       "producer": os.environ.get("RFQ_BENCH_PRODUCER", "process")},
+                       "producer": os.environ.get("RFQ_BENCH_PRODUCER", "process"),
+                       "admit": ("during step" if os.environ.get("RFQ_BENCH_OVERLAP_ADMIT", "1")
+                                 != "0" else "between steps")},
             # latency under load of the documents completed in the timed window
             # (submission -> last token, closed loop at in_flight_per_replica)
             "loaded_latency_s": loaded["e2e_s"],

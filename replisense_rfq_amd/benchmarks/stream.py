@@ -102,7 +102,7 @@ class DocStream:
 
     def __init__(self, engine, dp_rank: int, seed: int, in_flight: int,
                  formats: tuple | None = None, parse_procs: int = 4,
-                 producer: str | None = None):
+                 producer: str | None = None, overlap_admit: bool | None = None):
         from ..service.extract import build_messages
         from ..service.prompt import register_prompt_prefix
         from ..utils import synth
@@ -131,6 +131,9 @@ class DocStream:
         import os
 
         mode = producer or os.environ.get("RFQ_BENCH_PRODUCER", "process")
+        # admit new documents while a step runs on the device (runner.busy_hook)
+        self.overlap_admit = (overlap_admit if overlap_admit is not None
+                              else os.environ.get("RFQ_BENCH_OVERLAP_ADMIT", "1") != "0")
         self._proc = None
         self.thread = None
         if self.formats is None and mode == "process":
@@ -199,16 +202,34 @@ class DocStream:
         """Step until ``target`` documents completed in total (or perf_counter passes
         ``deadline``; then returns False)."""
         eng = self.engine
-        while self.completed < target:
-            if deadline is not None and time.perf_counter() > deadline:
-                return False
-            self._top_up(block=True)
-            if not eng.has_work():
-                continue
-            done = eng.step()
-            self.live -= len(done)
-            self.completed += len(done)
-            self.finished.extend(done)
+        runner = getattr(eng, "runner", None)
+        hooked = [False]
+
+        def admit():                     # runs while the step executes on the device
+            hooked[0] = True
+            self._top_up(block=False)
+
+        if runner is not None and self.overlap_admit:
+            runner.busy_hook = admit
+        try:
+            while self.completed < target:
+                if deadline is not None and time.perf_counter() > deadline:
+                    return False
+                # the documents retired by the previous step are replaced during this
+                # step's device time (admit) instead of between steps, where the GPU
+                # idles; only an empty engine (or a step that never launched) tops up here
+                if not hooked[0] or not eng.has_work():
+                    self._top_up(block=True)
+                if not eng.has_work():
+                    continue
+                hooked[0] = False
+                done = eng.step()
+                self.live -= len(done)
+                self.completed += len(done)
+                self.finished.extend(done)
+        finally:
+            if runner is not None:
+                runner.busy_hook = None
         return True
 
     def close(self):

@@ -90,9 +90,14 @@ class ModelRunner:
         if tp.enabled:
             self._setup_control_plane()
         # host-side split of a step: pack (scheduler), launch (upload + forward + sampler
-        # enqueue), wait (device drain + token readback); forward_s = launch + wait
+        # enqueue), overlap (busy_hook), wait (device drain + token readback)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0, "forward_s": 0.0,
-                      "pack_s": 0.0, "launch_s": 0.0, "wait_s": 0.0}
+                      "pack_s": 0.0, "launch_s": 0.0, "overlap_s": 0.0, "wait_s": 0.0}
+        # host work to run while the step executes on the device (after the launch,
+        # before the token readback), e.g. admitting new requests into the core: the
+        # core is between schedule_and_pack and post then, and add() only appends to
+        # the waiting queue, so the admitted requests are scheduled from the next step
+        self.busy_hook = None
 
     def _decode_splits(self, NA: int, max_ctx: int, graph: bool) -> int:
         if NA == 0 or not self.is_cuda:
@@ -262,9 +267,13 @@ class ModelRunner:
             logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
         t1 = time.perf_counter()
+        if self.busy_hook is not None:
+            self.busy_hook()
+        t2 = time.perf_counter()
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
         self.stats["launch_s"] += t1 - t0
-        self.stats["wait_s"] += time.perf_counter() - t1
+        self.stats["overlap_s"] += t2 - t1
+        self.stats["wait_s"] += time.perf_counter() - t2
         if self.check_finite:
             bad = int(self._nonfinite[0])
             if bad:

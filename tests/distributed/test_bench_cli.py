@@ -174,7 +174,8 @@ def test_bench_driver_flags_time_budget():
     assert out["vs_baseline"] is None
     # host-side split of the timed window (scheduler, launch, device wait, post)
     host = out["engine"]["host_s"]
-    assert {"pack_s", "launch_s", "wait_s", "post_s", "execute_s"} <= set(host)
+    assert {"pack_s", "launch_s", "overlap_s", "wait_s", "post_s", "execute_s"} <= set(host)
+    assert out["config"]["admit"] == "during step" and host["overlap_s"] > 0
     assert all(v >= 0 for v in host.values())
     assert host["execute_s"] <= out["ms_per_step"] * 20 / 1e3 + 1.0
 

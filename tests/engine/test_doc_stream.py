@@ -32,3 +32,33 @@ def test_process_producer_matches_thread():
         assert list(ia) == list(ib)
         assert (sa.seed, sa.min_items, sa.profile, sa.temperature) == \
             (sb.seed, sb.min_items, sb.profile, sb.temperature)
+
+
+def test_overlapped_admission_keeps_depth():
+    """Documents retired by a step are replaced during the next step's device time
+    (runner.busy_hook) instead of between steps; the stream still completes its target
+    with the engine holding exactly `live` requests, and the hook is removed after."""
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4,
+                                 decode_hints=True))
+    s = DocStream(eng, 0, 3, 4, producer="thread", overlap_admit=True)
+    seen = []
+    orig = s._top_up
+
+    def spy(block):
+        orig(block)
+        seen.append((block, s.live))
+
+    s._top_up = spy
+    try:
+        assert s.run_until(6, deadline=None)
+    finally:
+        s._top_up = orig
+        s.close()
+    assert s.completed >= 6
+    assert eng.runner.busy_hook is None
+    assert eng.runner.stats["overlap_s"] > 0
+    # after the first fill, every top-up ran inside a step (non-blocking) and kept the
+    # stream at its depth
+    assert seen[0][0] is True
+    assert any(not b for b, _ in seen[1:])
+    assert all(live <= 4 for _, live in seen)
