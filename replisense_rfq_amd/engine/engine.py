@@ -338,6 +338,7 @@ class AsyncEngine:
     def __init__(self, engine: LLMEngine):
         self.engine = engine          # (LLMEngine set the short GIL switch interval)
         self._inbox: queue.Queue = queue.Queue()
+        self._held: list = []                    # inbox messages deferred to the loop top
         self._stop = threading.Event()
         self._wake = threading.Event()
         self.error: BaseException | None = None
@@ -364,20 +365,48 @@ class AsyncEngine:
     def healthy(self) -> bool:
         return not self.stalled and self._thread.is_alive()
 
+    def _drain(self, in_step: bool = False):
+        """Apply the inbox.  ``in_step``: called by the runner while a step executes on
+        the device (runner.busy_hook), so new requests are admitted during GPU time
+        instead of between steps; aborts (which free KV blocks of sequences that may
+        be in the running step) and any add that raised wait for the loop top."""
+        if not in_step:
+            held, self._held = self._held, []
+            for msg in held:
+                self._apply(msg)
+        try:
+            while True:
+                msg = self._inbox.get_nowait()
+                if in_step and msg[0] == "add":
+                    try:
+                        self._apply(msg)
+                    except Exception:  # noqa: BLE001 - replayed (and raised) at the loop top
+                        self._held.append(msg)
+                elif in_step:
+                    self._held.append(msg)
+                else:
+                    self._apply(msg)
+        except queue.Empty:
+            pass
+
+    def _in_step(self):
+        self._drain(in_step=True)
+
+    def _apply(self, msg):
+        eng = self.engine
+        if msg[0] == "add":
+            _, prompt, params, cb, req = msg
+            req.seq = eng.add_request(prompt, params, cb)
+        elif msg[1].seq is not None:             # ("abort", req): deadline expired
+            eng.abort_request(msg[1].seq, "timeout")
+
     def _loop(self):
         eng = self.engine
+        runner = getattr(eng, "runner", None)
+        if runner is not None:
+            runner.busy_hook = self._in_step
         while not self._stop.is_set():
-            try:
-                while True:
-                    msg = self._inbox.get_nowait()
-                    if msg[0] == "add":
-                        _, prompt, params, cb, req = msg
-                        req.seq = eng.add_request(prompt, params, cb)
-                    else:                       # ("abort", req): deadline expired
-                        if msg[1].seq is not None:
-                            eng.abort_request(msg[1].seq, "timeout")
-            except queue.Empty:
-                pass
+            self._drain()
             if eng.has_work():
                 self.step_started = time.monotonic()
                 try:
@@ -416,3 +445,6 @@ class AsyncEngine:
         self._stop.set()
         self._wake.set()
         self._thread.join(timeout=5)
+        runner = getattr(self.engine, "runner", None)
+        if runner is not None and runner.busy_hook == self._in_step:
+            runner.busy_hook = None

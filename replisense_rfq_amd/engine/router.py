@@ -81,22 +81,50 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
     outq.put(("ready", idx, None))
     pending = {}
     served = 0
+    held = []                                  # inbox messages deferred to the loop top
+
+    def apply(msg) -> bool:                    # False: shut down
+        if msg is None:
+            return False
+        if msg[0] == "abort":                  # the client's deadline expired
+            for sid, (r, s) in list(pending.items()):
+                if r == msg[1]:
+                    eng.abort_request(s, "timeout")
+                    pending.pop(sid, None)
+            return True
+        rid, prompt, p = msg
+        seq = eng.add_request(prompt, SamplingParams(**p))
+        pending[seq.req_id] = (rid, seq)
+        return True
+
+    def admit_in_step():
+        """runner.busy_hook: admit new requests while the step runs on the device;
+        aborts and shutdown (which touch sequences of the running step), and an add
+        that raised, wait for the loop top."""
+        try:
+            while True:
+                msg = inq.get_nowait()
+                if msg is not None and msg[0] != "abort":
+                    try:
+                        apply(msg)
+                        continue
+                    except Exception:  # noqa: BLE001 - replayed (and raised) at the loop top
+                        pass
+                held.append(msg)
+        except queue.Empty:
+            pass
+
+    eng.runner.busy_hook = admit_in_step
     while True:
         try:
             while True:
-                msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
-                if msg is None:
+                if held:
+                    msg = held.pop(0)
+                else:
+                    msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
+                if not apply(msg):
                     eng.shutdown()                 # release the TP followers
                     return
-                if msg[0] == "abort":               # the client's deadline expired
-                    for sid, (r, s) in list(pending.items()):
-                        if r == msg[1]:
-                            eng.abort_request(s, "timeout")
-                            pending.pop(sid, None)
-                    continue
-                rid, prompt, p = msg
-                seq = eng.add_request(prompt, SamplingParams(**p))
-                pending[seq.req_id] = (rid, seq)
         except queue.Empty:
             pass
         if not eng.has_work():

@@ -3,6 +3,7 @@ chunking / preemption, end-to-end constrained generation, determinism, async
 front-end, runner packing."""
 import asyncio
 import json
+import time
 
 import numpy as np
 import pytest
@@ -239,3 +240,45 @@ def test_graph_key_latency_fallthrough():
     assert core.graph_key(17, 300) == (-1, -1)    # bucket 32: eager, no cross-bucket pad
     assert core.graph_key(64, 512) == (64, 512)
     assert core.graph_key(65, 65) == (-1, -1)     # beyond the captured buckets
+
+
+def test_async_engine_admits_during_step_defers_aborts(engine):
+    """AsyncEngine drains its inbox from runner.busy_hook while a step runs on the
+    device: adds are applied there, aborts (which free KV blocks of sequences that may
+    be in the running step) wait for the loop top, in order."""
+    from replisense_rfq_amd.engine.engine import _Request
+
+    aeng = AsyncEngine.__new__(AsyncEngine)          # no loop thread: drive _drain by hand
+    aeng.engine = engine
+    aeng._inbox = __import__("queue").Queue()
+    aeng._held = []
+    got = []
+    req, req2 = _Request(), _Request()
+    p = _prompts(engine, 2, base=70)
+    aeng._inbox.put(("add", p[0], engine.default_params(max_tokens=8), got.append, req))
+    aeng._inbox.put(("abort", req))
+    aeng._inbox.put(("add", p[1], engine.default_params(max_tokens=8), got.append, req2))
+    aeng._drain(in_step=True)
+    assert req.seq is not None and req2.seq is not None     # both adds applied in-step
+    assert [m[0] for m in aeng._held] == ["abort"]           # the abort was deferred
+    aeng._drain()                                            # loop top: abort applied
+    assert aeng._held == [] and req.seq.finish_reason == "timeout"
+    assert got and got[0] is req.seq
+    while engine.has_work():
+        engine.step()
+    assert req2.seq.finish_reason not in (None, "timeout")        # ran to its own end
+
+
+def test_async_engine_hook_installed_and_removed(engine):
+    aeng = AsyncEngine(engine)
+    try:
+        deadline = time.time() + 10
+        while engine.runner.busy_hook is None and time.time() < deadline:
+            time.sleep(0.01)
+        assert engine.runner.busy_hook == aeng._in_step
+        seq = asyncio.run(aeng.generate(_prompts(engine, 1, base=80)[0],
+                                        engine.default_params(max_tokens=8)))
+        assert seq.finish_reason not in (None, "timeout", "engine_error")
+    finally:
+        aeng.shutdown()
+    assert engine.runner.busy_hook is None
