@@ -267,13 +267,21 @@ class ModelRunner:
             logits = self.model.forward(self._meta(v, header))
             out = self._sample(logits, v["midx"], v["temps"], v["seeds"])
         t1 = time.perf_counter()
+        hook_err = None
         if self.busy_hook is not None:
-            self.busy_hook()
+            try:
+                self.busy_hook()
+            except Exception as e:  # noqa: BLE001 - re-raised once the step has drained
+                hook_err = e
         t2 = time.perf_counter()
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
         self.stats["launch_s"] += t1 - t0
         self.stats["overlap_s"] += t2 - t1
         self.stats["wait_s"] += time.perf_counter() - t2
+        if hook_err is not None:
+            # the device work of this step is finished (readback above), so the caller
+            # sees the hook's failure with no kernel of the step still in flight
+            raise hook_err
         if self.check_finite:
             bad = int(self._nonfinite[0])
             if bad:

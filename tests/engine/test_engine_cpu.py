@@ -282,3 +282,28 @@ def test_async_engine_hook_installed_and_removed(engine):
     finally:
         aeng.shutdown()
     assert engine.runner.busy_hook is None
+
+
+def test_busy_hook_failure_raised_after_step_drains(engine):
+    """A busy_hook that raises does not cut the step short: the runner reads the
+    step's tokens back (no kernel left in flight) and then re-raises the hook's error;
+    the next step runs normally."""
+    calls = []
+
+    def bad_hook():
+        calls.append(engine.runner.stats["steps"])
+        raise ValueError("hook failed")
+
+    p = _prompts(engine, 1, base=90)
+    seq = engine.add_request(p[0], engine.default_params(max_tokens=8), None)
+    engine.runner.busy_hook = bad_hook
+    try:
+        with pytest.raises(ValueError, match="hook failed"):
+            while engine.has_work():
+                engine.step()
+    finally:
+        engine.runner.busy_hook = None
+    assert calls and engine.runner.stats["wait_s"] >= 0.0
+    engine.abort_request(seq, "test")
+    while engine.has_work():
+        engine.step()
