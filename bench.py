@@ -42,7 +42,8 @@ import threading
 import time
 
 from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, loaded_latency,
-                                                  single_stream as _single_stream, validate)
+                                                  single_stream as _single_stream, token_shape,
+                                                  validate)
 
 BASELINE_P50_S = 0.883          # Groq llama3-70b p50 server time per request
 
@@ -82,9 +83,14 @@ def parse():
     ap.add_argument("--phases", default="auto",
                     help="extra phases after the timed window: comma list of http, mixtral, "
                          "70b; 'auto' = all on the 1-GPU run of the 8B bench, 'none' = off")
-    ap.add_argument("--phase-budget", type=float, default=300.0,
+    ap.add_argument("--phase-budget", type=float, default=400.0,
                     help="seconds for all extra phases together (each is bounded; a watchdog "
                          "prints the JSON line if they overrun)")
+    ap.add_argument("--http-open-rate", type=float, default=0.0,
+                    help="open-loop HTTP phase: offered requests/s (0 = 90 %% of the "
+                         "timed window's docs/s per replica)")
+    ap.add_argument("--http-open-warm", type=float, default=20.0)
+    ap.add_argument("--http-open-measure", type=float, default=40.0)
     ap.add_argument("--http-docs", type=int, default=512)
     ap.add_argument("--http-clients", type=int, default=64)
     ap.add_argument("--mixtral-model", default="mixtral-8x7b")
@@ -121,8 +127,8 @@ def _phase_list(args, world: int) -> list:
     if v in ("", "none", "0"):
         return []
     if v == "auto":
-        return ["http", "mixtral", "70b"] if (world == 1 and args.tp == 1
-                                              and args.model == "llama3-8b") else []
+        return ["http_open", "http", "mixtral", "70b"] if (world == 1 and args.tp == 1
+                                                           and args.model == "llama3-8b") else []
     return [p for p in v.split(",") if p]
 
 
@@ -233,6 +239,11 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
         eng = LLMEngine(cfg, tp=wctx)
         res["init_s"] = round(time.perf_counter() - t0, 1)
         res["custom_allreduce"] = wctx.car is not None
+        # why the custom xGMI all-reduce is (not) in use: "ok", "set-up failed ...",
+        # "self-test failed ...", or off on CPU / by config
+        res["car_status"] = wctx.car_status or ("ok" if wctx.car is not None else
+                                                "off" if not cfg.custom_allreduce else
+                                                "not enabled on this device")
         if wctx.rank == 0:
             try:
                 lat, detail = latency(eng, 0, args.tp_latency_runs)
@@ -244,7 +255,7 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
                     stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
                     warm = max(1, args.tp_in_flight // 2)
                     stream.run_until(warm)
-                    stream.finished.clear()
+                    stream.clear_window()
                     if eng.device.type == "cuda":
                         torch.cuda.synchronize()
                     t1 = time.perf_counter()
@@ -277,6 +288,12 @@ def main():
     t_start = time.perf_counter()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args))
+
+    # before anything touches HIP: this rank (and the producer / post-processing
+    # processes it spawns) runs on its GPU's NUMA-local cores
+    from replisense_rfq_amd.utils.affinity import pin_to_gpu
+
+    affinity = pin_to_gpu(int(os.environ.get("LOCAL_RANK", "0")))
 
     import torch
     import torch.distributed as dist
@@ -333,7 +350,7 @@ def main():
     mark("warmup")
     phase(lambda: stream.run_until(args.warmup * per))
     if stream is not None:
-        stream.finished.clear()
+        stream.clear_window()
     steps0 = engine.num_steps
     host0 = _host_timers(engine)
     barrier()
@@ -352,9 +369,15 @@ def main():
         dt = float(t.item())
     shape, loaded = {}, {"e2e_s": None, "ttft_s": None}
     done_in_window = 0
+    post = {}
     if stream is not None:
         done_in_window = stream.completed - args.warmup * per
-        shape = validate(engine, stream.finished[:2048])
+        # every document counted in the window was post-processed inside it (detokenise
+        # -> JSON recovery -> pydantic validation, rfq_agent.py:185-206)
+        shape = dict(token_shape(stream.finished), valid=stream.window_valid())
+        post = {"mode": stream.post_mode, "validated": len(stream.finished),
+                "fallback": stream.fallback,
+                "failed": len(stream.finished) - stream.valid - stream.fallback}
         loaded = loaded_latency(stream.finished)
         stream.close()
     stats = engine.stats()
@@ -404,7 +427,11 @@ def main():
                        # prompts built + tokenised in a spawned process (benchmarks.stream)
                        "producer": os.environ.get("RFQ_BENCH_PRODUCER", "process"),
                        "admit": ("during step" if os.environ.get("RFQ_BENCH_OVERLAP_ADMIT", "1")
-                                 != "0" else "between steps")},
+                                 != "0" else "between steps"),
+                       # a document counts once its post-processing (detokenise, JSON
+                       # recovery, pydantic validation) has run inside the timed window
+                       "counted": "validated in window"},
+            "postprocess": post,
             # latency under load of the documents completed in the timed window
             # (submission -> last token, closed loop at in_flight_per_replica)
             "loaded_latency_s": loaded["e2e_s"],
@@ -431,6 +458,7 @@ def main():
                        # forward launch, device wait, post-processing (grammar, retire)
                        "host_s": host,
                        "kv_blocks": stats.get("blocks"), "preempted": stats.get("preempted"),
+                       "affinity": affinity,
                        "wall_s": round(time.perf_counter() - t_start, 1)},
         }
 
@@ -456,6 +484,18 @@ def main():
         guard = threading.Timer(args.phase_budget + 120.0, on_overrun)
         guard.daemon = True
         guard.start()
+        if "http_open" in phases:
+            mark("phase:http_open")
+            rate = args.http_open_rate or 0.9 * out["value"] / max(1, dp_world)
+            r = ph.http_open_loop_phase(
+                engine, rate=rate, warm_s=args.http_open_warm,
+                measure_s=args.http_open_measure,
+                budget_s=min(args.http_open_warm + args.http_open_measure + 60.0, left()),
+                seed=args.seed)
+            r["engine_docs_per_s"] = round(out["value"] / max(1, dp_world), 3)
+            if r.get("docs_per_s"):
+                r["http_vs_engine"] = round(r["docs_per_s"] / r["engine_docs_per_s"], 3)
+            out["phases"]["http_open_loop"] = r
         if "http" in phases:
             mark("phase:http")
             out["phases"]["http_upload"] = ph.http_upload_phase(

@@ -280,7 +280,7 @@ async def _upload_file_param(request: Request):
     files = form.get("file")
     if not files:
         raise RequestValidationError(missing_field_detail("file"))
-    f = files[0]
+    f = files[-1]                  # the last part of that name, as Starlette's form.get()
     if isinstance(f, str):
         raise RequestValidationError([{"type": "value_error", "loc": ["body", "file"],
                                        "msg": "Value error, Expected UploadFile, received: "

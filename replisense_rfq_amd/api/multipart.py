@@ -111,7 +111,13 @@ class MultipartStream:
         p = self.part
         self.part = None
         if p is not None and p.name is not None:
-            self.fields.setdefault(p.name, []).append(p.value())
+            # a repeated field name keeps the LAST part (what Starlette's form.get()
+            # hands a single-valued FastAPI parameter); the earlier part's spool is
+            # closed, so repeated parts never hold more than one file's bytes
+            for old in self.fields.get(p.name, []):
+                if not isinstance(old, str):
+                    old.file.close()
+            self.fields[p.name] = [p.value()]
 
     def feed(self, chunk: bytes) -> None:
         self.buf += chunk
@@ -158,8 +164,6 @@ class MultipartStream:
                     if self.nfiles > MAX_FILES:
                         raise MultipartLimitError(
                             f"Too many files. Maximum number of files is {MAX_FILES}.")
-                    if part.name in self.fields:      # only files[0] is ever read
-                        part.limit = -1
                 else:
                     self.nfields += 1
                     if self.nfields > MAX_FIELDS:

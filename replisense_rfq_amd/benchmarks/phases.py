@@ -2,6 +2,9 @@
 Llama-3-8B docs/s window, so BASELINE.json's other configs get driver-clocked
 numbers in the same JSON line:
 
+  http_open the HTTP surface at ~90 % of the engine's docs/s: open-loop Poisson
+            arrivals of /parse-text/ and /upload/ through uvicorn + AsyncEngine
+            (docs/s, latency p50/p99, failures) -- http_open_loop_phase.
   http      config 3: the FastAPI service (api/main.py, the reference's
             app/main.py:205-288 contract) served in-process over real sockets by
             uvicorn, on the 8B engine the bench already built; ``clients``
@@ -180,6 +183,178 @@ def http_upload_phase(engine, n_docs: int = 512, clients: int = 64, client_procs
     return res
 
 
+# ------------------------------------------------------------ open-loop HTTP load
+async def _open_loop(url: str, sched: list, t0: float, deadline: float):
+    """Fire every scheduled request at its arrival time, never waiting for earlier
+    responses (open loop).  ``sched``: [(offset_s, kind, payload)].  Returns
+    [(offset_s, done_offset_s, latency_s, ok)]."""
+    import asyncio
+
+    import aiohttp
+
+    out = []
+
+    async def one(sess, off, kind, payload):
+        t_send = time.perf_counter()
+        status, body = 0, {}
+        try:
+            if kind == "text":
+                async with sess.post(url + "/parse-text/", json=payload) as r:
+                    status, body = r.status, await r.json()
+            else:
+                name, blob = payload
+                form = aiohttp.FormData()
+                form.add_field("file", blob, filename=name)
+                async with sess.post(url + "/upload/", data=form) as r:
+                    status, body = r.status, await r.json()
+        except (aiohttp.ClientError, asyncio.TimeoutError, ValueError):
+            pass
+        t_done = time.perf_counter()
+        data = body.get("data", {}) if status == 200 else {}
+        ok = bool(data.get("success")) and "validation warnings" not in data.get("message", "")
+        out.append((off, t_done - t0, t_done - t_send, ok))
+
+    conn = aiohttp.TCPConnector(limit=0)
+    tasks = []
+    async with aiohttp.ClientSession(connector=conn,
+                                     timeout=aiohttp.ClientTimeout(total=60)) as sess:
+        for off, kind, payload in sched:
+            delay = t0 + off - time.perf_counter()
+            if delay > 0:
+                await asyncio.sleep(delay)
+            if time.time() > deadline:
+                break
+            tasks.append(asyncio.ensure_future(one(sess, off, kind, payload)))
+        if tasks:
+            await asyncio.wait(tasks, timeout=max(1.0, deadline - time.time()))
+    return out
+
+
+def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt, out_q):
+    """One client process: a Poisson arrival stream at ``rate`` req/s for ``duration``
+    s of /parse-text/ emails and (``upload_share``) /upload/ attachments."""
+    import asyncio
+    import random
+
+    from ..utils import docgen, synth
+
+    rng = random.Random(seed)
+    sched, t, i = [], 0.0, 0
+    fmts = ("pdf", "xlsx", "docx")
+    while True:
+        t += rng.expovariate(rate)
+        if t >= duration:
+            break
+        d = synth.make_rfq(seed * 1_000_003 + i)
+        if rng.random() < upload_share:
+            f = fmts[i % 3]
+            sched.append((t, "file", (f"rfq_{seed}_{i}.{f}", docgen.rfq_attachment(d, f))))
+        else:
+            sched.append((t, "text", {"text": d.text, "source_file": f"email_{seed}_{i}"}))
+        i += 1
+    start_evt.wait()
+    t0 = time.perf_counter()
+    out_q.put(asyncio.run(_open_loop(url, sched, t0, deadline)))
+
+
+def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: float = 40.0,
+                         upload_share: float = 0.25, client_procs: int = 8,
+                         parse_procs: int = 4, budget_s: float = 120.0, seed: int = 0) -> dict:
+    """does the HTTP surface sustain the engine's throughput?
+
+    uvicorn + the FastAPI app (api/main.py, the reference's app/main.py:205-344
+    contract) + AsyncEngine on the already-built engine; ``client_procs`` spawned
+    processes issue Poisson arrivals at ``rate`` requests/s in total (open loop: an
+    arrival never waits for an earlier response), ``upload_share`` of them /upload/
+    attachments (pdf/xlsx/docx through the parser pool), the rest /parse-text/.
+    After ``warm_s`` of ramp-up, the window of ``measure_s`` reports the documents
+    completed per second (every one validated by the service and enveloped), the
+    latency of the requests sent inside the window, and timeouts / errors."""
+    import multiprocessing as mp
+
+    import uvicorn
+
+    from ..api import main as api
+    from ..engine.engine import AsyncEngine
+    from ..service.extract import EngineBackend, ExtractService
+
+    t_start = time.perf_counter()
+    res = {"config": "open-loop Poisson arrivals, /parse-text/ + /upload/ through uvicorn",
+           "offered_rate": round(rate, 2), "upload_share": upload_share,
+           "warm_s": warm_s, "measure_s": measure_s, "status": "running"}
+    import logging
+
+    pkg_log = logging.getLogger("replisense_rfq_amd")
+    level0 = pkg_log.level
+    pkg_log.setLevel(logging.WARNING)
+    hints0 = engine.cfg.decode_hints
+    engine.cfg.decode_hints = True
+    aeng = AsyncEngine(engine)
+    api.provide_generator(ExtractService(EngineBackend(engine, aeng)))
+    os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
+    port = _free_port()
+    server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
+                                           log_level="warning", access_log=False,
+                                           backlog=4096))
+    th = threading.Thread(target=server.run, name="bench-uvicorn-open", daemon=True)
+    th.start()
+    procs = []
+    try:
+        t0 = time.time()
+        while not server.started and time.time() - t0 < 60 and th.is_alive():
+            time.sleep(0.05)
+        if not server.started:
+            raise RuntimeError("uvicorn did not start")
+        url = f"http://127.0.0.1:{port}"
+        ctx = mp.get_context("spawn")
+        dur = warm_s + measure_s
+        deadline = time.time() + max(dur + 10.0, budget_s - (time.perf_counter() - t_start))
+        start_evt, out_q = ctx.Event(), ctx.Queue()
+        procs = [ctx.Process(target=_open_loop_proc,
+                             args=(url, rate / client_procs, dur, 7_000 + 101 * i + seed,
+                                   upload_share, deadline, start_evt, out_q), daemon=True)
+                 for i in range(client_procs)]
+        for p in procs:
+            p.start()
+        time.sleep(3.0)                       # clients import aiohttp and build documents
+        start_evt.set()
+        recs = []
+        for _ in procs:
+            recs += out_q.get(timeout=max(5.0, deadline - time.time() + 30))
+        for p in procs:
+            p.join(timeout=10)
+        lo, hi = warm_s, warm_s + measure_s
+        done_in = [r for r in recs if lo <= r[1] < hi]
+        sent_in = [r for r in recs if lo <= r[0] < hi]
+        ok = sum(r[3] for r in done_in)
+        res.update(requests=len(recs), docs=len(done_in),
+                   docs_per_s=round(len(done_in) / measure_s, 3),
+                   valid=round(ok / max(1, len(done_in)), 3),
+                   http_latency_s=pcts([r[2] for r in sent_in]),
+                   failed=sum(not r[3] for r in recs),
+                   unfinished=int(round(rate * dur)) - len(recs))
+        res["status"] = "ok"
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        server.should_exit = True
+        th.join(timeout=15)
+        aeng.shutdown()
+        api.provide_generator(None)
+        if api.parser is not None:
+            api.parser.close()
+        api.parser = api.field_generator = None
+        engine.cfg.decode_hints = hints0
+        pkg_log.setLevel(level0)
+        if engine.has_work():
+            engine.abort_all("abort")
+    res["phase_s"] = round(time.perf_counter() - t_start, 1)
+    return res
+
+
 # --------------------------------------------------------------- model phases
 def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 0,
                 docs: int = 0, latency_runs: int = 0, formats: tuple | None = None,
@@ -214,7 +389,7 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
                                parse_procs=parse_procs)
             on_gpu = eng.device.type == "cuda"
             if stream.run_until(warm_docs, deadline):
-                stream.finished.clear()
+                stream.clear_window()
                 if on_gpu:
                     torch.cuda.synchronize()
                 t1 = time.perf_counter()
@@ -228,7 +403,7 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
                            loaded_latency_s=loaded_latency(stream.finished)["e2e_s"],
                            formats=list(formats) if formats else None,
                            per_doc={k: round(v, 2) for k, v in
-                                    validate(eng, stream.finished[:1024]).items()})
+                                    validate(eng, stream.finished).items()})
                 if not done:
                     res["status"] = "timeout"
             else:

@@ -90,23 +90,55 @@ def _produce_proc(base: int, flavor: str, path, out_q, stop_evt) -> None:
         i += 1
 
 
+def _postprocess_proc(flavor: str, path, in_q, out_q) -> None:
+    """Spawned post-processing process: the service's extraction epilogue for every
+    completed document of the stream -- detokenise, JSON recovery and pydantic
+    validation (``parse_and_validate_response``, rfq_agent.py:185-206) -- off the
+    engine process's GIL, as the HTTP layer does it off the engine thread.  Receives
+    (key, output token ids), returns (key, validated, fallback).  ``None`` ends it.
+    Imports no torch and never touches the GPU."""
+    from ..engine.tokenizer import get_tokenizer
+    from ..service.extract import parse_and_validate_response
+
+    tok = get_tokenizer(flavor, path)
+    while True:
+        item = in_q.get()
+        if item is None:
+            return
+        key, ids = item
+        try:
+            out = parse_and_validate_response(tok.decode(ids), "direct_text_input")
+            ok = bool(out.get("success"))
+            fb = ok and "validation warnings" in out.get("message", "")
+        except Exception:  # noqa: BLE001 - a failed document is reported, never fatal
+            ok, fb = False, False
+        out_q.put((key, ok, fb))
+
+
 class DocStream:
     """One replica's continuous document stream over an LLMEngine.
 
     A producer thread builds and tokenises prompts ahead of the engine (as the
     HTTP front-end does while the engine steps); the engine loop keeps
-    ``in_flight`` documents admitted and counts completions.  ``run_until(n)``
-    steps the engine until ``n`` documents have completed in total and returns,
-    leaving the in-flight documents in place for the next call.
+    ``in_flight`` documents admitted.  A document *completes* only when the
+    service's post-processing has run on it: every finished sequence goes to a
+    spawned post-processing process (detokenise -> JSON recovery -> pydantic
+    validation, rfq_agent.py:185-206) and is counted when its validated result comes
+    back.  ``run_until(n)`` steps the engine until ``n`` documents have completed in
+    total and returns, leaving the in-flight documents in place for the next call.
+    ``post="inline"`` validates in this process instead (tests, tools).
     """
 
     def __init__(self, engine, dp_rank: int, seed: int, in_flight: int,
                  formats: tuple | None = None, parse_procs: int = 4,
-                 producer: str | None = None, overlap_admit: bool | None = None):
+                 producer: str | None = None, overlap_admit: bool | None = None,
+                 post: str | None = None):
+        from ..engine.engine import short_gil_switch
         from ..service.extract import build_messages
         from ..service.prompt import register_prompt_prefix
         from ..utils import synth
 
+        self._prev_switch = short_gil_switch()   # producer / post threads share the GIL
         self.engine = engine
         self.tok = engine.tokenizer
         register_prompt_prefix(self.tok)         # what the service's EngineBackend does
@@ -115,8 +147,13 @@ class DocStream:
         self.ready: queue.Queue = queue.Queue(maxsize=max(64, in_flight))
         self.stop = threading.Event()
         self.live = 0
-        self.completed = 0
+        self.completed = 0                       # documents validated (post-processed)
+        self.retired = 0                         # sequences the engine finished
         self.finished = []                       # sequences completed in the current window
+        self.valid = 0                           # of ``finished``: validated, no fallback
+        self.fallback = 0                        # validated through the G12 fallback
+        self._pending: dict = {}                 # key -> finished Sequence awaiting post
+        self._key = 0
         self._build, self._synth = build_messages, synth
         self.formats = tuple(formats) if formats else None
         self._pool = None
@@ -150,6 +187,18 @@ class DocStream:
             self.thread = threading.Thread(target=self._produce, name="bench-tokenize",
                                            daemon=True)
             self.thread.start()
+        # post-processing: a spawned process (default) or inline
+        self.post_mode = post or os.environ.get("RFQ_BENCH_POST", "process")
+        self._post = None
+        if self.post_mode == "process":
+            import multiprocessing as mp
+
+            ctx = mp.get_context("spawn")
+            self._post_in, self._post_out = ctx.Queue(), ctx.Queue()
+            self._post = ctx.Process(target=_postprocess_proc, name="bench-postprocess",
+                                     args=(self.tok.flavor, getattr(self.tok, "path", None),
+                                           self._post_in, self._post_out), daemon=True)
+            self._post.start()
 
     def _docs(self):
         i = 0
@@ -198,9 +247,53 @@ class DocStream:
             eng.add_request(ids, params)
             self.live += 1
 
+    def _submit_post(self, done) -> None:
+        """Hand the engine's finished sequences to the post-processing stage."""
+        for s in done:
+            if self._post is None:
+                from ..service.extract import parse_and_validate_response
+
+                try:
+                    out = parse_and_validate_response(self.engine.decode_text(s),
+                                                      "direct_text_input")
+                    ok = bool(out.get("success"))
+                    fb = ok and "validation warnings" in out.get("message", "")
+                except Exception:  # noqa: BLE001
+                    ok, fb = False, False
+                self._complete(s, ok, fb)
+            else:
+                self._key += 1
+                self._pending[self._key] = s
+                self._post_in.put((self._key, s.output_ids))
+
+    def _complete(self, s, ok: bool, fb: bool) -> None:
+        s.t_valid = time.perf_counter()
+        s.valid = ok and not fb
+        self.completed += 1
+        self.valid += s.valid
+        self.fallback += fb
+        self.finished.append(s)
+
+    def _collect(self, block: bool = False) -> None:
+        """Count the documents whose post-processing has come back."""
+        if self._post is None:
+            return
+        while self._pending:
+            try:
+                key, ok, fb = (self._post_out.get(timeout=1.0) if block
+                               else self._post_out.get_nowait())
+            except queue.Empty:
+                if block and not self._post.is_alive():
+                    raise RuntimeError(f"bench post-processing process exited "
+                                       f"(code {self._post.exitcode})")
+                return
+            self._complete(self._pending.pop(key), ok, fb)
+            block = False
+
     def run_until(self, target: int, deadline: float | None = None):
-        """Step until ``target`` documents completed in total (or perf_counter passes
-        ``deadline``; then returns False)."""
+        """Step until ``target`` documents completed in total -- finished by the engine
+        AND post-processed (detokenised, JSON-recovered, validated) -- or perf_counter
+        passes ``deadline`` (then returns False)."""
         eng = self.engine
         runner = getattr(eng, "runner", None)
         hooked = [False]
@@ -208,6 +301,7 @@ class DocStream:
         def admit():                     # runs while the step executes on the device
             hooked[0] = True
             self._top_up(block=False)
+            self._collect()
 
         if runner is not None and self.overlap_admit:
             runner.busy_hook = admit
@@ -215,18 +309,23 @@ class DocStream:
             while self.completed < target:
                 if deadline is not None and time.perf_counter() > deadline:
                     return False
+                self._collect()
+                if self.completed >= target:
+                    break
                 # the documents retired by the previous step are replaced during this
                 # step's device time (admit) instead of between steps, where the GPU
                 # idles; only an empty engine (or a step that never launched) tops up here
                 if not hooked[0] or not eng.has_work():
                     self._top_up(block=True)
                 if not eng.has_work():
+                    # everything in flight has left the engine: wait for its validation
+                    self._collect(block=True)
                     continue
                 hooked[0] = False
                 done = eng.step()
                 self.live -= len(done)
-                self.completed += len(done)
-                self.finished.extend(done)
+                self.retired += len(done)
+                self._submit_post(done)
         finally:
             if runner is not None:
                 runner.busy_hook = None
@@ -252,27 +351,61 @@ class DocStream:
             self.thread.join(timeout=10)
         if self._pool is not None:
             self._pool.shutdown(wait=False, cancel_futures=True)
+        if self._post is not None:
+            self._post_in.put(None)
+            self._post.join(timeout=10)
+            if self._post.is_alive():
+                self._post.terminate()
+                self._post.join(timeout=5)
+            self._post_in.cancel_join_thread()
+            self._post_out.cancel_join_thread()
+            self._post = None
+        self._pending.clear()
         if self.engine.has_work():
             self.engine.abort_all("abort")
         self.live = 0
+        import sys
+
+        sys.setswitchinterval(self._prev_switch)
+
+    def clear_window(self) -> None:
+        """Start a new measurement window: forget the completed documents so far."""
+        self.finished.clear()
+        self.valid = 0
+        self.fallback = 0
+
+    def window_valid(self) -> float:
+        """Share of the window's documents that validated on the schema's first path
+        (no G12 fallback): the post-processing result of EVERY counted document."""
+        return self.valid / max(1, len(self.finished))
+
+
+def token_shape(seqs) -> dict:
+    """Per-document token shape of a window's completions."""
+    n = max(1, len(seqs))
+    return dict(
+        prompt_tokens=sum(s.prompt_len for s in seqs) / n,
+        completion_tokens=sum(s.num_generated for s in seqs) / n,
+        sampled_tokens=sum(s.num_sampled for s in seqs) / n,
+        prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n)
 
 
 def validate(engine, seqs) -> dict:
-    """Post-process a window's completions like the service does (rfq_agent.py:185-206)
-    and report the per-document token shape."""
+    """Per-document token shape plus the share that validated (no G12 fallback).
+    Sequences a DocStream already post-processed carry their result (``s.valid``);
+    any other sequence is post-processed here like the service does
+    (rfq_agent.py:185-206)."""
     from ..service.extract import parse_and_validate_response
 
     n = max(1, len(seqs))
     ok = 0
     for s in seqs:
-        out = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
-        ok += bool(out.get("success")) and "validation warnings" not in out.get("message", "")
-    return dict(
-        prompt_tokens=sum(s.prompt_len for s in seqs) / n,
-        completion_tokens=sum(s.num_generated for s in seqs) / n,
-        sampled_tokens=sum(s.num_sampled for s in seqs) / n,
-        prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n,
-        valid=ok / n)
+        v = getattr(s, "valid", None)
+        if v is None:
+            out = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
+            v = bool(out.get("success")) and "validation warnings" not in out.get("message", "")
+        ok += bool(v)
+    return dict(token_shape(seqs), valid=ok / n)
 
 
 def pcts(vals) -> dict | None:
@@ -289,12 +422,14 @@ def pcts(vals) -> dict | None:
 
 def loaded_latency(seqs) -> dict:
     """Latency under load of the documents that completed inside a timed window:
-    submission to the engine -> last token (``e2e``) and -> first sampled token
+    submission to the engine -> validated result (``e2e``: last token plus the
+    post-processing stage when the stream ran it) and -> first sampled token
     (``ttft``), the server-side time a closed-loop client with this many requests
     in flight waits per document (the reference's only metric is per-request
     server time, /root/reference/app/rfq_agent.py:158-168; its LLM call times out
     at 30 s, rfq_agent.py:69)."""
-    e2e = [s.t_finish - s.t_arrival for s in seqs if s.t_finish and s.t_arrival]
+    e2e = [getattr(s, "t_valid", 0.0) or s.t_finish for s in seqs]
+    e2e = [t - s.t_arrival for t, s in zip(e2e, seqs) if t and s.t_arrival]
     ttft = [s.t_first_token - s.t_arrival for s in seqs if s.t_first_token and s.t_arrival]
     return {"e2e_s": pcts(e2e), "ttft_s": pcts(ttft)}
 

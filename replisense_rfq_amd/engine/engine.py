@@ -55,16 +55,24 @@ def resolve_device(spec: str, tp: TPContext) -> torch.device:
     return torch.device(spec)
 
 
+def short_gil_switch() -> float:
+    """Shorten the GIL switch interval for a process whose engine loop shares the
+    interpreter with other threads (HTTP event loop, prompt tokenisers, the bench's
+    admission hook).  Every native call of a step (schedule_and_pack, the token
+    readback, post) releases the GIL, and taking it back waits up to one switch
+    interval while another thread runs Python: at the default 5 ms that was several ms
+    of idle GPU per step (bench: pack 5.2 ms of a 113 ms step with a tokenizer thread
+    busy); 0.5 ms bounds it.  Called only by the loops that have such threads
+    (AsyncEngine, DocStream, the DP router worker), never by a bare LLMEngine.
+    Returns the previous interval so a temporary user can restore it."""
+    prev = sys.getswitchinterval()
+    sys.setswitchinterval(float(os.environ.get("RFQ_GIL_SWITCH_MS", "0.5")) / 1e3)
+    return prev
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig | None = None, tp: TPContext = SINGLE,
                  model=None, capture: bool = True):
-        # The engine loop hands the GIL back and forth with the threads around it (HTTP
-        # event loop, prompt tokenisers): every native call of a step (schedule_and_pack,
-        # the token readback, post) releases it, and taking it back waits up to one
-        # switch interval while another thread runs Python.  At the default 5 ms that is
-        # several ms of idle GPU per step (bench: pack 5.2 ms of a 113 ms step with the
-        # tokenizer thread busy); 0.5 ms bounds it.
-        sys.setswitchinterval(float(os.environ.get("RFQ_GIL_SWITCH_MS", "0.5")) / 1e3)
         self.cfg = cfg or EngineConfig()
         self.tp = tp
         self.device = resolve_device(self.cfg.device, tp)
@@ -106,7 +114,8 @@ class LLMEngine:
             limit = MAX_GRAPH_TOKENS
             if self.model_cfg.is_moe:
                 # MoE: graphs only where the per-expert skinny kernels run; larger
-                # steps go eager so they can use one hipBLASLt GEMM per expert
+                # steps go eager (the grouped dense MFMA GEMM, models/moe.py, is
+                # host-sync-free, but its token-count-dependent grid is not captured)
                 from ..models.moe import SKINNY_MAX_TOKENS
 
                 limit = int(os.environ.get("RFQ_MOE_GRAPH_TOKENS", SKINNY_MAX_TOKENS))
@@ -336,7 +345,8 @@ class AsyncEngine:
     """
 
     def __init__(self, engine: LLMEngine):
-        self.engine = engine          # (LLMEngine set the short GIL switch interval)
+        self.engine = engine
+        short_gil_switch()            # the HTTP event loop shares this interpreter
         self._inbox: queue.Queue = queue.Queue()
         self._held: list = []                    # inbox messages deferred to the loop top
         self._stop = threading.Event()
@@ -373,21 +383,42 @@ class AsyncEngine:
         if not in_step:
             held, self._held = self._held, []
             for msg in held:
-                self._apply(msg)
+                self._apply_or_fail(msg)
         try:
             while True:
                 msg = self._inbox.get_nowait()
                 if in_step and msg[0] == "add":
                     try:
                         self._apply(msg)
-                    except Exception:  # noqa: BLE001 - replayed (and raised) at the loop top
+                    except Exception:  # noqa: BLE001 - replayed at the loop top
                         self._held.append(msg)
                 elif in_step:
                     self._held.append(msg)
                 else:
-                    self._apply(msg)
+                    self._apply_or_fail(msg)
         except queue.Empty:
             pass
+
+    def _apply_or_fail(self, msg):
+        """Apply one inbox message at the loop top.  A message that raises fails only
+        its own request (an add's caller gets a finished ``engine_error`` Sequence, the
+        G8 error-dict path); the engine thread keeps serving everyone else."""
+        try:
+            self._apply(msg)
+        except Exception:  # noqa: BLE001
+            log.exception("request could not be admitted")
+            if msg[0] == "add":
+                _, prompt, params, cb, req = msg
+                s = Sequence(list(prompt), params or self.engine.default_params(), callback=cb)
+                s.status = Status.FINISHED
+                s.finish_reason = "engine_error"
+                s.t_finish = time.perf_counter()
+                req.seq = s
+                if cb is not None:
+                    try:
+                        cb(s)
+                    except Exception:  # pragma: no cover - callbacks must not kill the loop
+                        log.exception("sequence callback failed")
 
     def _in_step(self):
         self._drain(in_step=True)
@@ -412,6 +443,8 @@ class AsyncEngine:
                 try:
                     eng.step()
                 except BaseException as e:  # engine failure: fail every in-flight request
+                    # (including requests the busy hook admitted during this step: they
+                    # are in the core already and are failed with it, like the rest)
                     log.exception("engine step failed")
                     self.error = e
                     eng.abort_all("engine_error")

@@ -46,6 +46,9 @@ def _join_group(devices: str, tp_rank: int, tp: int, port: int):
     process group.  Runs before anything touches HIP."""
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices
+    from ..utils.affinity import pin_to_gpu
+
+    pin_to_gpu(tp_rank)           # NUMA-local cores of this process's device
     if tp <= 1:
         from ..parallel.tp import SINGLE
 
@@ -77,6 +80,9 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
 
     cfg = EngineConfig(**cfg_dict)
     eng = LLMEngine(cfg, tp=ctx)
+    from .engine import short_gil_switch
+
+    short_gil_switch()                         # the inbox feeder thread shares the GIL
     exit_after = FaultInjector().replica_exit_after()
     outq.put(("ready", idx, None))
     pending = {}
@@ -122,7 +128,15 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
                     msg = held.pop(0)
                 else:
                     msg = inq.get_nowait() if eng.has_work() else inq.get(timeout=0.05)
-                if not apply(msg):
+                try:
+                    alive = apply(msg)
+                except Exception:  # noqa: BLE001 - fail only this request, keep serving
+                    log.exception("replica %d: request could not be admitted", idx)
+                    if msg is not None and msg[0] != "abort":
+                        outq.put(("done", msg[0], {"text": "", "finish": "engine_error",
+                                                   "span": {}}))
+                    continue
+                if not alive:
                     eng.shutdown()                 # release the TP followers
                     return
         except queue.Empty:

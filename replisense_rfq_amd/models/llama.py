@@ -19,7 +19,7 @@ Residual adds are fused into the following RMSNorm, the q rotation happens in
 place inside the QKV GEMM output, and attention writes straight into the O-GEMM
 input, so a layer is 5 GEMMs + 5 custom kernels with no extra copies.  Every op
 is stream-ordered and allocation-stable, so the decode path is captured into a
-hipGraph by the engine (engine/graphs.py).
+hipGraph by the engine (ModelRunner.capture_graphs, engine/runner.py).
 """
 from __future__ import annotations
 

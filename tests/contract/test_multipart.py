@@ -44,10 +44,11 @@ def test_chunking_does_not_change_the_result(eol):
     blob = bytes(rng.randrange(256) for _ in range(50_000)) + b"\r\n--XyZ12 not a delimiter"
     body = _body([("note", None, b"hello"), ("file", "réq.pdf", blob),
                   ("file", "b.txt", b"")], eol)
+    body2 = _body([("note", None, b"hello"), ("file", "réq.pdf", blob)], eol)
     whole = _dump(parse_form(body, CT))
     assert whole["note"] == ["hello"]
-    assert whole["file"][0] == ("réq.pdf", len(blob), blob)
-    assert whole["file"][1] == ("b.txt", 0, b"")
+    assert whole["file"] == [("b.txt", 0, b"")]         # the last part of a repeated name
+    assert _dump(parse_form(body2, CT))["file"] == [("réq.pdf", len(blob), blob)]
     for trial in range(20):
         mp = MultipartStream(CT)
         i = 0
@@ -90,8 +91,8 @@ def test_api_order_400_before_413(monkeypatch):
 
 def test_limits_text_part_field_and_file_counts():
     """non-file parts are capped at 1 MiB and the field / file
-    counts at 1,000 (Starlette's limits); a second file part under the same name is
-    counted but never stored."""
+    counts at 1,000 (Starlette's limits); a repeated file part replaces the earlier one
+    (whose spool is closed), as Starlette's form.get() returns the last value."""
     from replisense_rfq_amd.api.multipart import MultipartLimitError
 
     with pytest.raises(MultipartLimitError):
@@ -100,12 +101,33 @@ def test_limits_text_part_field_and_file_counts():
         parse_form(_body([(f"f{i}", None, b"v") for i in range(1001)]), CT)
     with pytest.raises(MultipartLimitError):
         parse_form(_body([("file", f"{i}.txt", b"v") for i in range(1001)]), CT)
-    form = parse_form(_body([("file", "a.txt", b"first"), ("file", "b.txt", b"x" * 4096)]), CT)
-    first, second = form["file"]
-    assert _dump({"f": [first]})["f"][0] == ("a.txt", 5, b"first")
-    assert second.size == 4096
-    second.file.seek(0, 2)
-    assert second.file.tell() == 0
+    mp = MultipartStream(CT)
+    mp.feed(_body([("file", "a.txt", b"first"), ("file", "b.txt", b"x" * 4096)]))
+    form = mp.close()
+    (last,) = form["file"]
+    assert _dump({"f": [last]})["f"][0] == ("b.txt", 4096, b"x" * 4096)
+
+
+def test_api_two_file_parts_uses_the_last(monkeypatch):
+    """a body with two 'file' parts is processed with the LAST one (FastAPI's
+    single UploadFile parameter); a text field named 'file' followed by the real upload
+    no longer 422s."""
+    from replisense_rfq_amd.api import main
+    from replisense_rfq_amd.service.extract import ExtractService, MockBackend
+    from replisense_rfq_amd.service.parser import FileParser
+
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_parser, lambda: FileParser())
+    monkeypatch.setitem(main.app.dependency_overrides, main.get_field_generator,
+                        lambda: ExtractService(MockBackend()))
+    client = TestClient(main.app)
+    body = _body([("file", "a.exe", b"nope"), ("file", "b.txt", b"Need 5 bolts")])
+    r = client.post("/upload/", content=body, headers={"content-type": CT})
+    assert r.status_code == 200, r.text
+    assert r.json()["data"]["parsing_info"]["original_filename"] == "b.txt"
+    body = _body([("file", None, b"just text"), ("file", "c.txt", b"Need 7 nuts")])
+    r = client.post("/upload/", content=body, headers={"content-type": CT})
+    assert r.status_code == 200, r.text
+    assert r.json()["data"]["parsing_info"]["original_filename"] == "c.txt"
 
 
 def test_api_oversized_text_field_is_400(monkeypatch):

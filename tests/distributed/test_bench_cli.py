@@ -187,11 +187,18 @@ def test_bench_extra_phases_cpu():
     phase, all in the same JSON line (tiny models of the same architectures here)."""
     out = _run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0",
                 "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
-                "--latency-runs", "1", "--phases", "http,mixtral,70b", "--http-docs", "6",
+                "--latency-runs", "1", "--phases", "http_open,http,mixtral,70b",
+                "--http-open-rate", "3", "--http-open-warm", "2", "--http-open-measure", "4",
+                "--http-docs", "6",
                 "--http-clients", "3", "--mixtral-model", "tiny-mixtral",
                 "--mixtral-in-flight", "4", "--mixtral-warm", "2", "--mixtral-docs", "4",
                 "--big-model", "tiny-llama70", "--big-latency-runs", "1"], timeout=800)
     ph = out["phases"]
+    o = ph["http_open_loop"]
+    assert o["status"] == "ok", o
+    assert o["offered_rate"] == 3 and o["requests"] > 0 and o["failed"] == 0, o
+    assert o["docs_per_s"] > 0 and o["valid"] == 1.0 and o["http_latency_s"]["p50"] > 0
+    assert o["http_vs_engine"] > 0
     h = ph["http_upload"]
     assert h["status"] == "ok" and h["docs"] == 6 and h["valid"] == 1.0, h
     assert h["docs_per_s"] > 0 and h["http_latency_s"]["n"] == 6
@@ -210,7 +217,7 @@ def test_bench_phases_auto_only_on_one_gpu_8b():
 
     class A:
         phases, tp, model = "auto", 1, "llama3-8b"
-    assert bench._phase_list(A, 1) == ["http", "mixtral", "70b"]
+    assert bench._phase_list(A, 1) == ["http_open", "http", "mixtral", "70b"]
     assert bench._phase_list(A, 8) == [] and bench._phase_list(A, 2) == []
     A.model = "tiny-llama"
     assert bench._phase_list(A, 1) == []
@@ -237,3 +244,26 @@ def test_http_phase_releases_the_engine():
     del eng
     gc.collect()
     assert wr() is None, [type(r).__name__ for r in gc.get_referrers(wr())]
+
+
+@pytest.mark.timeout(1200)
+def test_bench_default_gpus8_flow_gloo():
+    """the driver's 8-GPU flow -- `bench.py --gpus 8` self-launching
+    8 ranks, DP=8 replicas for the docs/s window, then ONE TP=8 group for the
+    latency phase -- on gloo with tiny models of the same architectures.  The JSON
+    line carries the DP docs/s, the tp_latency block with car_status, the
+    in-window post-processing counts and the affinity report."""
+    out = _run([sys.executable, "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "0",
+                "--model", "tiny-llama", "--tp-latency-model", "tiny-llama70",
+                "--tp-latency-runs", "1", "--tp-docs", "2", "--tp-in-flight", "2",
+                "--docs-per-step", "1", "--max-num-seqs", "2", "--latency-runs", "1"],
+               timeout=1150, threads=1)
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    assert out["value"] > 0 and out["config"]["global_batch"] == 8
+    assert out["postprocess"]["validated"] >= 1 and out["postprocess"]["failed"] == 0
+    assert out["config"]["counted"] == "validated in window"
+    tpl = out["tp_latency"]
+    assert tpl["status"] == "ok", tpl
+    assert tpl["parallelism"] == "tp8" and tpl["p50_parse_text_latency_s"] > 0
+    assert isinstance(tpl["car_status"], str) and tpl["car_status"]
+    assert "status" in out["engine"]["affinity"]

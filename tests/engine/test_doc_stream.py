@@ -62,3 +62,30 @@ def test_overlapped_admission_keeps_depth():
     assert seen[0][0] is True
     assert any(not b for b, _ in seen[1:])
     assert all(live <= 4 for _, live in seen)
+
+
+def test_every_counted_document_was_postprocessed():
+    """a document counts only once the service's post-processing
+    (detokenise -> JSON recovery -> pydantic validation, rfq_agent.py:185-206) has
+    returned for it, inside the window; the validated share covers EVERY counted
+    document, not a sample taken after the window."""
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cpu", max_num_seqs=4,
+                                 decode_hints=True))
+    s = DocStream(eng, 0, 5, 4, producer="thread", post="process")
+    try:
+        assert s.run_until(3)
+        s.clear_window()
+        c0 = s.completed
+        assert s.run_until(c0 + 6)
+        assert s._post is not None and s.post_mode == "process"
+        win = list(s.finished)
+        assert len(win) == s.completed - c0 >= 6
+        for q in win:
+            assert q.t_valid >= q.t_finish > 0 and isinstance(q.valid, bool)
+        # retired by the engine but still in post-processing are NOT counted
+        assert s.completed + len(s._pending) == s.retired
+        assert s.valid + s.fallback <= len(win)
+        assert s.window_valid() == 1.0
+    finally:
+        s.close()
+    assert s._post is None

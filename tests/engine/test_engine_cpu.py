@@ -307,3 +307,44 @@ def test_busy_hook_failure_raised_after_step_drains(engine):
     engine.abort_request(seq, "test")
     while engine.has_work():
         engine.step()
+
+
+def test_async_engine_survives_add_failing_in_step_and_at_loop_top(engine):
+    """an add that raises inside the step hook is held and replayed
+    at the loop top; when the replay raises too, only that request fails (its caller
+    gets an engine_error Sequence) and the engine thread keeps serving the others."""
+    aeng = AsyncEngine(engine)
+    orig = engine.add_request
+    bad = _prompts(engine, 1, base=110)[0]
+
+    def flaky_add(prompt, params=None, callback=None):
+        if list(prompt) == list(bad):
+            raise RuntimeError("injected add failure")
+        return orig(prompt, params, callback)
+
+    engine.add_request = flaky_add
+    try:
+        async def run():
+            good = _prompts(engine, 2, base=120)
+            t1 = asyncio.ensure_future(aeng.generate(good[0], engine.default_params(max_tokens=8)))
+            await asyncio.sleep(0.05)              # a step is (likely) running: in-step path
+            tb = asyncio.ensure_future(aeng.generate(bad, engine.default_params(max_tokens=8),
+                                                     timeout=30))
+            t2 = asyncio.ensure_future(aeng.generate(good[1], engine.default_params(max_tokens=8),
+                                                     timeout=30))
+            return await asyncio.gather(t1, tb, t2)
+
+        s1, sb, s2 = asyncio.run(run())
+        assert sb.finish_reason == "engine_error"
+        assert s1.finish_reason not in (None, "engine_error")
+        assert s2.finish_reason not in (None, "engine_error")
+        assert aeng.healthy and aeng._thread.is_alive()
+        # a direct loop-top replay of a failing add also fails only that request
+        from replisense_rfq_amd.engine.engine import _Request
+
+        got, req = [], _Request()
+        aeng._apply_or_fail(("add", bad, engine.default_params(max_tokens=8), got.append, req))
+        assert got and got[0].finish_reason == "engine_error" and req.seq is got[0]
+    finally:
+        engine.add_request = orig
+        aeng.shutdown()

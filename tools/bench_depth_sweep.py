@@ -57,7 +57,7 @@ def main():
             # ramp: drain down to the new depth (no admissions while above it), then
             # one full turnover of documents at that depth
             stream.run_until(stream.completed + max(0, stream.live - d) + d)
-            stream.finished.clear()
+            stream.clear_window()
             steps0 = eng.num_steps
             if eng.device.type == "cuda":
                 torch.cuda.synchronize()
