@@ -89,8 +89,11 @@ def parse():
     ap.add_argument("--http-open-rate", type=float, default=0.0,
                     help="open-loop HTTP phase: offered requests/s (0 = 90 %% of the "
                          "timed window's docs/s per replica)")
-    ap.add_argument("--http-open-warm", type=float, default=20.0)
+    ap.add_argument("--http-open-warm", type=float, default=30.0)
     ap.add_argument("--http-open-measure", type=float, default=40.0)
+    ap.add_argument("--http-open-burst", type=float, default=0.75,
+                    help="open-loop HTTP phase: initial burst as a fraction of the "
+                         "in-flight depth (starts the queue near its steady state)")
     ap.add_argument("--http-docs", type=int, default=512)
     ap.add_argument("--http-clients", type=int, default=64)
     ap.add_argument("--mixtral-model", default="mixtral-8x7b")
@@ -491,7 +494,7 @@ def main():
                 engine, rate=rate, warm_s=args.http_open_warm,
                 measure_s=args.http_open_measure,
                 budget_s=min(args.http_open_warm + args.http_open_measure + 60.0, left()),
-                seed=args.seed)
+                seed=args.seed, burst_depth=int(args.http_open_burst * args.max_num_seqs))
             r["engine_docs_per_s"] = round(out["value"] / max(1, dp_world), 3)
             if r.get("docs_per_s"):
                 r["http_vs_engine"] = round(r["docs_per_s"] / r["engine_docs_per_s"], 3)

@@ -37,6 +37,14 @@ void launch_gemv_splitk_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, 
 void launch_gemv_splitk_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, float*, unsigned*, const int32_t*, const float*, const int32_t*,
                              bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
+                     float*, unsigned*, const int32_t*, const float*, const int32_t*, bf16_t*,
+                     bf16_t*, int, int, int, const int32_t*, int, const int32_t*,
+                     const int32_t*, const int32_t*, const int32_t*, const int32_t*, int, int,
+                     int, bf16_t*, int64_t, float*, float*, float, int, unsigned*, unsigned*,
+                     unsigned*, hipStream_t);
+void launch_attn_decode_reduce(const float*, const float*, bf16_t*, int64_t, int, int, int,
+                               hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
@@ -82,6 +90,9 @@ void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
 uint32_t car_read_error(const void*);
 uint32_t car_read_info(const void*);
 int car_norm_max_rows();
+bool car_push_fits(int, int, int, int64_t);
+void launch_car_push_add_norm(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
+                              const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
 void launch_car_oneshot_add_norm(char* const*, int, int, const bf16_t*, bf16_t*, int64_t,
                                  const bf16_t*, bf16_t*, int64_t, int, int, float, hipStream_t);
 void launch_moe_skinny(const bf16_t*, int64_t, const int32_t*, int, const int32_t*, const bf16_t*,
@@ -262,6 +273,92 @@ void gemv_splitk_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const
                                (int)Hq, (int)Hkv, k_cache.size(2), cur_stream());
 }
 
+// Fused QKV projection + RoPE + KV append + split-K decode attention in ONE launch
+// (decode_fused.hip): qkv = x . w^T (q columns written), this step's K / V appended to
+// the paged cache, and the decode attention over [work_seq, work_ct] rows leaves its
+// split partials in part_o / part_ml (num_splits > 1; merge with attn_decode_merge) or
+// writes `out` directly (num_splits == 1).  done: this layer's zeroed counter slot
+// (Hkv uint32); zero_slot: the previous layer's slot (zeroed by the launch); err: a
+// uint32 the kernel increments on a wait timeout.  cfg: split-K GEMV cfg (8 waves).
+void qkv_attn(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
+              const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
+              const Tensor& v_cache, int64_t Hq, int64_t Hkv, const Tensor& part,
+              const Tensor& tile_cnt, int64_t cfg, const Tensor& block_tables,
+              const Tensor& seq_q_start, const Tensor& seq_q_len, const Tensor& seq_kv_len,
+              const Tensor& work_seq, const Tensor& work_ct, int64_t list_tpi, int64_t run_tiles,
+              const Tensor& out, const Tensor& part_o, const Tensor& part_ml, double scale,
+              int64_t num_splits, const Tensor& done, const std::optional<Tensor>& zero_slot,
+              const Tensor& err) {
+  const int64_t N = w.size(0);
+  check_splitk("qkv_attn", x, w, qkv, part, tile_cnt, cfg, N, N / 32);
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "qkv_attn: w must be [(Hq + 2 Hkv) * 128, K]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == 128, "qkv_attn: cos_sin must be fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(2) == 32 &&
+                  k_cache.size(3) == 128 && k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  v_cache.sizes() == k_cache.sizes(),
+              "qkv_attn: cache must be [blocks, Hkv, 32, 128]");
+  TORCH_CHECK(positions.numel() >= x.size(0) && slot_mapping.numel() >= x.size(0),
+              "qkv_attn: metadata");
+  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "qkv_attn: GQA group must be <= 16");
+  CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
+  CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
+  CHECK_I32(work_seq); CHECK_I32(work_ct);
+  CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  const int rows = out.size(0);
+  TORCH_CHECK(rows <= x.size(0), "qkv_attn: attention rows must be rows of x");
+  TORCH_CHECK(work_seq.numel() == work_ct.numel(), "qkv_attn: work list mismatch");
+  TORCH_CHECK(block_tables.size(0) >= seq_q_len.numel() && seq_kv_len.numel() >= seq_q_len.numel()
+                  && seq_q_start.numel() >= seq_q_len.numel(),
+              "qkv_attn: per-sequence arrays mismatch");
+  TORCH_CHECK(list_tpi == 1 || list_tpi == 2, "qkv_attn: list_tpi in {1, 2}");
+  TORCH_CHECK(run_tiles >= 1 && run_tiles <= list_tpi, "qkv_attn: run_tiles in [1, list_tpi]");
+  TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "qkv_attn: num_splits in [1, 32]");
+  if (num_splits > 1) {
+    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat &&
+                    part_o.numel() >= (int64_t)rows * Hq * num_splits * 128 &&
+                    part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
+                "qkv_attn: fp32 partial buffers too small");
+  }
+  CHECK_DEV(done); CHECK_I32(done); CHECK_DEV(err); CHECK_I32(err);
+  TORCH_CHECK(done.numel() >= 32 * Hkv, "qkv_attn: done slot holds Hkv counters, 32 words apart");
+  unsigned* zs = nullptr;
+  if (zero_slot.has_value()) {
+    CHECK_DEV(*zero_slot); CHECK_I32(*zero_slot);
+    TORCH_CHECK(zero_slot->numel() >= 32 * Hkv, "qkv_attn: zero_slot holds Hkv counters");
+    TORCH_CHECK(zero_slot->data_ptr() != done.data_ptr(), "qkv_attn: zero_slot is the done slot");
+    zs = reinterpret_cast<unsigned*>(zero_slot->data_ptr());
+  }
+  rfq::launch_qkv_attn(
+      bp(x), x.stride(0), bp(w), (int)N, x.size(1), bpm(qkv), qkv.stride(0), x.size(0), (int)cfg,
+      part.data_ptr<float>(), reinterpret_cast<unsigned*>(tile_cnt.data_ptr()),
+      positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int32_t>(),
+      bpm(k_cache), bpm(v_cache), (int)Hq, (int)Hkv, 32, block_tables.data_ptr<int32_t>(),
+      block_tables.stride(0), seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
+      seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(), work_ct.data_ptr<int32_t>(),
+      work_seq.numel(), (int)list_tpi, (int)run_tiles, bpm(out), out.stride(0),
+      num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
+      num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, (float)scale, (int)num_splits,
+      reinterpret_cast<unsigned*>(done.data_ptr()), zs,
+      reinterpret_cast<unsigned*>(err.data_ptr()), cur_stream());
+}
+
+// Merge split-K decode-attention partials into bf16 rows (attn_decode_reduce).
+void attn_decode_merge(const Tensor& part_o, const Tensor& part_ml, const Tensor& out, int64_t Hq,
+                       int64_t num_splits) {
+  CHECK_DEV(out); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  const int rows = out.size(0);
+  TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "attn_decode_merge: num_splits in [1, 32]");
+  TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat &&
+                  part_o.numel() >= (int64_t)rows * Hq * num_splits * 128 &&
+                  part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
+              "attn_decode_merge: fp32 partial buffers too small");
+  TORCH_CHECK(out.size(1) >= Hq * 128, "attn_decode_merge: out [rows, >= Hq * 128]");
+  rfq::launch_attn_decode_reduce(part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bpm(out),
+                                 out.stride(0), rows, (int)Hq, (int)num_splits, cur_stream());
+}
+
 // y = x . w^T, split-K over (N/16) x KS workgroups with the in-launch per-tile
 // reduction (M <= 16).  tile_cnt: int32 [>= N/16], zero, left at zero.
 void gemv_splitk(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& part,
@@ -400,8 +497,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   && seq_q_start.numel() >= seq_q_len.numel(),
               "attn_decode: per-sequence arrays mismatch");
   TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "attn_decode: num_splits in [1, 32]");
-  TORCH_CHECK(waves == 1 || (waves == 4 && num_splits % 4 == 0),
-              "attn_decode: waves 1, or 4 with num_splits % 4 == 0");
+  TORCH_CHECK(waves == 1 || ((waves == 4 || waves == 8) && num_splits % waves == 0),
+              "attn_decode: waves 1, or 4 / 8 with num_splits % waves == 0");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
@@ -691,10 +788,12 @@ void car_allreduce(const Tensor& inp, const Tensor& out, c10::IntArrayRef bases,
 }
 
 // residual <- bf16(allreduce(inp) + residual); out <- rmsnorm(residual) * w, one launch
-// (custom_ar.hip car_oneshot_add_norm_kernel).  inp: contiguous [rows, d] bf16.
+// (custom_ar.hip).  inp: contiguous [rows, d] bf16.  algo: 0 = push form when the
+// double-buffered per-rank slots fit (rows <= 16), else staged; 1 = staged one-shot
+// (car_oneshot_add_norm_kernel); 2 = push (car_push_add_norm_kernel).
 void car_allreduce_add_norm(const Tensor& inp, const Tensor& residual, const Tensor& w,
                             double eps, const Tensor& out, c10::IntArrayRef bases, int64_t rank,
-                            int64_t capacity_bytes) {
+                            int64_t capacity_bytes, int64_t algo) {
   CHECK_DEV(inp); CHECK_BF16(inp); CHECK_BF16(residual); CHECK_BF16(w); CHECK_BF16(out);
   TORCH_CHECK(inp.dim() == 2 && inp.is_contiguous(), "car_allreduce_add_norm: inp [rows, d]");
   const int64_t rows = inp.size(0), d = inp.size(1);
@@ -714,9 +813,16 @@ void car_allreduce_add_norm(const Tensor& inp, const Tensor& residual, const Ten
   TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "car_allreduce_add_norm: world");
   char* b[8];
   for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
-  rfq::launch_car_oneshot_add_norm(b, (int)rank, world, bp(inp), bpm(residual), residual.stride(0),
-                                   bp(w), bpm(out), out.stride(0), (int)rows, (int)d, (float)eps,
-                                   cur_stream());
+  const bool push_ok = rfq::car_push_fits(world, (int)rows, (int)d, capacity_bytes);
+  TORCH_CHECK(algo != 2 || push_ok, "car_allreduce_add_norm: push slots exceed the buffer");
+  if (algo == 2 || (algo == 0 && push_ok && rows <= 16))
+    rfq::launch_car_push_add_norm(b, (int)rank, world, bp(inp), bpm(residual), residual.stride(0),
+                                  bp(w), bpm(out), out.stride(0), (int)rows, (int)d, (float)eps,
+                                  cur_stream());
+  else
+    rfq::launch_car_oneshot_add_norm(b, (int)rank, world, bp(inp), bpm(residual),
+                                     residual.stride(0), bp(w), bpm(out), out.stride(0), (int)rows,
+                                     (int)d, (float)eps, cur_stream());
 }
 
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
@@ -858,12 +964,20 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("gemv_splitk_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
         "Tensor(d!) part, Tensor(e!) tile_cnt, int cfg) -> ()");
+  m.def("qkv_attn(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
+        "Tensor(d!) part, Tensor(e!) tile_cnt, int cfg, Tensor block_tables, Tensor seq_q_start, "
+        "Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, int list_tpi, "
+        "int run_tiles, Tensor(f!) out, Tensor(g!) part_o, Tensor(h!) part_ml, float scale, "
+        "int num_splits, Tensor(i!) done, Tensor(j!)? zero_slot, Tensor(k!) err) -> ()");
+  m.def("attn_decode_merge(Tensor part_o, Tensor part_ml, Tensor(a!) out, int Hq, "
+        "int num_splits) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
   m.def("car_allreduce_add_norm(Tensor inp, Tensor(a!) residual, Tensor w, float eps, "
-        "Tensor(b!) out, int[] bases, int rank, int capacity_bytes) -> ()");
+        "Tensor(b!) out, int[] bases, int rank, int capacity_bytes, int algo=0) -> ()");
   // host-side setup of the custom all-reduce regions (no tensor dispatch)
   m.def("car_alloc(int data_bytes) -> int", &car_alloc_op);
   m.def("car_free(int ptr) -> ()", &car_free_op);
@@ -928,6 +1042,8 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("gemv_splitk_norm", &gemv_splitk_norm);
   m.impl("gemv_splitk_swiglu", &gemv_splitk_swiglu);
   m.impl("gemv_splitk_rope", &gemv_splitk_rope);
+  m.impl("qkv_attn", &qkv_attn);
+  m.impl("attn_decode_merge", &attn_decode_merge);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);

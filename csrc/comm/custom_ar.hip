@@ -37,6 +37,7 @@ struct CarSignal {
   uint32_t start[kCarMaxBlocks][kCarMaxRanks];
   uint32_t mid[kCarMaxBlocks][kCarMaxRanks];     // two-shot: reduced slices published
   uint32_t end[kCarMaxBlocks][kCarMaxRanks];
+  uint32_t push[2][kCarMaxBlocks][kCarMaxRanks]; // push one-shot: row published, by parity
   uint32_t counter[kCarMaxBlocks];
   uint32_t error;
   uint32_t info;             // first timeout: 0x80000000 | phase << 24 | block << 8 | peer
@@ -59,10 +60,15 @@ __device__ __forceinline__ void car_store(uint32_t* p, uint32_t v) {
 // device) is waited for the same 2 s however slow each poll is.  A timeout records
 // the first failing (phase, block, peer) in `info` for the host's diagnostics.
 constexpr uint64_t kCarSpinTicks = 200000000ull;           // 2 s at 100 MHz
-enum : uint32_t { kCarStart = 1, kCarMid = 2, kCarEnd = 3 };
+enum : uint32_t { kCarStart = 1, kCarMid = 2, kCarEnd = 3, kCarPush = 4 };
 
+// A region whose error counter is set (a peer went silent before) fails every wait at
+// once: after the first timeout a lost peer costs no further 2 s spins -- the runner
+// sees the error behind that step and the replica restarts on RCCL (router.py).
 __device__ __forceinline__ bool car_wait(CarSignal* self, uint32_t* p, uint32_t v,
                                          uint32_t phase, int b, int peer) {
+  if (__hip_atomic_load(&self->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+    return false;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == v) return true;
@@ -318,6 +324,128 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
   }
 }
 
+constexpr int kCarPushRows = 16;      // decode rows of the push form
+constexpr int kCarPushD = 8192;       // max row width of the push form (bf16)
+
+// Push one-shot all-reduce + residual-add RMSNorm for decode rows (the latency path's
+// 160 all-reduces per Llama-3-70B step at TP=8).  One xGMI hop instead of the staged
+// form's three (flag out, remote read, end flag):
+//   1. every rank WRITES its row b into slot [parity][rank][b] of every peer's staging
+//      (remote stores over its links, all peers at once), drains them (system-scope
+//      release), then stores the call counter c into flag push[parity][b][rank] of
+//      every peer;
+//   2. it waits on its OWN flags push[parity][b][*] == c (local polls);
+//   3. it sums the world rows that landed in its own staging (local reads), adds the
+//      residual and normalises, exactly like car_oneshot_add_norm.
+// No end barrier: parity = c & 1 alternates the staging and flag sets, and a rank can
+// only reach call c + 2 of row b after every peer published call c + 1 of row b, i.e.
+// after every peer's kernel of call c -- the last reader of the parity-c slots -- has
+// completed on its stream.  Same rounding points and block_sum order as the staged
+// kernel, so the result is bit-identical to it (and to all_reduce + fused_add_rms_norm).
+template <int NCH>
+__global__ __launch_bounds__(256) void car_push_add_norm_kernel(
+    CarPeers peers, int rank, int world, const bf16_t* in, bf16_t* __restrict__ residual,
+    int64_t res_stride, const bf16_t* __restrict__ w, bf16_t* out, int64_t out_stride, int d,
+    int rows, float eps) {
+  CarSignal* self = reinterpret_cast<CarSignal*>(peers.base[rank]);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int nchunk = d >> 3;
+  __shared__ uint32_t cnt_s;
+  __shared__ int fail_s;
+  __shared__ float scratch[16];
+  if (tid == 0) {
+    cnt_s = self->counter[b] + 1;
+    fail_s = 0;
+  }
+  __syncthreads();
+  const uint32_t c = cnt_s;
+  const int par = (int)(c & 1u);
+  // slot (par, src, row b) of a region: a fixed home per (parity, source rank, row)
+  // whatever the call's shape, so a call of another shape on a faster rank can never
+  // write into slots a slower rank is still reading (parity alternates per row b)
+  auto slot = [&](int p, int src) {
+    return reinterpret_cast<s16x8*>(peers.base[p] + kCarDataOffset) +
+           (((int64_t)par * kCarMaxRanks + src) * kCarPushRows + b) * (kCarPushD / 8);
+  };
+  const s16x8* src = reinterpret_cast<const s16x8*>(in) + (int64_t)b * nchunk;
+  s16x8* rr = reinterpret_cast<s16x8*>(residual + b * res_stride);
+  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
+  s16x8 xv[NCH], rv[NCH], wv[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = tid + k * 256;
+    if (ch < nchunk) {
+      xv[k] = src[ch];
+      rv[k] = rr[ch];
+      wv[k] = wr[ch];
+    }
+  }
+  // 1. push the row into every rank's slot [par][rank][b] (own region included)
+  for (int p = 0; p < world; ++p) {
+    s16x8* dst = slot(p, rank);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int ch = tid + k * 256;
+      if (ch < nchunk) dst[ch] = xv[k];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: pushed rows landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid < world) {
+    CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
+    car_store(&peer->push[par][b][rank], c);
+    // 2. wait for row b of peer `tid` in the own staging
+    if (!car_wait(self, &self->push[par][b][tid], c, kCarPush, b, tid)) fail_s = 1;
+  }
+  __syncthreads();
+  // 3. sum row b over the ranks (rank order, fp32, rounded to bf16 = the all-reduce
+  //    output), add the residual, round, normalise
+  float v[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = tid + k * 256;
+    if (ch < nchunk) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < world; ++p) {
+        const s16x8 pv = slot(rank, p)[ch];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f_s(pv[j]);
+      }
+      float a[8], r[8];
+      unpack8(pack8(acc), a);
+      unpack8(rv[k], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += r[j];
+      const s16x8 packed = pack8(a);
+      rr[ch] = packed;
+      unpack8(packed, v[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float rs = rsqrtf(ss / (float)d + eps);
+  s16x8* orow = reinterpret_cast<s16x8*>(out + b * out_stride);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int ch = tid + k * 256;
+    if (ch < nchunk) {
+      float wf[8], o[8];
+      unpack8(wv[k], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * rs * wf[j];
+      orow[ch] = pack8(o);
+    }
+  }
+  if (tid == 0) {
+    self->counter[b] = c;
+    if (fail_s) atomicAdd(&self->error, 1u);
+  }
+}
+
 // ------------------------------------------------------------------ host side
 int64_t car_signal_bytes() { return kCarDataOffset; }
 
@@ -338,6 +466,30 @@ void launch_car_oneshot_add_norm(char* const* bases, int rank, int world, const 
   else if (nch <= 4) CAR_NORM_LAUNCH(4);
   else CAR_NORM_LAUNCH(8);
 #undef CAR_NORM_LAUNCH
+}
+
+// the push form's fixed slot layout [2][kCarMaxRanks][kCarPushRows][kCarPushD] bf16 (4 MiB)
+// fits the staging capacity and the call's rows / width fit a slot
+bool car_push_fits(int world, int rows, int d, int64_t capacity) {
+  return world <= kCarMaxRanks && rows >= 1 && rows <= kCarPushRows && d <= kCarPushD &&
+         2ll * kCarMaxRanks * kCarPushRows * kCarPushD * 2 <= capacity;
+}
+
+void launch_car_push_add_norm(char* const* bases, int rank, int world, const bf16_t* in,
+                              bf16_t* residual, int64_t res_stride, const bf16_t* w,
+                              bf16_t* out, int64_t out_stride, int rows, int d, float eps,
+                              hipStream_t s) {
+  CarPeers peers{};
+  for (int p = 0; p < world; ++p) peers.base[p] = bases[p];
+  const int nch = (d / 8 + 255) / 256;
+#define CAR_PUSH_LAUNCH(N)                                                                   \
+  car_push_add_norm_kernel<N><<<rows, 256, 0, s>>>(peers, rank, world, in, residual,          \
+                                                   res_stride, w, out, out_stride, d, rows, eps)
+  if (nch <= 1) CAR_PUSH_LAUNCH(1);
+  else if (nch <= 2) CAR_PUSH_LAUNCH(2);
+  else if (nch <= 4) CAR_PUSH_LAUNCH(4);
+  else CAR_PUSH_LAUNCH(8);
+#undef CAR_PUSH_LAUNCH
 }
 
 hipError_t car_alloc(int64_t data_bytes, void** ptr) {

@@ -37,27 +37,9 @@
 //   * MODE 1 (suffix): the normal per-sequence kernel over keys [P*32, kv_len) that
 //     merges the prefix partial into its registers before the bf16 store.
 // Everything is derived on device, so captured decode graphs stay valid.
-#include "common.h"
+#include "attn_decode_core.h"
 
 namespace rfq {
-
-constexpr int kD = 128;
-constexpr int kPage = 32;  // tokens per KV block; one key tile == one page
-constexpr int kMinPrefixPages = 4;
-
-typedef __attribute__((address_space(1))) unsigned long long gu64;   // global, sc1 access
-typedef __attribute__((address_space(1))) unsigned gu32;
-__device__ __forceinline__ unsigned long long pack_f2(float lo, float hi) {
-  return (unsigned long long)__float_as_uint(lo) | ((unsigned long long)__float_as_uint(hi) << 32);
-}
-
-struct PrefixArgs {
-  const int32_t* meta;     // [0] shared prefix length in tokens (P * kPage), [1] row count
-  const int32_t* pflag;    // per sequence: 1 = keys [0, P*32) come from the prefix pass
-  const int32_t* rowlist;  // q rows of the participating sequences (meta[1] of them)
-  float* pre_o;            // [rows][Hq][128] unnormalised prefix output
-  float* pre_ml;           // [rows][Hq][2] running max (log2 domain), softmax sum
-};
 
 // Single workgroup: P = min over participating sequences of the shared leading page run.
 __global__ __launch_bounds__(1024) void attn_prefix_meta_kernel(
@@ -97,39 +79,6 @@ __global__ __launch_bounds__(1024) void attn_prefix_meta_kernel(
   if (tid == 0) { meta[0] = P * kPage; meta[1] = s_cnt; }
 }
 
-// LDS hand-off inside one wave's V tile buffer.  One wave per workgroup: the block
-// barrier (as before).  Several waves with independent split loops (different page
-// counts): a barrier would mismatch, and the tile buffer is the wave's own, so draining
-// this wave's LDS operations (in-order per wave) and fencing the compiler suffices.
-template <int NWV>
-__device__ __forceinline__ void wave_lds_sync() {
-  if constexpr (NWV == 1) {
-    __syncthreads();
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over.
-// NWV > 1 (small decode batches): a workgroup of NWV waves, one KV split per wave,
-// merged through LDS before the workgroup's single partial (or, with one workgroup per
-// item, the bf16 output) leaves the CU.  16 splits of one (work item, kv head) then
-// cost 4 workgroups + a 4-way in-kernel merge instead of 16 waves whose partials a
-// second launch (attn_decode_reduce) or a 16-way single-wave merge combines: the
-// decode step of a batch-1 request runs one attention launch per layer.
-// NTK: K / V pages past the first kNtFromPage of a sequence are loaded non-temporal.
-// Those pages belong to one sequence and are read once per step per layer; the leading
-// pages hold the prompt prefix every request shares (prefix cache), which the other
-// sequences' waves re-read from L2 / MALL and keep the default policy.
-constexpr int kNtFromPage = 16;
-
-template <bool NTL>
-__device__ __forceinline__ s16x8 ld16(const bf16_t* p) {
-  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const s16x8*>(p));
-  else return *reinterpret_cast<const s16x8*>(p);
-}
-
 template <int NT, int MODE = 0, int NWV = 1, bool NTK = false>
 __global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
@@ -140,426 +89,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
     int num_splits, PrefixArgs px = PrefixArgs{}, int32_t* __restrict__ tickets = nullptr) {
   __shared__ __attribute__((aligned(16))) bf16_t v_lds_all[NWV * kPage * kD];
-  const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;   // wave = inner split
-  bf16_t* v_lds = v_lds_all + wv * kPage * kD;
-  // split: the workgroup's (outer) split, which the partial / merge epilogue indexes;
-  // gsplit / nsplit: this wave's KV range among all NWV * num_splits
-  const int split = blockIdx.x, kvh = blockIdx.y, w = blockIdx.z;
-  const int gsplit = split * NWV + wv, nsplit = num_splits * NWV;
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4;   // 16-lane group
-  const int c = lane & 15;   // MFMA column
-  const int G = Hq / Hkv;
-  bool act[NT], cvalid[NT];
-  int h[NT], qrow[NT], lim[NT];
-  int seq, ql, kvl, base = 0;
-  if constexpr (MODE == 2) {
-    // columns are (row, head) pairs of the participating rows, 16 * NT per work item
-    const int P = px.meta[0], nrow = px.meta[1];
-    if (P == 0 || w * 16 * NT >= nrow * G) return;
-    seq = 0; ql = 1; kvl = P;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = (w * NT + t) * 16 + c;
-      act[t] = (w * NT + t) * 16 < nrow * G;           // wave-uniform
-      cvalid[t] = col < nrow * G;
-      qrow[t] = px.rowlist[cvalid[t] ? col / G : 0];
-      h[t] = kvh * G + (cvalid[t] ? col % G : 0);
-      lim[t] = P;                                      // the whole prefix is visible
-    }
-  } else {
-    seq = work_seq[w];
-    if (seq < 0) return;       // padding work item (graph-captured buckets)
-    ql = seq_q_len[seq];
-    kvl = seq_kv_len[seq];
-    if constexpr (MODE == 1) base = px.pflag[seq] ? px.meta[0] : 0;
-    // NT column tiles per work item share every K fragment and V tile they load
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int tile = work_ct[w] * NT + t;
-      act[t] = tile * 16 < ql * G;                       // wave-uniform
-      const int col = tile * 16 + c;
-      cvalid[t] = col < ql * G;
-      const int qi = cvalid[t] ? col / G : 0;
-      h[t] = kvh * G + (cvalid[t] ? col % G : 0);
-      qrow[t] = seq_q_start[seq] + qi;
-      lim[t] = kvl - ql + qi + 1;                        // keys [0, lim) visible
-    }
-  }
-
-  int tps = (kvl - base + nsplit - 1) / nsplit;
-  tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = base + gsplit * tps;
-  const int end = min(kvl, start + tps);
-
-  float m_run[NT], l_run[NT];
-  f32x4 o[NT][8];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    m_run[t] = -INFINITY;
-    l_run[t] = 0.f;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) o[t][m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-
-  if (start < end && ql > 0) {
-    // Q^T fragments: B[k = dh][col]; lane holds Q[qrow, h][32ks + 8g .. +7]
-    s16x8 qf[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const bf16_t* qp = q + (int64_t)qrow[t] * q_stride + (int64_t)h[t] * kD;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        qf[t][ks] = reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
-        if (!cvalid[t]) qf[t][ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
-      }
-    }
-    const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
-    const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
-    const int np = pg_last - pg0 + 1;
-    // block-table entries by wave-uniform (scalar, lgkmcnt-counted) loads, one page
-    // ahead: a vector load here would make every page's K / V issue wait on vmcnt(0),
-    // i.e. drain the page loads already in flight
-    int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
-    // issue page j's K fragments (A operand: row = key, k = dh) and V rows (g + 4i,
-    // chunk c) into registers; must be called with j = 0, 1, 2, ...
-    auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
-      const int64_t page = pg_next;
-      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
-      const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
-      const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
-      if (NTK && pg0 + j >= kNtFromPage) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            kf[mt][ks] = ld16<true>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) vr[i] = ld16<true>(vb + (g + 4 * i) * kD + 8 * c);
-      } else {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            kf[mt][ks] = ld16<false>(kb + (16 * mt + c) * kD + 32 * ks + 8 * g);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) vr[i] = ld16<false>(vb + (g + 4 * i) * kD + 8 * c);
-      }
-    };
-    auto process = [&](int j, const s16x8 (&kf)[2][4], const s16x8 (&vr)[8]) {
-      const int kt = start + j * kPage;
-      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
-      // ---- V tile -> LDS (swizzled), rows past the split/context zeroed ----
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = g + 4 * i, ch = c;
-        const s16x8 v = row >= nvalid ? (s16x8){0, 0, 0, 0, 0, 0, 0, 0} : vr[i];
-        const int pch = ch ^ ((row & 7) << 1);
-        reinterpret_cast<s16x8*>(v_lds + row * kD)[pch] = v;
-      }
-
-      s16x8 pb[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (!act[t]) continue;
-        // ---- S^T = K Q^T ----
-        f32x4 s[2];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          s[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf[mt][ks]),
-                                                            as_bf16x8(qf[t][ks]), s[mt], 0, 0, 0);
-        }
-        // lane holds S^T[key = 16mt + 4g + i][column c]
-        float mx = -INFINITY;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = 16 * mt + 4 * g + i;
-            float v = s[mt][i] * scale_log2;
-            if (key >= nvalid || kt + key >= lim[t]) v = -INFINITY;
-            s[mt][i] = v;
-            mx = fmaxf(mx, v);
-          }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m_run[t], mx);
-        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;  // fully-masked column so far
-        const float alpha = fast_exp2(m_run[t] - m_use);
-        float psum = 0.f;
-        float p[8];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          p[jj] = fast_exp2(s[jj >> 2][jj & 3] - m_use);
-          psum += p[jj];
-        }
-        l_run[t] = l_run[t] * alpha + psum;
-        m_run[t] = m_new;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) o[t][m] *= alpha;
-        // P^T as B operand: element j <-> key pi(g,j) = (j<4 ? 4g+j : 16+4g+j-4)
-        pb[t] = pack8(p);
-      }
-
-      wave_lds_sync<NWV>();  // V tile visible (one wave per tile buffer)
-
-      // ---- O^T += V^T P^T (one transposed V read feeds every tile) ----
-      const int q4 = c >> 2, p4 = c & 3;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int r0 = 4 * g + q4, r1 = 16 + 4 * g + q4;
-        const int ch = 2 * m + (p4 >> 1), sub = (p4 & 1) * 4;
-        const s16x4 a0 = ds_read_tr16(v_lds + r0 * kD + ((ch ^ ((r0 & 7) << 1)) * 8) + sub);
-        const s16x4 a1 = ds_read_tr16(v_lds + r1 * kD + ((ch ^ ((r1 & 7) << 1)) * 8) + sub);
-        const s16x8 a = (s16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          if (act[t])
-            o[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb[t]),
-                                                              o[t][m], 0, 0, 0);
-      }
-      wave_lds_sync<NWV>();  // before the next tile overwrites v_lds
-    };
-
-    s16x8 kA[2][4], vA[8];
-    if constexpr (NT == 1) {
-      // NT 1 has the registers for a second page in flight: page j+1's K / V loads
-      // are issued before page j is processed (two register sets, unrolled by two), so
-      // a split walking several pages pays one memory round trip, not one per page
-      // The counted wait (a real S_WAITCNT, which the compiler's wait pass accounts
-      // for) retires page j -- in flight during page j-1 -- BEFORE page j+1 is issued.
-      // Without it the wait pass, merging its scoreboard over the loop back edge, treats
-      // page j's loads as the newest and waits on page j+1's too (vmcnt 15..0).
-      constexpr int kVmcnt0 = 0x0F70;          // vmcnt(0), expcnt / lgkmcnt untouched
-      s16x8 kB[2][4], vB[8];
-      fetch(0, kA, vA);
-      for (int j = 0; j < np; j += 2) {
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        if (j + 1 < np) fetch(j + 1, kB, vB);
-        process(j, kA, vA);
-        if (j + 1 >= np) break;
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        if (j + 2 < np) fetch(j + 2, kA, vA);
-        process(j + 1, kB, vB);
-      }
-    } else {
-      for (int j = 0; j < np; ++j) {
-        fetch(j, kA, vA);
-        process(j, kA, vA);
-      }
-    }
-  }
-
-  if constexpr (NWV > 1) {
-    // ---- merge the NWV waves' splits through LDS (the V tile buffers are reused) ----
-    __shared__ float ml_lds[NWV][NT][16][2];
-    float* obuf = reinterpret_cast<float*>(v_lds_all);   // (NWV-1) x 8 x 64 f32x4 <= v_lds
-    static_assert((NWV - 1) * 8 * 64 * 16 <= NWV * kPage * kD * 2, "merge buffer");
-    float lt[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      lt[t] = l_run[t];
-      lt[t] += __shfl_xor(lt[t], 16, 64);
-      lt[t] += __shfl_xor(lt[t], 32, 64);
-    }
-    __syncthreads();                                   // every wave is done with v_lds
-    if (g == 0) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        ml_lds[wv][t][c][0] = m_run[t];
-        ml_lds[wv][t][c][1] = lt[t];
-      }
-    }
-    __syncthreads();
-    float a_self[NT], l_all[NT], m_all[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float ms = -INFINITY;
-#pragma unroll
-      for (int v2 = 0; v2 < NWV; ++v2) ms = fmaxf(ms, ml_lds[v2][t][c][0]);
-      const float mu = ms == -INFINITY ? 0.f : ms;
-      float l = 0.f;
-#pragma unroll
-      for (int v2 = 0; v2 < NWV; ++v2) {
-        const float mw = ml_lds[v2][t][c][0];
-        l += (mw == -INFINITY ? 0.f : fast_exp2(mw - mu)) * ml_lds[v2][t][c][1];
-      }
-      a_self[t] = m_run[t] == -INFINITY ? 0.f : fast_exp2(m_run[t] - mu);
-      m_all[t] = ms;
-      l_all[t] = l;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if (wv > 0) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-          reinterpret_cast<f32x4*>(obuf)[((wv - 1) * 8 + m) * 64 + lane] = o[t][m] * a_self[t];
-      }
-      __syncthreads();
-      if (wv == 0) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          f32x4 acc = o[t][m] * a_self[t];
-#pragma unroll
-          for (int v2 = 1; v2 < NWV; ++v2)
-            acc += reinterpret_cast<const f32x4*>(obuf)[((v2 - 1) * 8 + m) * 64 + lane];
-          o[t][m] = acc;
-        }
-      }
-      __syncthreads();
-    }
-    if (wv != 0) return;
-    // wave 0 carries the workgroup's merged state into the epilogue below: the
-    // per-lane partial sums must add up to the merged denominator over the 4 groups
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      m_run[t] = m_all[t];
-      l_run[t] = g == 0 ? l_all[t] : 0.f;
-    }
-  }
-
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    // total softmax denominator for column c (lanes c, c+16, c+32, c+48)
-    float l_tot = l_run[t];
-    l_tot += __shfl_xor(l_tot, 16, 64);
-    l_tot += __shfl_xor(l_tot, 32, 64);
-    if (!cvalid[t]) continue;
-    if constexpr (MODE == 2) {
-      const int64_t pidx = (int64_t)qrow[t] * Hq + h[t];
-      float* po = px.pre_o + pidx * kD;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) *reinterpret_cast<f32x4*>(po + 16 * m + 4 * g) = o[t][m];
-      if (g == 0) {
-        px.pre_ml[pidx * 2 + 0] = m_run[t];
-        px.pre_ml[pidx * 2 + 1] = l_tot;
-      }
-      continue;
-    }
-    if (MODE == 1 && num_splits == 1 && base > 0) {
-      // merge the shared-prefix partial of this (row, head) column
-      const int64_t pidx = (int64_t)qrow[t] * Hq + h[t];
-      const float pm = px.pre_ml[pidx * 2 + 0], pl = px.pre_ml[pidx * 2 + 1];
-      const float* po = px.pre_o + pidx * kD;
-      const float mt = fmaxf(m_run[t], pm);
-      const float mu = mt == -INFINITY ? 0.f : mt;
-      const float a1 = fast_exp2(m_run[t] - mu), a2 = fast_exp2(pm - mu);
-      l_tot = l_tot * a1 + pl * a2;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(po + 16 * m + 4 * g);
-        o[t][m] = o[t][m] * a1 + pv * a2;
-      }
-    }
-    if (num_splits == 1) {
-      const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-      bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        uint2 wv;
-        wv.x = pack_bf16x2(o[t][m][0] * inv, o[t][m][1] * inv);
-        wv.y = pack_bf16x2(o[t][m][2] * inv, o[t][m][3] * inv);
-        *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
-      }
-    } else {
-      // partials write-through (8-byte agent-scope atomic stores = sc1): the in-kernel
-      // merge below reads them without a release / acquire pair
-      const int64_t pidx = ((int64_t)qrow[t] * Hq + h[t]) * num_splits + split;
-      float* po = part_o + pidx * kD;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        gu64* d = (gu64*)(po + 16 * m + 4 * g);
-        __hip_atomic_store(d, pack_f2(o[t][m][0], o[t][m][1]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 1, pack_f2(o[t][m][2], o[t][m][3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (g == 0)
-        __hip_atomic_store((gu64*)(part_ml + pidx * 2), pack_f2(m_run[t], l_tot),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (MODE != 0 || num_splits == 1 || tickets == nullptr) return;
-
-  // Single pass (cdna_hip_programming.md §6 Guideline 16, R1 counter form): the
-  // partials above are sc1 stores, drained by this wave's vmcnt(0) before its relaxed
-  // agent-scope ticket add; the last of the num_splits waves of this (work item, kv
-  // head) reads every partial with sc1 loads (no L1 copy can be stale, so no acquire
-  // fence), merges them and writes the bf16 output -- no second reduce launch -- then
-  // zeroes the ticket for the next launch on the stream.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  gu32* tk = (gu32*)(tickets + (int64_t)w * Hkv + kvh);
-  unsigned prev = 0;
-  if (lane == 0) prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
-  if (prev != (unsigned)num_splits - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
-  if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (!act[t] || !cvalid[t]) continue;
-    const int64_t pbase = ((int64_t)qrow[t] * Hq + h[t]) * num_splits;
-    // every split's (max, sum) in flight at once (num_splits <= 16), then the partial
-    // rows 2 splits at a time: the merge is a few memory round trips, not 16 chained
-    float ms[16], ls[16];
-#pragma unroll
-    for (int sp = 0; sp < 16; ++sp) {
-      ms[sp] = -INFINITY;
-      ls[sp] = 0.f;
-      if (sp < num_splits) {
-        const unsigned long long x = __hip_atomic_load((const gu64*)(part_ml + (pbase + sp) * 2),
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ms[sp] = __uint_as_float((unsigned)x);
-        ls[sp] = __uint_as_float((unsigned)(x >> 32));
-      }
-    }
-    float gm = -INFINITY;
-#pragma unroll
-    for (int sp = 0; sp < 16; ++sp) gm = fmaxf(gm, ms[sp]);
-    f32x4 num[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) num[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float den = 0.f;
-    if (gm != -INFINITY) {
-#pragma unroll
-      for (int s0 = 0; s0 < 16; s0 += 2) {
-        if (s0 >= num_splits) break;
-        f32x4 pv[2][8];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float* po = part_o + (pbase + min(s0 + u, num_splits - 1)) * kD;
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const gu64* d = (const gu64*)(po + 16 * m + 4 * g);
-            const unsigned long long x0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long x1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pv[u][m] = (f32x4){__uint_as_float((unsigned)x0), __uint_as_float((unsigned)(x0 >> 32)),
-                               __uint_as_float((unsigned)x1), __uint_as_float((unsigned)(x1 >> 32))};
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int sp = s0 + u;
-          const float wgt = (sp < num_splits && ms[sp] != -INFINITY) ? fast_exp2(ms[sp] - gm) : 0.f;
-          den += wgt * ls[sp];
-#pragma unroll
-          for (int m = 0; m < 8; ++m) num[m] += wgt * pv[u][m];
-        }
-      }
-    }
-    const float inv = den > 0.f ? 1.f / den : 0.f;
-    bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      uint2 wv;
-      wv.x = pack_bf16x2(num[m][0] * inv, num[m][1] * inv);
-      wv.y = pack_bf16x2(num[m][2] * inv, num[m][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
-    }
-  }
+  attn_decode_body<NT, MODE, NWV, NTK, false>(
+      q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+      work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2, num_splits, px,
+      tickets, blockIdx.x, blockIdx.y, blockIdx.z, NWV > 1 ? (int)(threadIdx.x >> 6) : 0,
+      v_lds_all, FuseWait{});
 }
 
 // Merge split-K partials: one workgroup of 128 lanes (one per dh) per (row, head).
@@ -595,6 +129,16 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
   out[(int64_t)b * out_stride + (int64_t)h * kD + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
 
+// Merge split-K partials of `rows` q rows (the fused QKV + attention launch leaves them
+// for this kernel, decode_fused.hip).
+void launch_attn_decode_reduce(const float* part_o, const float* part_ml, bf16_t* out,
+                               int64_t out_stride, int rows, int Hq, int num_splits,
+                               hipStream_t s) {
+  if (rows == 0 || num_splits <= 1) return;
+  attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
+                                                      num_splits);
+}
+
 // rows = number of q rows covered (for the split-K reduce), W = work items
 void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                         const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
@@ -606,6 +150,28 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
                         hipStream_t s) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
+  if (waves == 8 && num_splits % 8 == 0) {
+    // 8 splits per workgroup (one per wave, 2 waves per SIMD) merged in LDS: with 8
+    // splits per (work item, kv head) the whole attention is ONE launch with no
+    // cross-workgroup merge (outer == 1 writes bf16 rows directly)
+    const int outer = num_splits / 8;
+    const dim3 grid8(outer, Hkv, W);
+    int32_t* tk8 = outer > 1 ? tickets : nullptr;
+    if (tiles_per_item == 2)
+      attn_decode_kernel<2, 0, 8><<<grid8, 512, 0, s>>>(
+          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
+          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
+          outer, PrefixArgs{}, tk8);
+    else
+      attn_decode_kernel<1, 0, 8><<<grid8, 512, 0, s>>>(
+          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
+          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
+          outer, PrefixArgs{}, tk8);
+    if (outer > 1 && tk8 == nullptr)
+      attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
+                                                          outer);
+    return;
+  }
   if (waves == 4 && num_splits % 4 == 0) {
     // 4 splits per workgroup merged in LDS; the workgroups' partials merged in-kernel
     // by the last to finish (tickets) or, without tickets, by the reduce launch

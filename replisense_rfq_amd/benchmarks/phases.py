@@ -230,9 +230,11 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
     return out
 
 
-def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt, out_q):
+def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt, out_q,
+                    burst: int = 0):
     """One client process: a Poisson arrival stream at ``rate`` req/s for ``duration``
-    s of /parse-text/ emails and (``upload_share``) /upload/ attachments."""
+    s of /parse-text/ emails and (``upload_share``) /upload/ attachments, after an
+    initial burst of ``burst`` requests spread over the first second."""
     import asyncio
     import random
 
@@ -242,7 +244,10 @@ def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt
     sched, t, i = [], 0.0, 0
     fmts = ("pdf", "xlsx", "docx")
     while True:
-        t += rng.expovariate(rate)
+        if i < burst:
+            t = i / max(1, burst)
+        else:
+            t = max(t, 1.0) + rng.expovariate(rate)
         if t >= duration:
             break
         d = synth.make_rfq(seed * 1_000_003 + i)
@@ -259,7 +264,8 @@ def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt
 
 def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: float = 40.0,
                          upload_share: float = 0.25, client_procs: int = 8,
-                         parse_procs: int = 4, budget_s: float = 120.0, seed: int = 0) -> dict:
+                         parse_procs: int = 4, budget_s: float = 120.0, seed: int = 0,
+                         burst_depth: int = 0) -> dict:
     """does the HTTP surface sustain the engine's throughput?
 
     uvicorn + the FastAPI app (api/main.py, the reference's app/main.py:205-344
@@ -267,9 +273,13 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
     processes issue Poisson arrivals at ``rate`` requests/s in total (open loop: an
     arrival never waits for an earlier response), ``upload_share`` of them /upload/
     attachments (pdf/xlsx/docx through the parser pool), the rest /parse-text/.
+    ``burst_depth`` requests arrive in the first second (the engine's throughput
+    rises only slowly with its depth, so a Poisson stream started on an empty engine
+    needs minutes to reach its steady queue; the burst starts it near that depth).
     After ``warm_s`` of ramp-up, the window of ``measure_s`` reports the documents
     completed per second (every one validated by the service and enveloped), the
-    latency of the requests sent inside the window, and timeouts / errors."""
+    latency of the requests sent inside the window, the engine's in-flight depth
+    (running + waiting, sampled every 0.5 s) and timeouts / errors."""
     import multiprocessing as mp
 
     import uvicorn
@@ -312,27 +322,43 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
         start_evt, out_q = ctx.Event(), ctx.Queue()
         procs = [ctx.Process(target=_open_loop_proc,
                              args=(url, rate / client_procs, dur, 7_000 + 101 * i + seed,
-                                   upload_share, deadline, start_evt, out_q), daemon=True)
+                                   upload_share, deadline, start_evt, out_q,
+                                   burst_depth // client_procs
+                                   + (i < burst_depth % client_procs)), daemon=True)
                  for i in range(client_procs)]
         for p in procs:
             p.start()
-        time.sleep(3.0)                       # clients import aiohttp and build documents
+        time.sleep(3.0 + burst_depth / 2000.0)   # clients import aiohttp, build documents
+        depth, stop = [], threading.Event()
+
+        def sample(t0=time.perf_counter()):
+            while not stop.wait(0.5):
+                depth.append((time.perf_counter() - t0,
+                              engine.core.num_running + engine.core.num_waiting))
+
+        sampler = threading.Thread(target=sample, daemon=True)
         start_evt.set()
+        sampler.start()
         recs = []
         for _ in procs:
             recs += out_q.get(timeout=max(5.0, deadline - time.time() + 30))
+        stop.set()
         for p in procs:
             p.join(timeout=10)
         lo, hi = warm_s, warm_s + measure_s
         done_in = [r for r in recs if lo <= r[1] < hi]
         sent_in = [r for r in recs if lo <= r[0] < hi]
         ok = sum(r[3] for r in done_in)
+        win_depth = [d for t, d in depth if lo <= t < hi]
         res.update(requests=len(recs), docs=len(done_in),
                    docs_per_s=round(len(done_in) / measure_s, 3),
                    valid=round(ok / max(1, len(done_in)), 3),
                    http_latency_s=pcts([r[2] for r in sent_in]),
                    failed=sum(not r[3] for r in recs),
-                   unfinished=int(round(rate * dur)) - len(recs))
+                   burst_depth=burst_depth,
+                   engine_depth={"mean": round(statistics.mean(win_depth), 1),
+                                 "min": min(win_depth), "max": max(win_depth)}
+                   if win_depth else None)
         res["status"] = "ok"
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"

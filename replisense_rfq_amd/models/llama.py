@@ -327,6 +327,19 @@ class DecoderLM:
         hq, hkv = self.hq, self.hkv
         lw = self.w["layers"][li]
         kc, vc = self.kv_k[li], self.kv_v[li]
+        fcfg = self._fused_cfg(m, x, lw["qkv"], shared)
+        if fcfg >= 0:
+            # one launch: QKV GEMV + RoPE + KV append + decode attention (decode_fused.hip)
+            ns = m.decode_splits if dec_parts is not None else 1
+            po, pm = dec_parts if dec_parts is not None else (attn, attn)
+            run_tiles = 1 if T == m.dec_q_len.shape[0] else m.decode_tiles
+            ops.qkv_attn(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
+                         hq, hkv, fcfg, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
+                         m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, m.decode_tiles, run_tiles,
+                         attn[:D], po, pm, self.scale, ns, li, self.cfg.n_layers)
+            if ns > 1:
+                ops.attn_decode_merge(po, pm, attn[:D], hq, ns)
+            return
         qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
                            hq, hkv)
         if shared is not None:
@@ -346,6 +359,19 @@ class DecoderLM:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
                              self.scale, m.prefill_qblk)
+
+    def _fused_cfg(self, m: ForwardMeta, x, w_qkv, shared) -> int:
+        """Split-K cfg for the fused QKV + attention launch, or -1 to run the two
+        launches: decode / jump-forward rows only (no prefill rows in the step, at most
+        16), the split-K rope plan chose a GEMV for this shape, and the work list has one
+        or two column tiles per item."""
+        T, D = m.num_tokens, m.num_decode
+        if (not ops.FUSED_QKV_ATTN or not x.is_cuda or D == 0 or T != D or T > 16
+                or shared is not None or m.decode_tiles not in (1, 2)
+                or m.dec_work_seq is None or self.cfg.n_layers > ops.FUSE_SLOTS
+                or 32 * self.hkv > ops.FUSE_SLOT_WORDS or x.stride(1) != 1 or x.stride(0) % 8):
+            return -1
+        return ops.qkv_attn_cfg(T, w_qkv.shape[0], x.shape[1])
 
     # ------------------------------------------------------------- conveniences
     def weight_bytes(self) -> int:

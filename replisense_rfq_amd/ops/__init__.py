@@ -362,6 +362,75 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
     return qkv
 
 
+# Fused QKV + RoPE + KV append + decode attention (decode_fused.hip): one launch per
+# layer instead of the split-K QKV GEMV followed by the decode-attention launch, on
+# steps of <= 16 decode / jump-forward rows with no prefill rows.  Bit-identical to the
+# two launches (tests/kernels test_qkv_attn_fused) but measured SLOWER on MI355X at
+# batch 1 (profiles/r4_fused_qkv_attn.md: the in-launch hand-off -- write-through
+# results, a drained count, a poll, sc1 reads -- costs what the launch boundary plus the
+# attention's metadata chain cost, and holding each tile's last workgroup for its
+# write-through drain delays the QKV grid), so it is off by default:
+# RFQ_FUSED_QKV_ATTN=1 turns it on.
+FUSED_QKV_ATTN = os.environ.get("RFQ_FUSED_QKV_ATTN", "0") == "1"
+FUSE_SLOTS = 128            # per-layer counter slots (>= layers of any model served)
+FUSE_SLOT_WORDS = 256       # Hkv <= 8 counters per slot, one 128-B line each
+
+
+def fuse_ws(device):
+    """(zeroed int32 counter slots [FUSE_SLOTS, 256], int32 timeout counter [4]) of the
+    fused QKV + attention launch; allocated before any graph capture (stable pointers).
+    Slot l belongs to layer l; layer l's launch zeroes slot l - 1 (layer 0 zeroes the
+    last layer's), so every slot is zero when its launch starts."""
+    d = torch.device(device)
+    key = ("fuse", d)
+    ws = _NORM_COUNTERS.get(key)
+    if ws is None:
+        ws = _NORM_COUNTERS[key] = (torch.zeros(FUSE_SLOTS, FUSE_SLOT_WORDS, dtype=torch.int32,
+                                                device=d),
+                                    torch.zeros(4, dtype=torch.int32, device=d))
+    return ws
+
+
+def qkv_attn_cfg(M: int, N: int, K: int) -> int:
+    """The split-K GEMV cfg the fused launch streams the QKV weight with: the rope
+    plan's split-K entry for this shape (8 waves: the fused kernel's attention waves
+    set its occupancy), or -1 when the plan has none."""
+    cfg = rope_plan(M, N, K)
+    if cfg < 0 or not (cfg & SPLITK_BIT):
+        return -1
+    return (cfg & 127) | 4
+
+
+def qkv_attn(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, cfg,
+             block_tables, q_start, q_len, kv_len, work_seq, work_ct, list_tpi, run_tiles,
+             out, part_o, part_ml, scale, num_splits, layer: int, num_layers: int):
+    """One launch: qkv = x w^T with NeoX RoPE and the paged KV append, plus the decode
+    attention of the rows [0, out.shape[0]) into ``out`` (num_splits == 1) or into the
+    split partials (merge them with :func:`attn_decode_merge`).  ``layer`` picks the
+    counter slot; the launch zeroes slot ``layer - 1`` (mod ``num_layers``)."""
+    done, err = fuse_ws(x.device)
+    part, tiles = splitk_ws(x.device)
+    qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+    zero = done[(layer - 1) % num_layers] if num_layers > 1 else None
+    _native.ops().qkv_attn(x, _wsel(w, cfg | SPLITK_BIT), qkv, positions, cos_sin, slot_mapping,
+                           k_cache, v_cache, Hq, Hkv, part, tiles, cfg & 127, block_tables,
+                           q_start, q_len, kv_len, work_seq, work_ct, list_tpi, run_tiles, out,
+                           part_o, part_ml, scale, num_splits, done[layer], zero, err)
+    return qkv
+
+
+def attn_decode_merge(part_o, part_ml, out, Hq, num_splits):
+    """Merge split-K decode-attention partials into bf16 rows of ``out``."""
+    _native.ops().attn_decode_merge(part_o, part_ml, out, Hq, num_splits)
+
+
+def fuse_errors(device) -> int:
+    """Wait timeouts the fused QKV + attention launch counted (0 = all hand-offs met)."""
+    key = ("fuse", torch.device(device))
+    ws = _NORM_COUNTERS.get(key)
+    return int(ws[1][0].item()) if ws is not None else 0
+
+
 # (N, K) -> (quantum q, table) where table[j] is the row-chunk split (in units of q
 # rows, largest first) for M in ((j-1)q, jq], or None to keep one GEMM.  Filled by
 # ops.autotune.tune_split at engine start: hipBLASLt's heuristic is uneven across

@@ -27,6 +27,9 @@ from ..ops import _native
 
 # RFQ_CAR_NORM=0: keep the all-reduce and the residual-add RMSNorm as two launches
 FUSE_NORM = os.environ.get("RFQ_CAR_NORM", "1") != "0"
+# fused all-reduce + norm form: 0 = push (one xGMI hop, double-buffered slots) for
+# decode rows, staged above; 1 = always the staged one-shot (flag, remote read, end flag)
+CAR_NORM_ALGO = 1 if os.environ.get("RFQ_CAR_PUSH", "1") == "0" else 0
 
 
 class CustomAllReduce:
@@ -92,12 +95,16 @@ class CustomAllReduce:
                 and all(x.data_ptr() % 16 == 0 for x in (t, residual, out)))
 
     def all_reduce_add_norm_(self, t: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
-                             eps: float, out: torch.Tensor) -> torch.Tensor:
+                             eps: float, out: torch.Tensor, algo: int | None = None
+                             ) -> torch.Tensor:
         """residual <- bf16(sum over the group of t + residual); out <- rmsnorm(residual)
         * w, in one launch (bit-identical to all_reduce_ + fused_add_rms_norm; t itself
-        is left holding this rank's partial)."""
+        is left holding this rank's partial).  Decode rows (<= 16) use the push form:
+        every rank writes its row into the peers' double-buffered slots and raises one
+        flag, so a call is one xGMI hop with no end barrier (custom_ar.hip)."""
         torch.ops.rfq_amd.car_allreduce_add_norm(t, residual, w, eps, out, self.bases,
-                                                 self.rank, self.capacity)
+                                                 self.rank, self.capacity,
+                                                 CAR_NORM_ALGO if algo is None else algo)
         self.calls += 1
         return out
 
@@ -110,7 +117,7 @@ class CustomAllReduce:
         v = int(_native.ops().car_error_info(self.ptr))
         if not v & 0x80000000:
             return ""
-        phase = {1: "start", 2: "mid", 3: "end"}.get((v >> 24) & 0x7F, "?")
+        phase = {1: "start", 2: "mid", 3: "end", 4: "push"}.get((v >> 24) & 0x7F, "?")
         return f"{phase} flag of peer {v & 0xFF} at block {(v >> 8) & 0xFFFF} timed out"
 
     def close(self) -> None:

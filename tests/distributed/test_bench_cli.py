@@ -197,6 +197,7 @@ def test_bench_extra_phases_cpu():
     o = ph["http_open_loop"]
     assert o["status"] == "ok", o
     assert o["offered_rate"] == 3 and o["requests"] > 0 and o["failed"] == 0, o
+    assert o["burst_depth"] == 3 and o["engine_depth"] is not None
     assert o["docs_per_s"] > 0 and o["valid"] == 1.0 and o["http_latency_s"]["p50"] > 0
     assert o["http_vs_engine"] > 0
     h = ph["http_upload"]

@@ -89,7 +89,27 @@ def _worker(rank, world, port, q):
             o2 = ops.fused_add_rms_norm(t2, r2, w, 1e-5)
             torch.cuda.synchronize()
             errs.append(0.0 if (torch.equal(r1, r2) and torch.equal(o1, o2)) else 99.0)
-        # ... and inside a captured graph, replayed with fresh inputs
+        # the push form (one xGMI hop, parity double-buffered slots, no end barrier) is
+        # bit identical to the staged one; five calls in a row alternate the parity and
+        # interleave with staged calls on the same per-block counters
+        for rows, d in ((1, 8192), (3, 4096), (16, 8192), (2, 1000)):
+            for it in range(5):
+                g = torch.Generator(device="cuda").manual_seed(rows * 7919 + d + it)
+                parts = [torch.randn(rows, d, generator=g, device="cuda").to(torch.bfloat16)
+                         for _ in range(world)]
+                resid = torch.randn(rows, d, generator=g, device="cuda").to(torch.bfloat16)
+                w = (1 + 0.1 * torch.randn(d, generator=g, device="cuda")).to(torch.bfloat16)
+                outs = []
+                for algo in ((2, 1) if it % 2 else (1, 2)):
+                    t1, r1 = parts[rank].clone(), resid.clone()
+                    o1 = torch.empty_like(t1)
+                    car.all_reduce_add_norm_(t1, r1, w, 1e-5, o1, algo=algo)
+                    outs.append((r1, o1))
+                torch.cuda.synchronize()
+                (ra, oa), (rb, ob) = outs
+                errs.append(0.0 if (torch.equal(ra, rb) and torch.equal(oa, ob)) else 98.0)
+        # ... and inside a captured graph, replayed with fresh inputs (the default form
+        # for 4 decode rows is the push kernel)
         t = torch.empty(4, 8192, device="cuda", dtype=torch.bfloat16)
         r = torch.empty_like(t)
         o = torch.empty_like(t)

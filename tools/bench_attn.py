@@ -142,6 +142,18 @@ def main():
                     row[f"s{sp}_w4_us"] = round(run_latency(C, Hq, Hkv, sp, L=L, waves=4), 2)
                 print(json.dumps(row), flush=True)
         return
+    if os.environ.get("LAT_W8"):
+        # one split per wave + the reduce launch (default) vs 8-wave workgroups merged in
+        # LDS: s8 w8 = ONE workgroup per kv head, no cross-workgroup merge at all
+        for Hq, Hkv, L in ((32, 8, 32), (64, 8, 80), (8, 1, 80)):
+            for C in (512, 1024, 2048, 3072):
+                row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
+                row["s16_w1_us"] = round(run_latency(C, Hq, Hkv, 16, L=L), 2)
+                row["s8_w8_us"] = round(run_latency(C, Hq, Hkv, 8, L=L, waves=8), 2)
+                row["s16_w8_us"] = round(run_latency(C, Hq, Hkv, 16, L=L, waves=8), 2)
+                row["s32_w8_us"] = round(run_latency(C, Hq, Hkv, 32, L=L, waves=8), 2)
+                print(json.dumps(row), flush=True)
+        return
     if os.environ.get("TILES_AB"):
         # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
         for B, C, P, q in [(2048, 800, 416, 1), (2048, 800, 416, 3), (3072, 800, 416, 1)]:

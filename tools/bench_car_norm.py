@@ -70,10 +70,14 @@ def _worker(rank, world, port, rows_list, q):
             car.all_reduce_(t, 1)
             ops.fused_add_rms_norm(t, r, w, 1e-5, out=o)
 
-        def one():
-            car.all_reduce_add_norm_(t, r, w, 1e-5, o)
+        def staged():
+            car.all_reduce_add_norm_(t, r, w, 1e-5, o, algo=1)
 
-        out.append((rows, _time_graph(two, dist), _time_graph(one, dist)))
+        def push():
+            car.all_reduce_add_norm_(t, r, w, 1e-5, o, algo=2)
+
+        out.append((rows, _time_graph(two, dist), _time_graph(staged, dist),
+                    _time_graph(push, dist) if rows <= 16 else float("nan")))
     q.put((rank, out, car.errors()))
     dist.barrier()
     car.close()
@@ -82,7 +86,7 @@ def _worker(rank, world, port, rows_list, q):
 
 def main():
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-    rows_list = [int(x) for x in sys.argv[2:]] or [1, 4, 8, 32]
+    rows_list = [int(x) for x in sys.argv[2:]] or [1, 4, 8, 16, 32]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -96,10 +100,11 @@ def main():
     res.sort()
     print(f"world {world} (ranks share one GPU), d 8192, us per call; flag timeouts "
           f"{[e for _, _, e in res]}")
-    print("| rows | all-reduce + add-norm (2 launches) | fused (1 launch) |")
-    print("|---|---|---|")
-    for rows, two, one in res[0][1]:
-        print(f"| {rows} | {two:.2f} | {one:.2f} |")
+    print("| rows | all-reduce + add-norm (2 launches) | fused staged (flag, remote read, "
+          "end flag) | fused push (one hop, parity slots) |")
+    print("|---|---|---|---|")
+    for rows, two, one, push in res[0][1]:
+        print(f"| {rows} | {two:.2f} | {one:.2f} | {push:.2f} |")
 
 
 if __name__ == "__main__":
