@@ -45,13 +45,17 @@ void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, i
                      unsigned*, hipStream_t);
 void launch_attn_decode_reduce(const float*, const float*, bf16_t*, int64_t, int, int, int,
                                hipStream_t);
+bool gemv_merge_fits(int, int, int, int);
+void launch_gemv_splitk_merge(const float*, const float*, int, const bf16_t*, int, int, bf16_t*,
+                              int64_t, int, int, float*, unsigned*, bf16_t*, int64_t,
+                              const bf16_t*, bf16_t*, int64_t, float, unsigned*, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
-                        float, int, int, int32_t*, int, hipStream_t);
+                        float, int, int, int32_t*, int, hipStream_t, bool);
 void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16_t*,
                                const int32_t*, int, const int32_t*, const int32_t*,
                                const int32_t*, int, const int32_t*, const int32_t*, int, int,
@@ -359,6 +363,63 @@ void attn_decode_merge(const Tensor& part_o, const Tensor& part_ml, const Tensor
                                  out.stride(0), rows, (int)Hq, (int)num_splits, cur_stream());
 }
 
+// y = attn . w^T where attn [M, Hq * 128] is the decode attention still in its split
+// partials (part_o [M][Hq][S][128], part_ml [M][Hq][S][2] fp32): the split merge runs as
+// the split-K GEMV's prologue (gemv_core.h AM).  With residual / norm_w / out / counter
+// given, the residual-add RMSNorm epilogue of gemv_splitk_norm follows.
+void gemv_splitk_merge(const Tensor& part_o, const Tensor& part_ml, int64_t S, const Tensor& w,
+                       const Tensor& y, const Tensor& part, const Tensor& tile_cnt, int64_t cfg,
+                       const std::optional<Tensor>& residual, const std::optional<Tensor>& norm_w,
+                       double eps, const std::optional<Tensor>& out,
+                       const std::optional<Tensor>& counter) {
+  CHECK_DEV(y); CHECK_BF16(w); CHECK_BF16(y); CHECK_ROWMAJOR(y); CHECK_I32(tile_cnt);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemv_splitk_merge: w must be contiguous [N, K]");
+  const int64_t M = y.size(0), N = w.size(0), K = w.size(1), KS = 2 << (cfg & 3);
+  TORCH_CHECK(rfq::gemv_merge_fits((int)M, (int)K, (int)cfg, (int)S),
+              "gemv_splitk_merge: M <= 16, 2 <= S <= 16, K % 128 == 0, K / 128 >= KS, "
+              "M * slice heads * 128 <= 16384, no persistent cfg");
+  TORCH_CHECK(N % 16 == 0 && y.size(1) == N && y.stride(0) % 8 == 0, "gemv_splitk_merge: y [M, N]");
+  TORCH_CHECK(part_o.is_cuda() && part_ml.is_cuda() && part_o.scalar_type() == at::kFloat &&
+                  part_ml.scalar_type() == at::kFloat && part_o.is_contiguous() &&
+                  part_ml.is_contiguous() && part_o.numel() >= M * (K / 128) * S * 128 &&
+                  part_ml.numel() >= M * (K / 128) * S * 2,
+              "gemv_splitk_merge: fp32 partials [M][Hq][S][128] / [M][Hq][S][2]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
+              "gemv_splitk_merge: fp32 partials workspace of KS*M*N floats");
+  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, "gemv_splitk_merge: tile counters");
+  const bool norm = residual.has_value();
+  TORCH_CHECK(norm == norm_w.has_value() && norm == out.has_value() && norm == counter.has_value(),
+              "gemv_splitk_merge: residual, norm_w, out and counter go together");
+  rfq::bf16_t* res = nullptr;
+  rfq::bf16_t* o = nullptr;
+  const rfq::bf16_t* nw = nullptr;
+  unsigned* cnt = nullptr;
+  int64_t rs = 0, os = 0;
+  if (norm) {
+    CHECK_BF16(*residual); CHECK_BF16(*norm_w); CHECK_BF16(*out); CHECK_I32(*counter);
+    CHECK_ROWMAJOR(*residual); CHECK_ROWMAJOR(*out);
+    const int threads = (cfg & 4) ? 512 : 256;
+    TORCH_CHECK(N % 8 == 0 && N / 8 <= 4 * threads, "gemv_splitk_merge: N <= 32 * threads");
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N && out->size(0) == M &&
+                    out->size(1) == N && norm_w->numel() == N,
+                "gemv_splitk_merge: norm shapes");
+    TORCH_CHECK(residual->stride(0) % 8 == 0 && out->stride(0) % 8 == 0,
+                "gemv_splitk_merge: alignment");
+    TORCH_CHECK(counter->is_cuda() && counter->numel() >= 1, "gemv_splitk_merge: counter");
+    res = bpm(*residual);
+    o = bpm(*out);
+    nw = bp(*norm_w);
+    cnt = reinterpret_cast<unsigned*>(counter->data_ptr());
+    rs = residual->stride(0);
+    os = out->stride(0);
+  }
+  rfq::launch_gemv_splitk_merge(part_o.data_ptr<float>(), part_ml.data_ptr<float>(), (int)S, bp(w),
+                                (int)N, (int)K, bpm(y), y.stride(0), (int)M, (int)cfg,
+                                part.data_ptr<float>(),
+                                reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), res, rs, nw, o,
+                                os, (float)eps, cnt, cur_stream());
+}
+
 // y = x . w^T, split-K over (N/16) x KS workgroups with the in-launch per-tile
 // reduction (M <= 16).  tile_cnt: int32 [>= N/16], zero, left at zero.
 void gemv_splitk(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& part,
@@ -480,7 +541,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
                  const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
                  int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item,
-                 const std::optional<Tensor>& tickets, int64_t waves) {
+                 const std::optional<Tensor>& tickets, int64_t waves, bool reduce) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode: tiles_per_item in {1, 2}");
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
@@ -506,6 +567,8 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                     part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
                 "attn_decode: partial buffers too small");
   }
+  TORCH_CHECK(reduce || !tickets.has_value(),
+              "attn_decode: reduce=False leaves the partials to the consumer (no tickets)");
   int32_t* tk = nullptr;
   if (tickets.has_value() && num_splits > 1) {
     // zero-initialised once by the caller; the merging wave resets its entry
@@ -521,7 +584,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
-                          (float)scale, num_splits, tiles_per_item, tk, (int)waves, cur_stream());
+                          (float)scale, num_splits, tiles_per_item, tk, (int)waves, cur_stream(), reduce);
 }
 
 // Shared-prefix (cascade) decode attention, num_splits == 1; see attn_decode.hip.
@@ -972,6 +1035,9 @@ TORCH_LIBRARY(rfq_amd, m) {
         "int num_splits, Tensor(i!) done, Tensor(j!)? zero_slot, Tensor(k!) err) -> ()");
   m.def("attn_decode_merge(Tensor part_o, Tensor part_ml, Tensor(a!) out, int Hq, "
         "int num_splits) -> ()");
+  m.def("gemv_splitk_merge(Tensor part_o, Tensor part_ml, int S, Tensor w, Tensor(a!) y, "
+        "Tensor(b!) part, Tensor(c!) tile_cnt, int cfg, Tensor(d!)? residual, Tensor? norm_w, "
+        "float eps, Tensor(e!)? out, Tensor(f!)? counter) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
@@ -995,7 +1061,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
-        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None, int waves=1) -> ()");
+        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None, int waves=1, "
+        "bool reduce=True) -> ()");
   m.def("attn_decode_shared(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_ct, Tensor(a!) out, Tensor(b!) ws_i32, Tensor(c!) pre_o, Tensor(d!) pre_ml, "
@@ -1044,6 +1111,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("gemv_splitk_rope", &gemv_splitk_rope);
   m.impl("qkv_attn", &qkv_attn);
   m.impl("attn_decode_merge", &attn_decode_merge);
+  m.impl("gemv_splitk_merge", &gemv_splitk_merge);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);

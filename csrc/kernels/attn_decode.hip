@@ -139,7 +139,8 @@ void launch_attn_decode_reduce(const float* part_o, const float* part_ml, bf16_t
                                                       num_splits);
 }
 
-// rows = number of q rows covered (for the split-K reduce), W = work items
+// rows = number of q rows covered (for the split-K reduce), W = work items;
+// reduce = false leaves split partials for the consumer to merge (gemv_splitk_merge)
 void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                         const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
                         const int32_t* seq_q_start, const int32_t* seq_q_len,
@@ -147,7 +148,7 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
                         const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
                         float* part_o, float* part_ml, int Hq, int Hkv, float scale,
                         int num_splits, int tiles_per_item, int32_t* tickets, int waves,
-                        hipStream_t s) {
+                        hipStream_t s, bool reduce) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
   if (waves == 8 && num_splits % 8 == 0) {
@@ -167,7 +168,7 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
           q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
           seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
           outer, PrefixArgs{}, tk8);
-    if (outer > 1 && tk8 == nullptr)
+    if (outer > 1 && tk8 == nullptr && reduce)
       attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                           outer);
     return;
@@ -188,7 +189,7 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
           q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
           seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
           outer, PrefixArgs{}, tk4);
-    if (outer > 1 && tk4 == nullptr)
+    if (outer > 1 && tk4 == nullptr && reduce)
       attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                           outer);
     return;
@@ -212,7 +213,7 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
   }
 #undef RFQ_AD_LAUNCH
   // without a ticket buffer the split partials are merged by a second launch
-  if (num_splits > 1 && tk == nullptr)
+  if (num_splits > 1 && tk == nullptr && reduce)
     attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
                                                         num_splits);
 }

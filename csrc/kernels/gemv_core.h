@@ -167,16 +167,39 @@ enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
 // attention waves of that kv head, running in the same launch, poll that counter and
 // read q and the new KV rows with sc1 loads (cdna_hip_programming.md §6 Guideline 16,
 // R1 counter form; the producer is one wave, so no workgroup barrier is needed).
-template <int NW, int U, int EPI, bool TL, bool NTL, bool PUB = false>
+//
+// AM (attention-merge prologue; kGvPlain / kGvNorm): X is not read from memory but is
+// the decode attention output still in its split-K partials (attn_decode.hip with
+// num_splits > 1 and no reduce launch): part_o [rows][Hq][S][128], part_ml
+// [rows][Hq][S][2] fp32, K = Hq * 128, so a unit's K slice is a run of whole heads.
+// The unit first issues its first weight round, then every thread merges float4
+// granules of the slice's heads (all S partials in flight at once, the same
+// arithmetic and order as attn_decode_reduce_kernel, so bit-identical rows) into a
+// bf16 LDS copy of the M x slice rows, and the MFMA loop reads X from there.  This is
+// the o projection with the separate merge launch folded in: the partial reads (a few
+// KB per head, L2-resident) overlap the unit's own weight stream instead of costing a
+// launch boundary plus the merge kernel's latency chain.
+struct AttnMerge {
+  const float* po;
+  const float* ml;
+  int S;                          // splits, 2..16
+};
+constexpr int kAmMaxS = 16;
+constexpr int kAmLdsElems = 16384;  // M * (slice heads) * 128 bf16 <= 32 KB
+
+template <int NW, int U, int EPI, bool TL, bool NTL, bool PUB = false, bool AM = false>
 __device__ __forceinline__ void gemv_splitk_unit(
     int unit, int ntile, const bf16_t* __restrict__ X, int64_t ldx,
     const bf16_t* __restrict__ W, int K, bf16_t* __restrict__ Y, int64_t ldy, int M, int KS,
     float* __restrict__ part, int Nn, unsigned* __restrict__ tile_cnt, const NormEpi& ep,
-    const RopeEpi& re, int up_off, unsigned* __restrict__ done = nullptr) {
+    const RopeEpi& re, int up_off, unsigned* __restrict__ done = nullptr,
+    AttnMerge am = AttnMerge{}) {
   static_assert(!PUB || EPI == kGvRope, "PUB: the rope epilogue only");
+  static_assert(!AM || EPI == kGvPlain || EPI == kGvNorm, "AM: plain / norm epilogues only");
   constexpr int NT = EPI >= kGvSwi ? 2 : 1;
   __shared__ f32x4 red[NW][NT][64];
   __shared__ float nscratch[17];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[AM ? kAmLdsElems : 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int bt = unit / KS, slice = unit - bt * KS;
@@ -202,21 +225,86 @@ __device__ __forceinline__ void gemv_splitk_unit(
     wp[a] = TL ? W + (int64_t)(row0[a] >> 4) * (K >> 7) * 2048 + lane * 8
                : W + (int64_t)(row0[a] + r) * K + g * 8;
   const bool xv = r < M;
-  const bf16_t* xp = X + (int64_t)(xv ? r : 0) * ldx + g * 8;
+  // AM: X rows live in LDS as [M][nks * 128] (slice-relative k); else in global memory
+  const bf16_t* xp = AM ? xs + (int64_t)(xv ? r : 0) * nks * 128 - sl0 * 128 + g * 8
+                        : X + (int64_t)(xv ? r : 0) * ldx + g * 8;
   const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
   f32x4 acc[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   int ks = ks0;
+  s16x8 w0[U][NT][4];
+  bool pre = false;
+  if constexpr (AM) {
+    // the first weight round goes out before the merge so the two overlap
+    if (ks + U <= ks1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            w0[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
+      pre = true;
+    }
+    const int Hq = K >> 7, S = am.S;
+    for (int it = threadIdx.x; it < M * nks * 32; it += NW * 64) {
+      const int d4 = it & 31, rest = it >> 5;
+      const int rr = rest / nks, hl = rest - rr * nks;
+      const int64_t bh = (int64_t)rr * Hq + sl0 + hl;
+      const float* mlp = am.ml + bh * S * 2;
+      const float* pop = am.po + bh * S * 128 + d4 * 4;
+      float2 m2[kAmMaxS];
+      f32x4 p[kAmMaxS];
+#pragma unroll
+      for (int s = 0; s < kAmMaxS; ++s)
+        if (s < S) {
+          m2[s] = *reinterpret_cast<const float2*>(mlp + 2 * s);
+          p[s] = *reinterpret_cast<const f32x4*>(pop + s * 128);
+        }
+      float gm = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < kAmMaxS; ++s)
+        if (s < S) gm = fmaxf(gm, m2[s].x);
+      f32x4 num = {0.f, 0.f, 0.f, 0.f};
+      float den = 0.f;
+      if (gm != -INFINITY) {
+#pragma unroll
+        for (int s = 0; s < kAmMaxS; ++s) {   // no break / continue: keeps m2 / p in VGPRs
+          if (s < S && m2[s].x != -INFINITY) {
+            const float wgt = fast_exp2(m2[s].x - gm);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) num[i] += wgt * p[s][i];
+            den += wgt * m2[s].y;
+          }
+        }
+      }
+      uint2 v;
+      v.x = pack_bf16x2(den > 0.f ? num[0] / den : 0.f, den > 0.f ? num[1] / den : 0.f);
+      v.y = pack_bf16x2(den > 0.f ? num[2] / den : 0.f, den > 0.f ? num[3] / den : 0.f);
+      *reinterpret_cast<uint2*>(xs + (rr * nks + hl) * 128 + d4 * 4) = v;
+    }
+    __syncthreads();
+  }
   for (; ks + U <= ks1; ks += U) {
     s16x8 w[U][NT][4], x[U][4];
+    if (AM && pre) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int a = 0; a < NT; ++a)
+        for (int a = 0; a < NT; ++a)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
+          for (int j = 0; j < 4; ++j) w[u][a][j] = w0[u][a][j];
+      pre = false;
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll

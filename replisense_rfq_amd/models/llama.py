@@ -206,14 +206,24 @@ class DecoderLM:
         dec_parts, shared = self._attn_scratch(m, x)
         moe_bufs = self.moe_buffers(T) if (cfg.is_moe and x.is_cuda) else None
         L = cfg.n_layers
+        # TP = 1 latency path: the o / down skinny GEMM runs the residual-add
+        # RMSNorm in its last workgroup when the start-up plan measured it faster
+        fuse = not self.tp.enabled and T <= ops.NORM_FUSE_MAX_M
+        mcfg = self._merge_cfg(m, x, dec_parts, shared, fuse)
         for li in range(L):
             lw = w["layers"][li]
-            self._attend(li, x, attn, m, dec_parts, shared)
-            # TP = 1 latency path: the o / down skinny GEMM runs the residual-add
-            # RMSNorm in its last workgroup when the start-up plan measured it faster
-            fuse = not self.tp.enabled and T <= ops.NORM_FUSE_MAX_M
-            if not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
-                                                 x)):
+            self._attend(li, x, attn, m, dec_parts, shared, merge=mcfg >= 0)
+            if mcfg >= 0:
+                # the attention left its split partials: the o GEMV merges them itself
+                po, pm = dec_parts
+                if fuse:
+                    ops.linear_merge(po, pm, m.decode_splits, lw["o"], T, mcfg,
+                                     norm=(residual, lw["mlp_norm"], eps, x))
+                else:
+                    o = ops.linear_merge(po, pm, m.decode_splits, lw["o"], T, mcfg)
+                    self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
+            elif not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
+                                                   x)):
                 o = ops.linear(attn, lw["o"])
                 self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
@@ -320,9 +330,12 @@ class DecoderLM:
                       torch.empty(D * hq * 2, device=self.device))
         return dec_parts, shared
 
-    def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared) -> None:
+    def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared,
+                merge: bool = False) -> None:
         """QKV GEMM + RoPE + paged-KV append, then decode / prefill attention into
-        ``attn`` (rows [0, T) of x and attn; rows past T are SP padding)."""
+        ``attn`` (rows [0, T) of x and attn; rows past T are SP padding).  ``merge``:
+        the decode attention leaves its split partials in ``dec_parts`` for the o
+        projection (ops.linear_merge) instead of merging them into ``attn``."""
         T, D = m.num_tokens, m.num_decode
         hq, hkv = self.hq, self.hkv
         lw = self.w["layers"][li]
@@ -354,11 +367,30 @@ class DecoderLM:
             ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                             m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
                             hq, hkv, self.scale, ns, m.decode_tiles,
-                            self._dec_tickets(m.dec_work_seq.numel(), waves), waves)
+                            None if merge else self._dec_tickets(m.dec_work_seq.numel(), waves),
+                            waves, reduce=not merge)
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
                              self.scale, m.prefill_qblk)
+
+    def _merge_cfg(self, m: ForwardMeta, x, dec_parts, shared, norm: bool) -> int:
+        """Split-K cfg of the o projection that merges the decode attention's split
+        partials in its prologue (ops.linear_merge), or -1: decode / jump-forward rows
+        only, split attention through the one-wave kernel and the separate merge launch
+        (no tickets, no 4-wave form, no cascade, no fused QKV + attention launch), and a
+        start-up plan entry that measured the fold faster."""
+        T, D = m.num_tokens, m.num_decode
+        if (not x.is_cuda or D == 0 or T != D or T > 16 or dec_parts is None
+                or shared is not None or SINGLE_PASS_DECODE):
+            return -1
+        ns = m.decode_splits
+        if DECODE_WG_MERGE and ns >= 4 and ns % 4 == 0:
+            return -1
+        if self._fused_cfg(m, x, self.w["layers"][0]["qkv"], shared) >= 0:
+            return -1
+        wo = self.w["layers"][0]["o"]
+        return ops.merge_plan(T, wo.shape[0], wo.shape[1], ns, norm)
 
     def _fused_cfg(self, m: ForwardMeta, x, w_qkv, shared) -> int:
         """Split-K cfg for the fused QKV + attention launch, or -1 to run the two

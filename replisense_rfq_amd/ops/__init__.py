@@ -285,6 +285,51 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     return True
 
 
+# (M, N, K, S, norm) -> split-K GEMV cfg (| SPLITK_BIT) of the o projection that merges
+# the decode attention's S split partials in its prologue (gemv_splitk_merge), filled
+# by autotune.tune_merge where it beat merge launch + planned o path; absent = unfused.
+_MERGE_PLAN: dict[tuple, int] = {}
+MERGE_AM_MAX_S = 16
+MERGE_AM_LDS = 16384
+
+
+def set_merge_plan(plan: dict) -> None:
+    _MERGE_PLAN.clear()
+    _MERGE_PLAN.update(plan)
+
+
+def gemv_merge_fits(M: int, K: int, cfg: int, S: int) -> bool:
+    """Host mirror of gemm_skinny.hip gemv_merge_fits: the slice's merged rows fit the
+    kernel's LDS copy."""
+    KS = 2 << (cfg & 3)
+    nks_all = K // 128
+    nks_max = -(-nks_all // KS)
+    return (1 <= M <= 16 and 2 <= S <= MERGE_AM_MAX_S and K % 128 == 0 and nks_all >= KS
+            and M * nks_max * 128 <= MERGE_AM_LDS and not cfg & SPLITK_PERSIST)
+
+
+def merge_plan(M: int, N: int, K: int, S: int, norm: bool) -> int:
+    return _MERGE_PLAN.get((M, N, K, S, norm), -1) if _MERGE_PLAN else -1
+
+
+def linear_merge(part_o, part_ml, S: int, w, M: int, cfg: int, norm=None) -> torch.Tensor:
+    """y [M, N] = attn . w^T where attn [M, K] is still split into the decode attention's
+    S partials (attn_decode reduce=False): the merge runs in the split-K GEMV's prologue.
+    ``norm`` = (residual, norm_w, eps, out): the residual-add RMSNorm epilogue too."""
+    N, K = w.shape
+    y = torch.empty((M, N), dtype=w.dtype, device=w.device)
+    part, tiles = splitk_ws(w.device)
+    if norm is None:
+        _native.ops().gemv_splitk_merge(part_o, part_ml, S, _wsel(w, cfg), y, part, tiles,
+                                        cfg & 127, None, None, 0.0, None, None)
+    else:
+        residual, norm_w, eps, out = norm
+        _native.ops().gemv_splitk_merge(part_o, part_ml, S, _wsel(w, cfg), y, part, tiles,
+                                        cfg & 127, residual, norm_w, eps, out,
+                                        norm_counter(w.device))
+    return y
+
+
 # (M, F, K) -> skinny cfg of the gate|up projection with the SwiGLU epilogue
 # (gemm_skinny.hip SWI: out [M, F] = silu(x Wg^T) * (x Wu^T)), or absent = unfused.
 _SWI_PLAN: dict[tuple[int, int, int], int] = {}
@@ -626,18 +671,20 @@ def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
 
 def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq, work_ct,
                 out, part_o, part_ml, Hq, Hkv, scale, num_splits=1, tiles_per_item=1,
-                tickets=None, waves: int = 1):
+                tickets=None, waves: int = 1, reduce: bool = True):
     """Paged attention for decode / short-extend rows (see csrc/kernels/attn_decode.hip).
     A work item (work_seq[w], work_ct[w]) covers column tiles
     [work_ct*tiles_per_item, +tiles_per_item) of its sequence's q_len*G (query, head) pairs.
     With num_splits > 1, ``tickets`` (int32 zeros, >= work items * Hkv, reset by the kernel)
     makes it single-pass: the last split to finish merges the partials in-kernel.
     ``waves`` = 4 (num_splits % 4 == 0): four splits per workgroup merged through LDS,
-    so only num_splits / 4 partials reach the in-kernel (or reduce-launch) merge."""
+    so only num_splits / 4 partials reach the in-kernel (or reduce-launch) merge.
+    ``reduce=False`` (num_splits > 1, no tickets): the split partials are left in
+    part_o / part_ml for the o projection to merge (:func:`linear_merge`)."""
     if _gpu(q):
         _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
                                   work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
-                                  num_splits, tiles_per_item, tickets, waves)
+                                  num_splits, tiles_per_item, tickets, waves, reduce)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
                          out, Hq, Hkv, scale)

@@ -736,6 +736,64 @@ def test_gemv_splitk(gpu, M, cfg, N, K):
 
 
 @pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("S", [2, 8, 16])
+@pytest.mark.parametrize("cfg", [0, 1, 9, 13 | 16 | 32, 14 | 16])
+@pytest.mark.parametrize("Hq,N", [(8, 8192), (32, 4096)])
+def test_gemv_splitk_merge(gpu, M, S, cfg, Hq, N):
+    """o projection with the decode attention's split merge as its prologue
+    (gemv_splitk_merge) == attn_decode_merge followed by gemv_splitk, bit for bit (plain
+    and residual-add RMSNorm epilogues, row-major and tiled weights, splits with no keys
+    (m = -inf)); the merged rows vs an fp32 merge; tickets and the norm counter left at
+    zero over repeated launches."""
+    K = Hq * 128
+    if not ops.gemv_merge_fits(M, K, cfg, S):
+        pytest.skip("slice rows exceed the LDS copy")
+    torch.manual_seed(M * 31 + S + cfg + Hq)
+    po = torch.randn(M, Hq, S, 128, device=gpu)
+    ml = torch.empty(M, Hq, S, 2, device=gpu)
+    ml[..., 0] = torch.randn(M, Hq, S, device=gpu) * 4
+    ml[..., 1] = torch.rand(M, Hq, S, device=gpu) * 30 + 0.5
+    empty = torch.rand(M, Hq, S, device=gpu) < 0.2
+    ml[..., 0][empty] = float("-inf")
+    ml[..., 1][empty] = 0.0
+    ml[0, 0, :, 0] = float("-inf")                      # a head with no keys at all -> 0
+    ml[0, 0, :, 1] = 0.0
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    ww = ops.tile_weight(w) if cfg & ops.SPLITK_TILED else w
+    part, tiles = ops.splitk_ws(gpu)
+    attn = torch.empty(M, K, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.attn_decode_merge(po, ml, attn, Hq, S)
+    # fp32 merge oracle for the rows the prologue builds
+    m = ml[..., 0]
+    gm = m.amax(-1, keepdim=True)
+    wgt = torch.where(m == float("-inf"), torch.zeros_like(m), torch.exp2(m - gm))
+    wgt = torch.nan_to_num(wgt)
+    den = (wgt * ml[..., 1]).sum(-1)
+    num = (wgt[..., None] * po).sum(-2)
+    want_attn = torch.where(den[..., None] > 0, num / den.clamp_min(1e-30)[..., None],
+                            torch.zeros_like(num)).reshape(M, K)
+    _close(attn, want_attn, 2e-2, 1e-2, "merge oracle")
+    y0, y1 = (torch.empty(M, N, device=gpu, dtype=BF) for _ in range(2))
+    torch.ops.rfq_amd.gemv_splitk(attn, ww, y0, part, tiles, cfg)
+    for it in range(3):
+        y1.fill_(float("nan"))
+        torch.ops.rfq_amd.gemv_splitk_merge(po, ml, S, ww, y1, part, tiles, cfg, None, None, 0.0,
+                                            None, None)
+        assert torch.equal(y0, y1), f"plain it={it}"
+    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
+    res = torch.randn(M, N, device=gpu, dtype=BF)
+    counter = torch.zeros(4, dtype=torch.int32, device=gpu)
+    r0, r1 = res.clone(), res.clone()
+    o0, o1 = (torch.empty(M, N, device=gpu, dtype=BF) for _ in range(2))
+    torch.ops.rfq_amd.gemv_splitk_norm(attn, ww, y0, r0, nw, 1e-5, o0, counter, part, tiles, cfg)
+    torch.ops.rfq_amd.gemv_splitk_merge(po, ml, S, ww, y1, part, tiles, cfg, r1, nw, 1e-5, o1,
+                                        counter)
+    assert torch.equal(r0, r1) and torch.equal(o0, o1), "norm epilogue"
+    torch.cuda.synchronize()
+    assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
+
+
+@pytest.mark.parametrize("M", [1, 3, 16])
 @pytest.mark.parametrize("cfg", [0, 2, 9, 13, 14])
 @pytest.mark.parametrize("F,K", [(3584, 8192), (512, 1024)])
 def test_gemv_splitk_swiglu(gpu, M, cfg, F, K):
