@@ -66,6 +66,7 @@ void launch_attn_prefill(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, c
                          const int32_t*, int, bf16_t*, int64_t, int, int, float, int, int,
                          float*, int32_t*, int, hipStream_t);
 int prefill_split_ws_floats();
+void set_attn_prefill_timing(uint64_t*);
 int prefill_split_tickets();
 void launch_sample_partial(const bf16_t*, int64_t, int, int, int, const uint32_t*, int,
                            const int32_t*, const float*, const uint64_t*, float*, int32_t*, int,
@@ -418,6 +419,17 @@ void gemv_splitk_merge(const Tensor& part_o, const Tensor& part_ml, int64_t S, c
                                 part.data_ptr<float>(),
                                 reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), res, rs, nw, o,
                                 os, (float)eps, cnt, cur_stream());
+}
+
+// Diagnostics: while `buf` is set (int64, >= 8 words per workgroup), every attn_prefill
+// launch stamps each workgroup's phases (s_memrealtime, 100 MHz) into it; an empty
+// tensor clears it.
+void attn_prefill_timing(const Tensor& buf) {
+  CHECK_DEV(buf);
+  TORCH_CHECK(buf.scalar_type() == at::kLong && buf.is_contiguous(),
+              "attn_prefill_timing: int64 buffer");
+  rfq::set_attn_prefill_timing(
+      buf.numel() > 0 ? reinterpret_cast<uint64_t*>(buf.data_ptr()) : nullptr);
 }
 
 // y = x . w^T, split-K over (N/16) x KS workgroups with the in-launch per-tile
@@ -1067,6 +1079,7 @@ TORCH_LIBRARY(rfq_amd, m) {
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_ct, Tensor(a!) out, Tensor(b!) ws_i32, Tensor(c!) pre_o, Tensor(d!) pre_ml, "
         "int Hq, int Hkv, float scale, int tiles_per_item, bool run_meta) -> ()");
+  m.def("attn_prefill_timing(Tensor(a!) buf) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
         "Tensor work_qblk, Tensor(a!) out, int Hq, int Hkv, float scale, int qblk=32, "
@@ -1120,6 +1133,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("attn_decode", &attn_decode);
   m.impl("attn_decode_shared", &attn_decode_shared);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("attn_prefill_timing", &attn_prefill_timing);
   m.impl("sample_partial", &sample_partial);
   m.impl("sample_final", &sample_final);
   m.impl("moe_topk", &moe_topk);

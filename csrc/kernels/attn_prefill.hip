@@ -61,8 +61,14 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_qblk, bf16_t* __restrict__ out, int64_t out_stride, int Hq,
     int Hkv, float scale_log2, int hgroups, int kvsplit = 1, float* __restrict__ ws = nullptr,
-    int32_t* __restrict__ tickets = nullptr) {
+    int32_t* __restrict__ tickets = nullptr, uint64_t* __restrict__ ts = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // ts (diagnostics, attn_prefill_timing): per workgroup 8 words of s_memrealtime
+  // (100 MHz) stamps written by thread 0 -- entry, metadata, first tiles landed, key
+  // loop done, split hand-off done, end; word 6 = tiles | split << 16 | merger << 17
+  const bool stamp = ts != nullptr && threadIdx.x == 0;
+  uint64_t* const tsw = ts != nullptr ? ts + (int64_t)blockIdx.x * 8 : nullptr;
+  if (stamp) tsw[0] = __builtin_amdgcn_s_memrealtime();
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
   constexpr int NT = NW * 64;
   constexpr int NCH = kKT * 16 / NT;
@@ -114,6 +120,10 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   const bool split = nact > 1;
   const int t0 = kvs * ntiles / nact;
   const int t1 = (kvs + 1) * ntiles / nact;
+  if (stamp) {
+    tsw[1] = __builtin_amdgcn_s_memrealtime();
+    tsw[6] = (uint64_t)(t1 - t0) | ((uint64_t)split << 16);
+  }
   const int wend = min(wt, t1);
 
   lds_c* const lbase = (lds_c*)smem;
@@ -327,6 +337,7 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   wait_dma(t0 + 2 < t1);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if (stamp) tsw[2] = __builtin_amdgcn_s_memrealtime();
   if (wend > t0) {
     qk(t0);
     sm_max();
@@ -360,6 +371,7 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     asm volatile("" ::: "memory");
   }
 
+  if (stamp) tsw[3] = __builtin_amdgcn_s_memrealtime();
   float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   if (split) {
     // Hand-off of the unnormalised O, running max (raw score units) and row sum between
@@ -393,45 +405,75 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
         __hip_atomic_store(tickets + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if (stamp) {
+      tsw[4] = __builtin_amdgcn_s_memrealtime();
+      tsw[6] |= (uint64_t)s_second << 17;
+    }
     if (!s_second) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
-    // every partner's (max, sum) first, then one rescale per partial
-    float m_p[kMaxKvSplit], l_p[kMaxKvSplit];
+    // The np = nact - 1 partners p(i) (ascending split index, skipping this one) are
+    // merged in ascending order, as one rescale per partial.  Their loads are
+    // pipelined: every (max, sum) and the first partial's O go out together; with 4
+    // waves (512 VGPRs per lane) the second's too, and the third's once the first has
+    // been consumed (two load round trips instead of one per partner plus one for the
+    // (max, sum)); the 8-wave form (256 VGPRs, a second 64-register buffer spills)
+    // loads each further partial after the previous one is absorbed.
+    const int np = nact - 1;
+    auto pidx = [&](int i) { return i < kvs ? i : i + 1; };
+    auto part = [&](int i) {
+      return ws + (((int64_t)bid * kMaxKvSplit + pidx(i)) * NW + wid) * kPart;
+    };
+    auto ld8 = [&](const float* p) {
+      return __hip_atomic_load((const gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    unsigned long long mlv[kMaxKvSplit - 1];
+#pragma unroll
+    for (int i = 0; i < kMaxKvSplit - 1; ++i)
+      mlv[i] = i < np ? ld8(part(i) + 4096 + lane * 2) : 0ull;
+    unsigned long long ua[32], ub[NW == 4 ? 32 : 1];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) ua[i] = ld8(part(0) + (i * 64 + lane) * 2);
+    if constexpr (NW == 4) {
+      if (np > 1) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) ub[i] = ld8(part(1) + (i * 64 + lane) * 2);
+      }
+    }
+    float m_p[kMaxKvSplit - 1], l_p[kMaxKvSplit - 1];
     float m_n = m_run;
 #pragma unroll
-    for (int j = 0; j < kMaxKvSplit; ++j) {
-      m_p[j] = -INFINITY;
-      l_p[j] = 0.f;
-      if (j < nact && j != kvs) {
-        const float* other = ws + (((int64_t)bid * kMaxKvSplit + j) * NW + wid) * kPart;
-        const unsigned long long ml =
-            __hip_atomic_load((const gu64*)(other + 4096 + lane * 2), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-        m_p[j] = __uint_as_float((unsigned)ml);
-        l_p[j] = __uint_as_float((unsigned)(ml >> 32));
-        m_n = fmaxf(m_n, m_p[j]);
-      }
+    for (int i = 0; i < kMaxKvSplit - 1; ++i) {
+      m_p[i] = i < np ? __uint_as_float((unsigned)mlv[i]) : -INFINITY;
+      l_p[i] = i < np ? __uint_as_float((unsigned)(mlv[i] >> 32)) : 0.f;
+      m_n = fmaxf(m_n, m_p[i]);
     }
     const float a_s = m_run == -INFINITY ? 0.f : fast_exp2((m_run - m_n) * scale_log2);
     l_tot *= a_s;
 #pragma unroll
     for (int m = 0; m < 4; ++m) o[m] *= a_s;
+    auto absorb = [&](const unsigned long long* u, int i) {
+      const float a_o = m_p[i] == -INFINITY ? 0.f : fast_exp2((m_p[i] - m_n) * scale_log2);
+      l_tot += l_p[i] * a_o;
 #pragma unroll
-    for (int j = 0; j < kMaxKvSplit; ++j) {
-      if (j >= nact || j == kvs) continue;
-      const float a_o = m_p[j] == -INFINITY ? 0.f : fast_exp2((m_p[j] - m_n) * scale_log2);
-      l_tot += l_p[j] * a_o;
-      const float* other = ws + (((int64_t)bid * kMaxKvSplit + j) * NW + wid) * kPart;
-      unsigned long long u[32];
+      for (int k = 0; k < 32; ++k) {
+        const int m = k >> 3, e = 2 * (k & 7);
+        o[m][e] += __uint_as_float((unsigned)u[k]) * a_o;
+        o[m][e + 1] += __uint_as_float((unsigned)(u[k] >> 32)) * a_o;
+      }
+    };
+    absorb(ua, 0);
+    if constexpr (NW == 4) {
+      if (np > 2) {
 #pragma unroll
-      for (int i = 0; i < 32; ++i)
-        u[i] = __hip_atomic_load((const gu64*)(other + (i * 64 + lane) * 2), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 0; i < 32; ++i) ua[i] = ld8(part(2) + (i * 64 + lane) * 2);
+      }
+      if (np > 1) absorb(ub, 1);
+      if (np > 2) absorb(ua, 2);
+    } else {
+      for (int i2 = 1; i2 < np; ++i2) {
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const int m = i >> 3, e = 2 * (i & 7);
-        o[m][e] += __uint_as_float((unsigned)u[i]) * a_o;
-        o[m][e + 1] += __uint_as_float((unsigned)(u[i] >> 32)) * a_o;
+        for (int i = 0; i < 32; ++i) ua[i] = ld8(part(i2) + (i * 64 + lane) * 2);
+        absorb(ua, i2);
       }
     }
   }
@@ -456,6 +498,7 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
       *reinterpret_cast<u32x4*>(out + (int64_t)(tok0 + qs + row) * out_stride +
                                 (int64_t)head * kPD + 8 * cc) = v;
   }
+  if (stamp) tsw[5] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Split-KV workspace (ws, tickets): per (work item, kv head, head group) up to 4 splits
@@ -471,6 +514,11 @@ int prefill_split_tickets() { return kPrefillSplitMaxWg / 2; }
 // hsplit_below: when num_work * Hkv is below this many workgroups (the grid cannot
 // fill the CUs) and the 8 waves are one query block of 8 heads (G = 8, qblk 32), the
 // heads are split over 2 workgroups of 4 waves (0 = never).
+// Diagnostics: while set, every attn_prefill launch stamps its workgroups' phases into
+// this buffer (>= 8 words per workgroup; attn_prefill_kernel ts).
+static uint64_t* g_prefill_ts = nullptr;
+void set_attn_prefill_timing(uint64_t* buf) { g_prefill_ts = buf; }
+
 void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                          const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
                          const int32_t* seq_q_start, const int32_t* seq_q_len,
@@ -488,14 +536,14 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
   //     top while the grid fits the CUs once;
   //   8-wave split-KV (small_mode 2): all G heads in one 8-wave workgroup (two waves per
   //     SIMD), the key tiles split 2-4 ways.
-  // small_mode 0 (auto) takes the head split while it can also split the keys (grids up
-  // to 64 workgroups) and the 8-wave split-KV above that: B1 S4096 Hq8/Hkv1 98 -> 76 us,
-  // B2 S2048 54 -> 46 us, B1 S2048 34 either way, B1 S1024 19 vs 25 us
-  // (profiles/r3_prefill_kv8.md).
+  // small_mode 0 (auto) takes the head split while it can also split the keys 4 ways
+  // (grids below 64 workgroups) and the 8-wave split-KV from 64 on: B1 S4096 Hq8/Hkv1
+  // 98 -> 76 us, B2 S2048 54 -> 46 us, B1 S1024 17 vs 22 us (profiles/r3_prefill_kv8.md);
+  // B1 S2048 (64 items) 32.8 -> 31.0 us kernel time (profiles/r4_prefill_small_grid.md).
   const int wg0 = num_work * Hkv;
   const bool small = nw == 8 && wg0 < hsplit_below && ws != nullptr && tickets != nullptr;
   const bool kv8 = small && (small_mode == 2 ||
-                             (small_mode == 0 && wg0 * 4 > kPrefillSplitMaxWg &&
+                             (small_mode == 0 && wg0 * 4 >= kPrefillSplitMaxWg &&
                               wg0 * 2 <= kPrefillSplitMaxWg));
   if (kv8) {
     const int wg = wg0;
@@ -504,7 +552,8 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
     attn_prefill_kernel<8><<<grid8, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                    bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                    work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                   scale_log2, 1, kvsplit, ws, tickets);
+                                                   scale_log2, 1, kvsplit, ws, tickets,
+                                                   g_prefill_ts);
     return;
   }
   if (nw == 8 && G == 8 && num_work * Hkv < hsplit_below) {
@@ -522,7 +571,8 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
     attn_prefill_kernel<4><<<grid2, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                    bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                    work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                   scale_log2, 2, kvsplit, ws, tickets);
+                                                   scale_log2, 2, kvsplit, ws, tickets,
+                                                   g_prefill_ts);
     return;
   }
   dim3 grid(num_work * Hkv);
@@ -530,12 +580,14 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
     attn_prefill_kernel<8><<<grid, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                  scale_log2, 1);
+                                                  scale_log2, 1, 1, nullptr, nullptr,
+                                                  g_prefill_ts);
   else
     attn_prefill_kernel<4><<<grid, 256, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
-                                                  scale_log2, 1);
+                                                  scale_log2, 1, 1, nullptr, nullptr,
+                                                  g_prefill_ts);
 }
 
 }  // namespace rfq

@@ -23,6 +23,7 @@ with ``status`` set, and a model phase frees its engine before the next starts.
 from __future__ import annotations
 
 import gc
+import logging
 import os
 import statistics
 import threading
@@ -262,10 +263,44 @@ def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt
     out_q.put(asyncio.run(_open_loop(url, sched, t0, deadline)))
 
 
+def _api_server_proc(cfg_dict: dict, inq, outq, parse_procs: int, port_q, stop_evt) -> None:
+    """The service's API process with the engine in another process (the service's
+    RFQ_ENGINE_PROCESS=1 layout): uvicorn + the FastAPI app, HTTP parsing, attachment
+    parsing (its parser pool), chat template + tokenisation and the G9-G12 validation
+    here; requests go to the engine loop over (inq, outq) through an attached
+    DPRouter.  Reports its port on ``port_q``, then serves until ``stop_evt``."""
+    import uvicorn
+
+    from ..api import main as api
+    from ..engine.router import DPRouter
+    from ..service.extract import ExtractService
+    from ..utils.config import EngineConfig
+
+    logging.getLogger("replisense_rfq_amd").setLevel(logging.WARNING)
+    os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
+    router = DPRouter(EngineConfig(**cfg_dict), 1, queues=(inq, outq))
+    api.provide_generator(ExtractService(router.backend()))
+    port = _free_port()
+    server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
+                                           log_level="warning", access_log=False,
+                                           backlog=4096))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    t0 = time.time()
+    while not server.started and time.time() - t0 < 60 and th.is_alive():
+        time.sleep(0.05)
+    port_q.put(port if server.started else None)
+    while th.is_alive() and not stop_evt.wait(0.2):
+        pass
+    server.should_exit = True                   # lifespan exit closes the parser pool
+    th.join(timeout=15)
+    router._stop = True
+
+
 def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: float = 40.0,
                          upload_share: float = 0.25, client_procs: int = 8,
                          parse_procs: int = 4, budget_s: float = 120.0, seed: int = 0,
-                         burst_depth: int = 0) -> dict:
+                         burst_depth: int = 0, api_process: bool = True) -> dict:
     """does the HTTP surface sustain the engine's throughput?
 
     uvicorn + the FastAPI app (api/main.py, the reference's app/main.py:205-344
@@ -277,46 +312,67 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
     rises only slowly with its depth, so a Poisson stream started on an empty engine
     needs minutes to reach its steady queue; the burst starts it near that depth).
     After ``warm_s`` of ramp-up, the window of ``measure_s`` reports the documents
-    completed per second (every one validated by the service and enveloped), the
-    latency of the requests sent inside the window, the engine's in-flight depth
-    (running + waiting, sampled every 0.5 s) and timeouts / errors."""
-    import multiprocessing as mp
+    completed and validated per second (each one validated by the service and
+    enveloped), the latency of the requests sent inside the window, the engine's
+    in-flight depth (running + waiting, sampled every 0.5 s) and timeouts / errors.
 
-    import uvicorn
+    ``api_process`` (default): the service's RFQ_ENGINE_PROCESS=1 layout -- the API
+    runs in its own spawned process (``_api_server_proc``) and reaches this process's
+    engine loop (engine/router.py ``serve_loop``) over two queues, so HTTP, parsing,
+    tokenisation and validation never take the engine thread's GIL.  False: uvicorn in
+    a thread of this process on AsyncEngine (the in-process default)."""
+    import multiprocessing as mp
 
     from ..api import main as api
     from ..engine.engine import AsyncEngine
+    from ..engine.router import serve_loop
     from ..service.extract import EngineBackend, ExtractService
 
     t_start = time.perf_counter()
     res = {"config": "open-loop Poisson arrivals, /parse-text/ + /upload/ through uvicorn",
+           "layout": "api process + engine process" if api_process else "one process",
            "offered_rate": round(rate, 2), "upload_share": upload_share,
            "warm_s": warm_s, "measure_s": measure_s, "status": "running"}
-    import logging
-
     pkg_log = logging.getLogger("replisense_rfq_amd")
     level0 = pkg_log.level
     pkg_log.setLevel(logging.WARNING)
     hints0 = engine.cfg.decode_hints
     engine.cfg.decode_hints = True
-    aeng = AsyncEngine(engine)
-    api.provide_generator(ExtractService(EngineBackend(engine, aeng)))
-    os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
-    port = _free_port()
-    server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
-                                           log_level="warning", access_log=False,
-                                           backlog=4096))
-    th = threading.Thread(target=server.run, name="bench-uvicorn-open", daemon=True)
-    th.start()
-    procs = []
+    ctx = mp.get_context("spawn")
+    procs, aeng, server, th, api_proc, eng_th, inq = [], None, None, None, None, None, None
     try:
-        t0 = time.time()
-        while not server.started and time.time() - t0 < 60 and th.is_alive():
-            time.sleep(0.05)
-        if not server.started:
-            raise RuntimeError("uvicorn did not start")
+        if api_process:
+            inq, outq, port_q, api_stop = ctx.Queue(), ctx.Queue(), ctx.Queue(), ctx.Event()
+            api_proc = ctx.Process(target=_api_server_proc,
+                                   args=(engine.cfg.to_dict(), inq, outq, parse_procs, port_q,
+                                         api_stop),
+                                   daemon=False)
+            api_proc.start()
+            eng_th = threading.Thread(target=serve_loop, args=(engine, inq, outq),
+                                      kwargs={"shutdown_engine": False},
+                                      name="bench-engine-loop", daemon=True)
+            eng_th.start()
+            port = port_q.get(timeout=180)
+            if port is None:
+                raise RuntimeError("API process: uvicorn did not start")
+        else:
+            import uvicorn
+
+            aeng = AsyncEngine(engine)
+            api.provide_generator(ExtractService(EngineBackend(engine, aeng)))
+            os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
+            port = _free_port()
+            server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
+                                                   log_level="warning", access_log=False,
+                                                   backlog=4096))
+            th = threading.Thread(target=server.run, name="bench-uvicorn-open", daemon=True)
+            th.start()
+            t0 = time.time()
+            while not server.started and time.time() - t0 < 60 and th.is_alive():
+                time.sleep(0.05)
+            if not server.started:
+                raise RuntimeError("uvicorn did not start")
         url = f"http://127.0.0.1:{port}"
-        ctx = mp.get_context("spawn")
         dur = warm_s + measure_s
         deadline = time.time() + max(dur + 10.0, budget_s - (time.perf_counter() - t_start))
         start_evt, out_q = ctx.Event(), ctx.Queue()
@@ -350,8 +406,9 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
         sent_in = [r for r in recs if lo <= r[0] < hi]
         ok = sum(r[3] for r in done_in)
         win_depth = [d for t, d in depth if lo <= t < hi]
-        res.update(requests=len(recs), docs=len(done_in),
-                   docs_per_s=round(len(done_in) / measure_s, 3),
+        # docs = responses completed in the window whose extraction validated
+        res.update(requests=len(recs), docs=ok, responses=len(done_in),
+                   docs_per_s=round(ok / measure_s, 3),
                    valid=round(ok / max(1, len(done_in)), 3),
                    http_latency_s=pcts([r[2] for r in sent_in]),
                    failed=sum(not r[3] for r in recs),
@@ -366,13 +423,26 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
         for p in procs:
             if p.is_alive():
                 p.kill()
-        server.should_exit = True
-        th.join(timeout=15)
-        aeng.shutdown()
-        api.provide_generator(None)
-        if api.parser is not None:
-            api.parser.close()
-        api.parser = api.field_generator = None
+        if api_proc is not None:
+            api_stop.set()
+            api_proc.join(timeout=30)
+            if api_proc.is_alive():
+                api_proc.terminate()
+                api_proc.join(timeout=10)
+            if api_proc.is_alive():
+                api_proc.kill()
+        if eng_th is not None:
+            inq.put(None)                       # ends serve_loop; the engine stays up
+            eng_th.join(timeout=60)
+        if server is not None:
+            server.should_exit = True
+            th.join(timeout=15)
+        if aeng is not None:
+            aeng.shutdown()
+            api.provide_generator(None)
+            if api.parser is not None:
+                api.parser.close()
+            api.parser = api.field_generator = None
         engine.cfg.decode_hints = hints0
         pkg_log.setLevel(level0)
         if engine.has_work():

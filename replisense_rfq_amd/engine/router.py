@@ -75,8 +75,6 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
     from ..utils.config import EngineConfig
     from ..utils.faults import FaultInjector
     from .engine import LLMEngine
-    from ..utils.faults import CustomAllReduceError
-    from .sequence import SamplingParams
 
     cfg = EngineConfig(**cfg_dict)
     eng = LLMEngine(cfg, tp=ctx)
@@ -85,6 +83,19 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
     short_gil_switch()                         # the inbox feeder thread shares the GIL
     exit_after = FaultInjector().replica_exit_after()
     outq.put(("ready", idx, None))
+    serve_loop(eng, inq, outq, idx, exit_after)
+
+
+def serve_loop(eng, inq, outq, idx: int = 0, exit_after=None,
+               shutdown_engine: bool = True) -> None:
+    """The engine side of the request queues: admit (rid, prompt, params) messages
+    (also while a step runs on the device), step, and answer ("done", rid, result).
+    Runs a replica worker process's engine (``_worker``) or, with
+    ``shutdown_engine=False``, an engine that outlives the loop (the bench's
+    separate-process HTTP phase).  A ``None`` message ends the loop."""
+    from ..utils.faults import CustomAllReduceError
+    from .sequence import SamplingParams
+
     pending = {}
     served = 0
     held = []                                  # inbox messages deferred to the loop top
@@ -137,7 +148,9 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
                                                    "span": {}}))
                     continue
                 if not alive:
-                    eng.shutdown()                 # release the TP followers
+                    if shutdown_engine:
+                        eng.shutdown()             # release the TP followers
+                    eng.runner.busy_hook = None
                     return
         except queue.Empty:
             pass
@@ -170,7 +183,10 @@ def _worker(idx: int, devices: str, cfg_dict: dict, inq, outq, tp: int = 1, port
 
 class DPRouter:
     def __init__(self, cfg, n_replicas: int, devices_per_replica: int = 1,
-                 restart: bool = True):
+                 restart: bool = True, queues=None):
+        """``queues`` = (inq, outq): attach to ONE engine loop that another process
+        already runs (``serve_loop``) instead of spawning replicas; it is taken as
+        ready and is never restarted."""
         self.cfg = cfg
         self.n = n_replicas
         self.dpr = devices_per_replica
@@ -193,7 +209,13 @@ class DPRouter:
         self._lock = threading.Lock()
         self._cfg_dict = dict(cfg.to_dict())
         self._cfg_dict["dp"] = 1
-        for i in range(n_replicas):
+        if queues is not None:
+            if n_replicas != 1:
+                raise ValueError("attached queues serve exactly one replica")
+            self.inqs[0], self.outq = queues
+            self.ready[0] = True
+            self.restart = False
+        for i in range(n_replicas if queues is None else 0):
             self._spawn(i)
         deadline = time.time() + 1800
         while not all(self.ready) and time.time() < deadline:
@@ -379,9 +401,19 @@ class RouterBackend:
 def maybe_router(cfg):
     """A DPRouter when RFQ_DP > 1 or RFQ_TP > 1 (replicas of cfg.tp processes/devices
     each) or when the single engine should live in its own process
-    (RFQ_ENGINE_PROCESS=1: the API process then only parses HTTP, tokenises and
-    validates), else None."""
-    own_process = os.environ.get("RFQ_ENGINE_PROCESS", "0").lower() in ("1", "true", "on")
+    (RFQ_ENGINE_PROCESS: the API process then only parses HTTP, tokenises and
+    validates), else None.  RFQ_ENGINE_PROCESS defaults to "auto" = on for a GPU engine:
+    with the API in the engine's process its Python (HTTP, parsing, chat template,
+    validation) shares the engine thread's GIL and the service delivered 0.86x the
+    engine's docs/s; in two processes 1.01x (profiles/r4_http_open_loop.md)."""
+    v = os.environ.get("RFQ_ENGINE_PROCESS", "auto").lower()
+    dev = cfg.device
+    if dev == "auto":
+        import torch
+
+        # device_count() does not initialise HIP in this (API) process
+        dev = "cuda" if torch.cuda.device_count() > 0 else "cpu"
+    own_process = v in ("1", "true", "on") or (v == "auto" and dev != "cpu")
     if cfg.dp <= 1 and cfg.tp <= 1 and not own_process:
         return None
     return DPRouter(cfg, max(1, cfg.dp), max(1, cfg.tp))

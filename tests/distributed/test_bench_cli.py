@@ -198,6 +198,7 @@ def test_bench_extra_phases_cpu():
     assert o["status"] == "ok", o
     assert o["offered_rate"] == 3 and o["requests"] > 0 and o["failed"] == 0, o
     assert o["burst_depth"] == 3 and o["engine_depth"] is not None
+    assert o["layout"] == "api process + engine process" and o["responses"] >= o["docs"]
     assert o["docs_per_s"] > 0 and o["valid"] == 1.0 and o["http_latency_s"]["p50"] > 0
     assert o["http_vs_engine"] > 0
     h = ph["http_upload"]
@@ -243,7 +244,14 @@ def test_http_phase_releases_the_engine():
     assert res["status"] == "ok", res
     wr = weakref.ref(eng)
     del eng
-    gc.collect()
+    import time
+
+    t_end = time.time() + 10.0        # the server / parser threads wind down asynchronously
+    while True:
+        gc.collect()
+        if wr() is None or time.time() > t_end:
+            break
+        time.sleep(0.2)
     assert wr() is None, [type(r).__name__ for r in gc.get_referrers(wr())]
 
 

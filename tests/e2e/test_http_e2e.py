@@ -95,11 +95,12 @@ def test_http_mock_backend():
 
 @pytest.mark.gpu
 def test_http_engine_backend(gpu):
-    """The service default: REFERENCE grammar profile, no decoding hints (random
+    """The in-process layout (RFQ_ENGINE_PROCESS=0; the GPU default is the engine in
+    its own process, below): REFERENCE grammar profile, no decoding hints (random
     weights then fill strings until the token-budget close-out): every response is
     the reference's success envelope (validated or fallback dict)."""
     proc, url = _serve({"RFQ_BACKEND": "engine", "RFQ_MODEL": "tiny-llama", "RFQ_MAX_BATCH": "16",
-                        "RFQ_KV_FRACTION": "0.05"})
+                        "RFQ_KV_FRACTION": "0.05", "RFQ_ENGINE_PROCESS": "0"})
     try:
         outs = _exercise(url, n=12, validate=False)
         assert all(o["success"] for o in outs)
@@ -109,11 +110,10 @@ def test_http_engine_backend(gpu):
 
 @pytest.mark.gpu
 def test_http_engine_process_router(gpu):
-    """The router spawn path on the GPU: the engine in its own process
-    (RFQ_ENGINE_PROCESS=1), pinned through HIP_VISIBLE_DEVICES."""
+    """The router spawn path on the GPU, the service default there: the engine in its
+    own process (RFQ_ENGINE_PROCESS=auto), pinned through HIP_VISIBLE_DEVICES."""
     proc, url = _serve({"RFQ_BACKEND": "engine", "RFQ_MODEL": "tiny-llama", "RFQ_MAX_BATCH": "16",
-                        "RFQ_KV_FRACTION": "0.05", "RFQ_ENGINE_PROCESS": "1",
-                        "RFQ_DECODE_HINTS": "1"})
+                        "RFQ_KV_FRACTION": "0.05", "RFQ_DECODE_HINTS": "1"})
     try:
         outs = _exercise(url, n=8)
         assert all(o["success"] for o in outs)

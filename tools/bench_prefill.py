@@ -34,8 +34,10 @@ def run(B, S, Hq, Hkv, iters=10):
     wq = torch.arange(nqb, dtype=torch.int32, device=dev).repeat(B)
     hs = int(os.environ["HSPLIT"]) if "HSPLIT" in os.environ else None
     kvs = os.environ["KVSPLIT"] != "0" if "KVSPLIT" in os.environ else None
+    sm = int(os.environ["SMALL"]) if "SMALL" in os.environ else None
     f = lambda: ops.attn_prefill(q, k, v, bt, qs, ql, kvl, ws, wq, out, Hq, Hkv,  # noqa: E731
-                                 1 / math.sqrt(128), qblk, hsplit_below=hs, kvsplit=kvs)
+                                 1 / math.sqrt(128), qblk, hsplit_below=hs, kvsplit=kvs,
+                                 small_mode=sm)
     f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,10 +60,17 @@ def run(B, S, Hq, Hkv, iters=10):
     return us, flops / us / 1e6
 
 
+SHAPES = [(1, 2048, 32, 8), (4, 2048, 32, 8), (1, 2048, 8, 1), (8, 2048, 8, 1),
+          (16, 512, 32, 8), (1, 8192, 32, 8), (1, 1024, 8, 1), (1, 4096, 8, 1), (2, 2048, 8, 1)]
+
+
 def main():
-    for B, S, Hq, Hkv in [(1, 2048, 32, 8), (4, 2048, 32, 8), (1, 2048, 8, 1), (8, 2048, 8, 1),
-                          (16, 512, 32, 8), (1, 8192, 32, 8), (1, 1024, 8, 1), (1, 4096, 8, 1),
-                          (2, 2048, 8, 1)]:
+    # SHAPES=BxSxHqxHkv,...  (env) overrides the default list; HSPLIT / KVSPLIT / SMALL
+    # pick the small-grid forms (ops.attn_prefill)
+    shapes = SHAPES
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["SHAPES"].split(",")]
+    for B, S, Hq, Hkv in shapes:
         us, tf = run(B, S, Hq, Hkv)
         print(json.dumps({"B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "us": round(us, 1),
                           "TFLOPs": round(tf, 1), "pct_of_2.5PF": round(tf / 25.0, 1)}),
