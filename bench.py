@@ -355,6 +355,7 @@ def main():
     if stream is not None:
         stream.clear_window()
     steps0 = engine.num_steps
+    gsteps0 = engine.stats().get("graph_steps", 0)
     host0 = _host_timers(engine)
     barrier()
     sync()
@@ -365,6 +366,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     steps_timed = engine.num_steps - steps0
+    gsteps_timed = engine.stats().get("graph_steps", 0) - gsteps0
     host = {k: round(v - host0[k], 3) for k, v in _host_timers(engine).items()}
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=engine.device if on_gpu else "cpu")
@@ -426,7 +428,12 @@ def main():
                        "in_flight_per_replica": args.max_num_seqs,
                        "temperature": cfg.temperature, "grammar": cfg.grammar,
                        "profile": "synthetic", "decode_hints": True,
-                       "jump_forward": cfg.jump_forward, "graphs": cfg.use_graphs,
+                       "jump_forward": cfg.jump_forward,
+                       # hipGraphs are captured for decode-only steps of up to the largest
+                       # bucket of sequences; the count says how many timed steps used one
+                       "graphs": (f"{gsteps_timed} of {steps_timed} timed steps (captured for "
+                                  f"decode-only steps <= {max(cfg.graph_buckets)} sequences)"
+                                  if cfg.use_graphs else "off"),
                        # prompts built + tokenised in a spawned process (benchmarks.stream)
                        "producer": os.environ.get("RFQ_BENCH_PRODUCER", "process"),
                        "admit": ("during step" if os.environ.get("RFQ_BENCH_OVERLAP_ADMIT", "1")

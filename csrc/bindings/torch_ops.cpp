@@ -974,6 +974,9 @@ void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu
   TORCH_CHECK(w.size(1) == K && K % 64 == 0 && K >= 64, "gemm_dense: w [N, K], K % 64 == 0");
   TORCH_CHECK(!(cfg & 4) || (K % 128 == 0 && w.size(0) % 16 == 0 && w.is_contiguous()),
               "gemm_dense: the decode-tiled weight layout (cfg bit 2) needs K % 128 == 0");
+  TORCH_CHECK(!(cfg & 8) || (K % 128 == 0 && !(cfg & 4)),
+              "gemm_dense: the one-wave-per-SIMD kernel (cfg bit 3) needs K % 128 == 0 and a "
+              "row-major weight");
   TORCH_CHECK(swiglu ? (N % 256 == 0) : (N % 256 == 0),
               "gemm_dense: N % 256 == 0 (2F with F % 128 == 0 for swiglu)");
   TORCH_CHECK(out.size(0) == M && out.size(1) == n_out, "gemm_dense: out shape");

@@ -441,6 +441,9 @@ __global__ __launch_bounds__(512) void gemm_dense_kernel(
   }
 }
 
+void launch_gemm_w4(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int, int,
+                    int, int, bool, int, hipStream_t);
+
 // out = x w^T ([M, N]) or, swiglu, act = silu(x Wg^T) * (x Wu^T) ([M, F], w = [2F, K],
 // up rows at up_off = F).  n_out = N or F.
 void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, bf16_t* out,
@@ -450,6 +453,13 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   const int tiles_m = (M + kGM - 1) / kGM;
   const int tiles_n = swiglu ? n_out / 128 : n_out / kGN;
   const int grid = tiles_m * tiles_n;
+  // cfg bit 3: the one-wave-per-SIMD kernel (gemm_w4.hip; K % 128 == 0); with bits 4-6
+  // its diagnostic timing builds (WRONG results): 16 no DMA, 32 no fragment reads, 64 no
+  // waits / barriers in the K loop
+  if (cfg & 8) {
+    launch_gemm_w4(x, ldx, w, ldw, out, ldo, M, n_out, K, up_off, swiglu, (cfg >> 4) & 7, s);
+    return;
+  }
   // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile;
   // bit 2: w in the decode-tiled layout (16x16x32, 2 phases)
 #define RFQ_GD_LAUNCH(E, F, P) \

@@ -1,0 +1,304 @@
+// Dense large-M projection GEMM, one wave per SIMD (the throughput path's hipBLASLt
+// replacement candidate; SURVEY.md §2.4 K3/K8/K9/K11, K10 SwiGLU in the epilogue):
+//
+//   out[M, N] = x[M, K] . w[N, K]^T                         (kW4Store)
+//   act[M, F] = silu(x . Wg^T) * (x . Wu^T), w = [Wg; Wu]    (kW4Swiglu, up rows at up_off)
+//
+// gemm_dense.hip's 8-wave ping-pong parks a quarter of its wave cycles at barriers and
+// tops out at 1.67 PF/s with no memory traffic at all (profiles/r3_gemm_dense.md).  This
+// kernel is the other structure: 4 waves per 256 x 256 tile, each wave alone on its SIMD
+// with a 128 x 128 quadrant of the output in 64 16x16 fp32 accumulators (256 registers,
+// AGPRs), so nothing but its own instruction stream competes for the SIMD, and one
+// barrier per 32-deep K-step.
+//
+//  * K-step = 32.  LDS: 4 stages x {W image, X image} of [256 rows][32 k] bf16 (16 KB
+//    each, 128 KB).  Row rho's 16-byte chunk c sits at chunk c ^ ((rho >> 2) & 3): the 16
+//    lanes of a ds_read_b128 quarter (16 rows, one chunk) hit 16 distinct 4-bank groups.
+//    LDS-DMA (global_load_lds_dwordx4) writes lane-linearly, so the swizzle is applied
+//    to the per-lane source column.
+//  * Step t: wait for stage t+1's DMA (own pieces: vmcnt leaving step t+2's 8 pieces in
+//    flight), one barrier (every wave's pieces landed; every wave has consumed the
+//    stage that step t+3's DMA overwrites), then 16 groups of [one ds_read_b128 of step
+//    t+1's fragments, one DMA piece of step t+3 (first 8 groups), four MFMAs of step t on
+//    the fragments read during step t-1].  The DMA runs 2 steps (128 MFMAs per wave)
+//    ahead of its first reader; the fragment reads one step.
+//  * Fragment reads are inline-asm ds_read_b128 with an lgkmcnt(0) at the top of the
+//    next step tied to the destination registers (through the builtin the compiler
+//    guards LDS reads with vmcnt(0) against the in-flight DMA: it cannot tell the
+//    stages apart, and that would drain the prefetch every step).
+//  * MFMA operands are swapped (C^T = W X^T, as gemm_dense): a lane holds 4 consecutive
+//    output columns of one row (8-byte stores), and with SwiGLU the wave's W rows are 64
+//    gate + the matching 64 up rows, so gate and up of an output meet in one lane.
+//  * Block order: bijective XCD remap, then groups of 16 row-tiles swept w-tile by
+//    w-tile (blocks sharing a weight panel run together on one XCD's L2).
+// Shapes: K % 128 == 0, N % 256 == 0 (F % 128 with SwiGLU), any M >= 1 (rows past M read
+// row M-1 and are not stored), 16-byte aligned rows.
+#include <type_traits>
+
+#include "common.h"
+
+namespace rfq {
+
+constexpr int kW4M = 256, kW4N = 256, kW4K = 64;
+constexpr int kW4Stages = 2;
+constexpr int kW4Img = 256 * kW4K;                 // bf16 elements per operand image
+constexpr int kW4StageB = 2 * kW4Img * 2;          // bytes per stage (W then X)
+constexpr int kW4Lds = kW4Stages * kW4StageB;      // 128 KB
+constexpr int kW4GroupM = 16;
+
+enum : int { kW4Store = 0, kW4Swiglu = 1 };
+
+typedef __attribute__((address_space(3))) char w4_lds_c;
+
+#define W4_READ(DST, ADDR, OFF) \
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(DST) : "v"(ADDR), "i"(OFF))
+
+// ABL (diagnostic timing builds, WRONG results): 1 = no DMA in the K loop, 2 = no
+// fragment reads in the K loop (registers kept live), 4 = no vmcnt wait / barrier.
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
+                    int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
+                    int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem_w4[];
+  w4_lds_c* const lds = (w4_lds_c*)smem_w4;
+
+  // ---- block -> (row tile, weight tile): bijective XCD remap, then L2 groups
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
+  const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+  const int per_group = kW4GroupM * tiles_n;
+  const int gid = wg / per_group, first_m = gid * kW4GroupM;
+  const int gm = min(tiles_m - first_m, kW4GroupM);
+  const int rin = wg - gid * per_group;
+  const int tm = first_m + rin % gm, tn = rin / gm;
+  const int row0 = tm * kW4M;
+  const int m_valid = min(M - row0, kW4M);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int rr = lane & 15, kq = lane >> 4;
+
+  // ---- DMA: per 64-deep K-tile a stage holds the W image (256 rows x 128 B, 32 pieces
+  // of 8 rows) and the X image (32 pieces); wave wid issues W pieces 8 wid + q and X
+  // pieces 8 wid + q (q = 0..7).  Lane -> image row 8 p + lane / 8, physical chunk lane & 7,
+  // source chunk (lane & 7) ^ ((row >> 1) & 7).  buffer_load ... lds with the per-piece
+  // row offset and the K-tile offset in SGPRs: one VGPR offset per lane for W, one per
+  // X piece (rows past M are clamped to row M-1).
+  const int lrow = lane >> 3, lch = lane & 7;
+  const int lsw = lch ^ ((lrow >> 1) & 7);          // same for rows 8p + lrow (8p even)
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(x + (int64_t)row0 * ldx), (short)0, 0x7fffffff, 0x00020000);
+  const int w_voff = (lrow * (int)ldw + 8 * lsw) * 2;
+  int x_voff[8], w_soff[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int p = 8 * wid + q;                      // piece 0..31 of each image
+    x_voff[q] = (min(8 * p + lrow, m_valid - 1) * (int)ldx + 8 * lsw) * 2;
+    int n0;                                         // W row of the piece's first image row
+    if constexpr (EPI == kW4Swiglu) {
+      const int i = (p >> 1) & 7, wc = p >> 4;      // image row 8p = 128 wc + 16 i + 8 (p & 1)
+      n0 = (i < 4 ? 0 : up_off) + tn * 128 + 64 * wc + 16 * (i & 3) + 8 * (p & 1);
+    } else {
+      n0 = tn * kW4N + 8 * p;
+    }
+    w_soff[q] = __builtin_amdgcn_readfirstlane(n0 * (int)ldw * 2);
+  }
+  auto dma = [&](int q, int stage, int k0) {        // k0: element offset of the K-tile
+    w4_lds_c* const st = lds + stage * kW4StageB;
+    const int p = 8 * wid + q;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(st + p * 1024), 16, w_voff,
+                                             w_soff[q] + 2 * k0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(st + kW4Img * 2 + p * 1024), 16,
+                                             x_voff[q], 2 * k0, 0, 0);
+  };
+
+  // ---- fragment addresses: W subtile i = image rows 128 wn + 16 i + rr, X subtile j =
+  // rows 128 wm + 16 j + rr; k-half h reads chunk 4 h + kq at (4 h + kq) ^ ((rr >> 1) & 7);
+  // subtile steps of 2 KB are ds_read immediates
+  const int sw = (rr >> 1) & 7;
+  const int lo0 = rr * 128 + 16 * (kq ^ sw), lo1 = rr * 128 + 16 * ((4 + kq) ^ sw);
+  const int wo = 16384 * wn, xo = kW4Img * 2 + 16384 * wm;
+
+  f32x4 acc[8][8];                                  // [W subtile i][X subtile j]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  s16x8 f0[16], f1[16];      // fragments of k-half 0 / 1 of a K-tile: [0..7] W_i, [8..15] X_j
+
+  // every fragment read issued so far has landed; the operands tie the registers to the
+  // wait so no MFMA reading them is scheduled above it
+  auto wait_frags = [&](s16x8 (&f)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]),
+                   "+v"(f[6]), "+v"(f[7]), "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]),
+                   "+v"(f[12]), "+v"(f[13]), "+v"(f[14]), "+v"(f[15]));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // One k-half: 64 MFMAs on `cur`, 16 fragment reads into `nxt` (k-half NH of the K-tile
+  // in stage RS), and (DM) the 16 DMA pieces of K-tile k3 into stage S3, two per group in
+  // the first 8 groups.
+  auto half = [&](s16x8 (&cur)[16], s16x8 (&nxt)[16], auto RD, auto NH, int rs, auto DM,
+                  int s3, int k3) {
+    constexpr bool rd = decltype(RD)::value, dm = decltype(DM)::value;
+    constexpr int nh = decltype(NH)::value;
+    w4_lds_c* const pw = lds + rs * kW4StageB + wo + (nh ? lo1 : lo0);
+    w4_lds_c* const px = lds + rs * kW4StageB + xo + (nh ? lo1 : lo0);
+#define W4_GROUP(G)                                                                       \
+    {                                                                                     \
+      if constexpr (rd && !(ABL & 2)) {                                                   \
+        if constexpr ((G) < 8) W4_READ(nxt[G], pw, 2048 * ((G) & 7));                     \
+        else W4_READ(nxt[G], px, 2048 * ((G) & 7));                                       \
+      }                                                                                   \
+      if constexpr (rd && (ABL & 2)) asm volatile("" : "+v"(nxt[G]));                     \
+      if constexpr ((G) < 8 && dm && !(ABL & 1)) dma(G, s3, k3);                          \
+      _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                                  \
+        const int i = (G) >> 1, j = ((G) & 1) * 4 + jj;                                   \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),            \
+                                                            as_bf16x8(cur[8 + j]),        \
+                                                            acc[i][j], 0, 0, 0);          \
+      }                                                                                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+    }
+    W4_GROUP(0) W4_GROUP(1) W4_GROUP(2) W4_GROUP(3) W4_GROUP(4) W4_GROUP(5) W4_GROUP(6)
+    W4_GROUP(7) W4_GROUP(8) W4_GROUP(9) W4_GROUP(10) W4_GROUP(11) W4_GROUP(12) W4_GROUP(13)
+    W4_GROUP(14) W4_GROUP(15)
+#undef W4_GROUP
+  };
+  // the boundary inside K-tile t: K-tile t+1's DMA (own pieces) landed, k-half 1's
+  // fragments landed, one barrier (every wave: the same, and done reading stage t's
+  // image, which K-tile t+2's DMA overwrites next)
+  auto mid = [&]() {
+    if constexpr (!(ABL & 4)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_frags(f1);
+      __builtin_amdgcn_s_barrier();
+    } else {
+      wait_frags(f1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  const int nk = K / 64;
+  // ---- prologue: K-tiles 0 and 1 in flight, tile 0 landed, its k-half 0 read
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma(q, 0, 0);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(q, 1, 64);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    w4_lds_c* const pw = lds + wo + lo0;
+    w4_lds_c* const px = lds + xo + lo0;
+    W4_READ(f0[0], pw, 0);     W4_READ(f0[1], pw, 2048);  W4_READ(f0[2], pw, 4096);
+    W4_READ(f0[3], pw, 6144);  W4_READ(f0[4], pw, 8192);  W4_READ(f0[5], pw, 10240);
+    W4_READ(f0[6], pw, 12288); W4_READ(f0[7], pw, 14336);
+    W4_READ(f0[8], px, 0);     W4_READ(f0[9], px, 2048);  W4_READ(f0[10], px, 4096);
+    W4_READ(f0[11], px, 6144); W4_READ(f0[12], px, 8192); W4_READ(f0[13], px, 10240);
+    W4_READ(f0[14], px, 12288); W4_READ(f0[15], px, 14336);
+  }
+
+  // ---- K-tile t: half 0 (MFMAs on f0, reads of half 1 into f1, same stage), the
+  // boundary, half 1 (MFMAs on f1, reads of K-tile t+1's half 0 into f0, DMA of t+2
+  // into this stage)
+  int t = 0;
+  for (; t + 2 < nk; ++t) {
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0);
+    mid();
+    half(f1, f0, T_{}, H0{}, (t + 1) & 1, T_{}, t & 1, (t + 2) * 64);
+  }
+  // the last two K-tiles (nk is even): no more DMA
+  wait_frags(f0);
+  half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0);
+  mid();
+  half(f1, f0, T_{}, H0{}, (t + 1) & 1, F_{}, 0, 0);
+  wait_frags(f0);
+  half(f0, f1, T_{}, H1{}, (t + 1) & 1, F_{}, 0, 0);
+  mid();
+  half(f1, f0, F_{}, H0{}, 0, F_{}, 0, 0);
+
+  // ---- epilogue.  Lane holds out[row0 + 128 wm + 16 j + rr][n0 + 16 i + 4 kq + 0..3]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int trow = 128 * wm + 16 * j + rr;
+    if (trow >= m_valid) continue;
+    bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
+    if constexpr (EPI == kW4Swiglu) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float gf = bf2f(f2bf(acc[i][j][u]));          // = the gate GEMM's bf16
+          const float sg = gf / (1.f + __expf(-gf));
+          o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + i][j][u]));
+        }
+        uint2 v;
+        v.x = pack_bf16x2(o[0], o[1]);
+        v.y = pack_bf16x2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(orow + tn * 128 + 64 * wn + 16 * i + 4 * kq) = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint2 v;
+        v.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(orow + tn * kW4N + 128 * wn + 16 * i + 4 * kq) = v;
+      }
+    }
+  }
+}
+#undef W4_READ
+
+// out = x w^T ([M, N]) or, swiglu, act = silu(x Wg^T) * (x Wu^T) ([M, F], w = [2F, K], up
+// rows at up_off = F).  n_out = N or F.
+void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, bf16_t* out,
+                    int64_t ldo, int M, int n_out, int K, int up_off, bool swiglu, int abl,
+                    hipStream_t s) {
+  if (M <= 0) return;
+  const int tiles_m = (M + kW4M - 1) / kW4M;
+  const int tiles_n = swiglu ? n_out / 128 : n_out / kW4N;
+  const int grid = tiles_m * tiles_n;
+  if (abl && !swiglu) {
+#define W4_ABL(A)                                                                       \
+  gemm_w4_kernel<kW4Store, A><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, \
+                                                        up_off, tiles_m, tiles_n)
+    switch (abl) {
+      case 1: W4_ABL(1); break;
+      case 2: W4_ABL(2); break;
+      case 3: W4_ABL(3); break;
+      case 4: W4_ABL(4); break;
+      case 5: W4_ABL(5); break;
+      case 6: W4_ABL(6); break;
+      default: W4_ABL(7); break;
+    }
+#undef W4_ABL
+    return;
+  }
+  if (swiglu)
+    gemm_w4_kernel<kW4Swiglu><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                        tiles_m, tiles_n);
+  else
+    gemm_w4_kernel<kW4Store><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                       tiles_m, tiles_n);
+}
+
+}  // namespace rfq

@@ -921,14 +921,19 @@ def test_skinny_gemm_short_k_tail(gpu, M, cfg, N, K):
     _close(y, x.float() @ w.float().t(), 2e-2, 1e-2, f"skinny tail M={M} cfg={cfg} K={K}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 128), (256, 768, 1024),
-                                   (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096)])
+                                   (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096),
+                                   (777, 2048, 512), (256, 512, 256)])
 def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
-    """The 256x256 8-wave MFMA GEMM (gemm_dense.hip) against the fp32 oracle, asymmetric
-    operands, row tails (M % 256 != 0), one-tile and many-tile K loops; swiglu vs the
-    unfused GEMM -> bf16 -> silu_mul rounding."""
+    """The 256x256 8-wave MFMA GEMM (gemm_dense.hip) and the one-wave-per-SIMD kernel
+    (cfg 8, gemm_w4.hip: K % 128 == 0) against the fp32 oracle, asymmetric operands, row
+    tails (M % 256 != 0), one-tile and many-tile K loops (K 128 / 256: only the w4
+    kernel's 4-step tail; 512: one steady iteration); swiglu vs the unfused GEMM ->
+    bf16 -> silu_mul rounding."""
+    if cfg & 8 and K % 128:
+        pytest.skip("the w4 kernel needs K % 128 == 0")
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     x = ((torch.rand(M, K, device="cuda", generator=g) * 2 - 1)).to(BF)
     w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(BF)
@@ -941,7 +946,7 @@ def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8])
 def test_gemm_dense_identity_asymmetric(gpu, cfg):
     """A = I with an asymmetric B catches a transposed C write (§3)."""
     K = 256
