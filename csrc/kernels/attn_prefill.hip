@@ -379,6 +379,13 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     // 8-byte stores drained by vmcnt(0) + barrier, a relaxed agent-scope ticket, sc1
     // loads of the partner's partial by the second arriver, which merges and writes the
     // output; it resets the ticket for the next launch.  No fences, no L2 writeback.
+    // Memory-model note: the ordering rests on the gfx950 ISA, not on a C++ release /
+    // acquire pair -- every handed-off store and load is an sc1 (device-coherent)
+    // access, the stores are retired by vmcnt(0) before the barrier that precedes the
+    // ticket, and the ticket is an L2 atomic.  An acq_rel agent-scope ticket would
+    // compile to an L2 writeback + invalidate (buffer_wbl2 / buffer_inv), several µs
+    // per split; gemv_core.h's split-K ticket relies on the same three facts.  The
+    // GPU tests exercise every split form four times per case.
     typedef __attribute__((address_space(1))) unsigned long long gu64;
     constexpr int kPart = 64 * 64 + 64 * 2;               // floats per wave
     float* mine = ws + (((int64_t)bid * kMaxKvSplit + kvs) * NW + wid) * kPart;

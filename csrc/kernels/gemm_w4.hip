@@ -44,7 +44,6 @@ constexpr int kW4Stages = 2;
 constexpr int kW4Img = 256 * kW4K;                 // bf16 elements per operand image
 constexpr int kW4StageB = 2 * kW4Img * 2;          // bytes per stage (W then X)
 constexpr int kW4Lds = kW4Stages * kW4StageB;      // 128 KB
-constexpr int kW4GroupM = 16;
 
 enum : int { kW4Store = 0, kW4Swiglu = 1 };
 
@@ -55,11 +54,15 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 
 // ABL (diagnostic timing builds, WRONG results): 1 = no DMA in the K loop, 2 = no
 // fragment reads in the K loop (registers kept live), 4 = no vmcnt wait / barrier.
-template <int EPI, int ABL = 0>
+// SPREAD: the 16 DMA pieces of half 1 go out one per MFMA group over all 16 groups (the
+// texture path takes ~16-23 cycles per 1 KB piece; two per group in the first 8 groups
+// back the wave's issue up behind it), at the cost of a shorter landing window for the
+// last pieces.
+template <int EPI, int ABL = 0, bool SPREAD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
-                    int tiles_m, int tiles_n) {
+                    int tiles_m, int tiles_n, int group_m) {
   extern __shared__ __attribute__((aligned(16))) char smem_w4[];
   w4_lds_c* const lds = (w4_lds_c*)smem_w4;
 
@@ -68,9 +71,9 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   const int bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
   const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
-  const int per_group = kW4GroupM * tiles_n;
-  const int gid = wg / per_group, first_m = gid * kW4GroupM;
-  const int gm = min(tiles_m - first_m, kW4GroupM);
+  const int per_group = group_m * tiles_n;
+  const int gid = wg / per_group, first_m = gid * group_m;
+  const int gm = min(tiles_m - first_m, group_m);
   const int rin = wg - gid * per_group;
   const int tm = first_m + rin % gm, tn = rin / gm;
   const int row0 = tm * kW4M;
@@ -88,17 +91,20 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   // row offset and the K-tile offset in SGPRs: one VGPR offset per lane for W, one per
   // X piece (rows past M are clamped to row M-1).
   const int lrow = lane >> 3, lch = lane & 7;
-  const int lsw = lch ^ ((lrow >> 1) & 7);          // same for rows 8p + lrow (8p even)
+  // source chunk of image row 8p + lrow: lch ^ (((8p + lrow) >> 1) & 7), i.e. it depends on
+  // the piece's parity (4p & 7): one W lane offset per parity
+  auto src_chunk = [&](int p) { return lch ^ (((8 * p + lrow) >> 1) & 7); };
   const __amdgpu_buffer_rsrc_t wr =
       __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(x + (int64_t)row0 * ldx), (short)0, 0x7fffffff, 0x00020000);
-  const int w_voff = (lrow * (int)ldw + 8 * lsw) * 2;
+  const int w_voff[2] = {(lrow * (int)ldw + 8 * src_chunk(0)) * 2,
+                         (lrow * (int)ldw + 8 * src_chunk(1)) * 2};
   int x_voff[8], w_soff[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int p = 8 * wid + q;                      // piece 0..31 of each image
-    x_voff[q] = (min(8 * p + lrow, m_valid - 1) * (int)ldx + 8 * lsw) * 2;
+    x_voff[q] = (min(8 * p + lrow, m_valid - 1) * (int)ldx + 8 * src_chunk(p)) * 2;
     int n0;                                         // W row of the piece's first image row
     if constexpr (EPI == kW4Swiglu) {
       const int i = (p >> 1) & 7, wc = p >> 4;      // image row 8p = 128 wc + 16 i + 8 (p & 1)
@@ -108,13 +114,19 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     }
     w_soff[q] = __builtin_amdgcn_readfirstlane(n0 * (int)ldw * 2);
   }
-  auto dma = [&](int q, int stage, int k0) {        // k0: element offset of the K-tile
+  auto dma_w = [&](int q, int stage, int k0) {      // k0: element offset of the K-tile
     w4_lds_c* const st = lds + stage * kW4StageB;
-    const int p = 8 * wid + q;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(st + p * 1024), 16, w_voff,
-                                             w_soff[q] + 2 * k0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(st + kW4Img * 2 + p * 1024), 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(st + (8 * wid + q) * 1024), 16,
+                                             w_voff[q & 1], w_soff[q] + 2 * k0, 0, 0);
+  };
+  auto dma_x = [&](int q, int stage, int k0) {
+    w4_lds_c* const st = lds + stage * kW4StageB + kW4Img * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(st + (8 * wid + q) * 1024), 16,
                                              x_voff[q], 2 * k0, 0, 0);
+  };
+  auto dma = [&](int q, int stage, int k0) {
+    dma_w(q, stage, k0);
+    dma_x(q, stage, k0);
   };
 
   // ---- fragment addresses: W subtile i = image rows 128 wn + 16 i + rr, X subtile j =
@@ -151,26 +163,46 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     constexpr int nh = decltype(NH)::value;
     w4_lds_c* const pw = lds + rs * kW4StageB + wo + (nh ? lo1 : lo0);
     w4_lds_c* const px = lds + rs * kW4StageB + xo + (nh ? lo1 : lo0);
+#define W4_MFMA(G, JJ)                                                                     \
+    {                                                                                     \
+      const int i = (G) >> 1, j = ((G) & 1) * 4 + (JJ);                                   \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),              \
+                                                          as_bf16x8(cur[8 + j]), acc[i][j], \
+                                                          0, 0, 0);                       \
+    }
+    /* [MFMA, DMA piece, MFMA, fragment read, MFMA, MFMA]: a DMA piece's issue (~16-23   \
+       cycles of the texture path) starts right behind an MFMA, so it overlaps that      \
+       MFMA's execution instead of an idle pipe */                                        \
 #define W4_GROUP(G)                                                                       \
     {                                                                                     \
+      W4_MFMA(G, 0)                                                                       \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr (dm && !(ABL & 1)) {                                                   \
+        if constexpr (SPREAD) {                 /* X first: fewer blocks share it */     \
+          if constexpr ((G) < 8) dma_x(G, s3, k3);                                        \
+          else dma_w((G) & 7, s3, k3);                                                    \
+        } else if constexpr ((G) < 8) {                                                   \
+          dma(G, s3, k3);                                                                 \
+        }                                                                                 \
+      }                                                                                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      W4_MFMA(G, 1)                                                                       \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
       if constexpr (rd && !(ABL & 2)) {                                                   \
         if constexpr ((G) < 8) W4_READ(nxt[G], pw, 2048 * ((G) & 7));                     \
         else W4_READ(nxt[G], px, 2048 * ((G) & 7));                                       \
       }                                                                                   \
       if constexpr (rd && (ABL & 2)) asm volatile("" : "+v"(nxt[G]));                     \
-      if constexpr ((G) < 8 && dm && !(ABL & 1)) dma(G, s3, k3);                          \
-      _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                                  \
-        const int i = (G) >> 1, j = ((G) & 1) * 4 + jj;                                   \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),            \
-                                                            as_bf16x8(cur[8 + j]),        \
-                                                            acc[i][j], 0, 0, 0);          \
-      }                                                                                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      W4_MFMA(G, 2)                                                                       \
+      W4_MFMA(G, 3)                                                                       \
       __builtin_amdgcn_sched_barrier(0);                                                  \
     }
     W4_GROUP(0) W4_GROUP(1) W4_GROUP(2) W4_GROUP(3) W4_GROUP(4) W4_GROUP(5) W4_GROUP(6)
     W4_GROUP(7) W4_GROUP(8) W4_GROUP(9) W4_GROUP(10) W4_GROUP(11) W4_GROUP(12) W4_GROUP(13)
     W4_GROUP(14) W4_GROUP(15)
 #undef W4_GROUP
+#undef W4_MFMA
   };
   // the boundary inside K-tile t: K-tile t+1's DMA (own pieces) landed, k-half 1's
   // fragments landed, one barrier (every wave: the same, and done reading stage t's
@@ -277,11 +309,14 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
   const int tiles_m = (M + kW4M - 1) / kW4M;
   const int tiles_n = swiglu ? n_out / 128 : n_out / kW4N;
   const int grid = tiles_m * tiles_n;
-  if (abl && !swiglu) {
+  // abl bits 4-5: row tiles per L2 group (16, 8, 4, 32): the 32 blocks an XCD runs at
+  // once are group x (32 / group) tiles
+  const int gmr = ((abl >> 4) & 3) == 0 ? 16 : ((abl >> 4) & 3) == 1 ? 8 : ((abl >> 4) & 3) == 2 ? 4 : 32;
+  if ((abl & 7) && !swiglu) {
 #define W4_ABL(A)                                                                       \
   gemm_w4_kernel<kW4Store, A><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, \
-                                                        up_off, tiles_m, tiles_n)
-    switch (abl) {
+                                                        up_off, tiles_m, tiles_n, gmr)
+    switch (abl & 7) {
       case 1: W4_ABL(1); break;
       case 2: W4_ABL(2); break;
       case 3: W4_ABL(3); break;
@@ -293,12 +328,22 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
 #undef W4_ABL
     return;
   }
-  if (swiglu)
-    gemm_w4_kernel<kW4Swiglu><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
-                                                        tiles_m, tiles_n);
-  else
-    gemm_w4_kernel<kW4Store><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
-                                                       tiles_m, tiles_n);
+  const bool spread = abl & 8;
+  if (swiglu) {
+    if (spread)
+      gemm_w4_kernel<kW4Swiglu, 0, true><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K,
+                                                                   up_off, tiles_m, tiles_n, gmr);
+    else
+      gemm_w4_kernel<kW4Swiglu><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                          tiles_m, tiles_n, gmr);
+  } else {
+    if (spread)
+      gemm_w4_kernel<kW4Store, 0, true><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K,
+                                                                  up_off, tiles_m, tiles_n, gmr);
+    else
+      gemm_w4_kernel<kW4Store><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                         tiles_m, tiles_n, gmr);
+  }
 }
 
 }  // namespace rfq

@@ -485,6 +485,8 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                     sum(times[c] for c in table[j]) + 4.0 * (len(table[j]) - 1)
                 best_c, t_best = -1, t_lib * DENSE_MARGIN
                 for c in DENSE_CFGS:
+                    if c & 8 and K % 128:            # gemm_w4 needs K % 128 == 0
+                        continue
                     t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, out[:m], False, c),
                               [w], reps, graph=False)
                     if t < t_best:
@@ -497,6 +499,8 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                     t_ref = min(t_lib, t_best) + t_silu
                     bs, ts = -1, t_ref * DENSE_MARGIN
                     for c in DENSE_CFGS:
+                        if c & 8 and K % 128:
+                            continue
                         t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, act[:m], True, c),
                                   [w], reps, graph=False)
                         if t < ts:
