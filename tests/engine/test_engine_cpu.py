@@ -348,3 +348,39 @@ def test_async_engine_survives_add_failing_in_step_and_at_loop_top(engine):
     finally:
         engine.add_request = orig
         aeng.shutdown()
+
+
+def test_serve_loop_behind_attached_router_keeps_engine(engine):
+    """The bench's two-process HTTP layout on one engine: serve_loop (engine side of the
+    request queues) + a DPRouter attached to those queues (API side) serve requests
+    through the extraction service; a None message ends the loop without shutting the
+    engine down, which then still generates directly."""
+    import queue
+    import threading
+
+    from replisense_rfq_amd.engine.router import DPRouter, serve_loop
+
+    inq, outq = queue.Queue(), queue.Queue()
+    th = threading.Thread(target=serve_loop, args=(engine, inq, outq),
+                          kwargs={"shutdown_engine": False}, daemon=True)
+    th.start()
+    router = DPRouter(engine.cfg, 1, queues=(inq, outq))
+    svc = ExtractService(router.backend())
+
+    async def go():
+        docs = [synth.make_rfq(90 + i).text for i in range(3)]
+        return await asyncio.gather(*(svc.generate_async(d, "mail") for d in docs))
+
+    try:
+        outs = asyncio.run(go())
+        assert router.stats()["completed"] == 3 and router.stats()["outstanding"] == 0
+    finally:
+        router._stop = True
+        inq.put(None)
+        th.join(timeout=30)
+    assert not th.is_alive()
+    for o in outs:
+        assert o["success"] is True and o["message"] == "RFQ processed from mail"
+    assert engine.runner.busy_hook is None
+    seqs = engine.generate(_prompts(engine, 1, base=95))
+    assert seqs[0].finish_reason in ("stop", "length", "grammar_done", "eos")
