@@ -58,7 +58,10 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 // texture path takes ~16-23 cycles per 1 KB piece; two per group in the first 8 groups
 // back the wave's issue up behind it), at the cost of a shorter landing window for the
 // last pieces.
-template <int EPI, int ABL = 0, bool SPREAD = false>
+// EARLY: the 16 fragment reads of a half go out two per group in its first 8 groups (the
+// last one then has 8 groups = 32 MFMAs to land before the next half's lgkmcnt(0));
+// otherwise one per group over all 16.
+template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
@@ -173,6 +176,14 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     /* [MFMA, DMA piece, MFMA, fragment read, MFMA, MFMA]: a DMA piece's issue (~16-23   \
        cycles of the texture path) starts right behind an MFMA, so it overlaps that      \
        MFMA's execution instead of an idle pipe */                                        \
+#define W4_FRAG(F)                                                                        \
+    {                                                                                     \
+      if constexpr (rd && !(ABL & 2)) {                                                   \
+        if constexpr ((F) < 8) W4_READ(nxt[F], pw, 2048 * ((F) & 7));                     \
+        else W4_READ(nxt[F], px, 2048 * ((F) & 7));                                       \
+      }                                                                                   \
+      if constexpr (rd && (ABL & 2)) asm volatile("" : "+v"(nxt[F]));                     \
+    }
 #define W4_GROUP(G)                                                                       \
     {                                                                                     \
       W4_MFMA(G, 0)                                                                       \
@@ -188,13 +199,16 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
       __builtin_amdgcn_sched_barrier(0);                                                  \
       W4_MFMA(G, 1)                                                                       \
       __builtin_amdgcn_sched_barrier(0);                                                  \
-      if constexpr (rd && !(ABL & 2)) {                                                   \
-        if constexpr ((G) < 8) W4_READ(nxt[G], pw, 2048 * ((G) & 7));                     \
-        else W4_READ(nxt[G], px, 2048 * ((G) & 7));                                       \
+      if constexpr (EARLY) {                                                              \
+        if constexpr ((G) < 8) W4_FRAG(2 * (G));                                          \
+      } else {                                                                            \
+        W4_FRAG(G);                                                                       \
       }                                                                                   \
-      if constexpr (rd && (ABL & 2)) asm volatile("" : "+v"(nxt[G]));                     \
       __builtin_amdgcn_sched_barrier(0);                                                  \
       W4_MFMA(G, 2)                                                                       \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr (EARLY && (G) < 8) W4_FRAG(2 * (G) + 1);                               \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
       W4_MFMA(G, 3)                                                                       \
       __builtin_amdgcn_sched_barrier(0);                                                  \
     }
@@ -203,6 +217,7 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     W4_GROUP(14) W4_GROUP(15)
 #undef W4_GROUP
 #undef W4_MFMA
+#undef W4_FRAG
   };
   // the boundary inside K-tile t: K-tile t+1's DMA (own pieces) landed, k-half 1's
   // fragments landed, one barrier (every wave: the same, and done reading stage t's
@@ -328,7 +343,16 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
 #undef W4_ABL
     return;
   }
-  const bool spread = abl & 8;
+  const bool spread = abl & 8, early = abl & 64;
+  if (spread && early) {
+    if (swiglu)
+      gemm_w4_kernel<kW4Swiglu, 0, true, true><<<grid, 256, kW4Lds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    else
+      gemm_w4_kernel<kW4Store, 0, true, true><<<grid, 256, kW4Lds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    return;
+  }
   if (swiglu) {
     if (spread)
       gemm_w4_kernel<kW4Swiglu, 0, true><<<grid, 256, kW4Lds, s>>>(x, ldx, w, ldw, out, ldo, M, K,

@@ -430,7 +430,10 @@ def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0
 LT_CANDIDATES = int(os.environ.get("RFQ_GEMM_LT_CANDIDATES", "6"))   # heuristic algorithms timed per (M bucket, N, K)
 # RFQ_GEMM_DENSE=0 keeps every large-M projection on hipBLASLt
 DENSE_ON = os.environ.get("RFQ_GEMM_DENSE", "1") != "0"
-DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2").split(","))
+# 2: gemm_dense's 8-wave ping-pong; 1672 = 8 | 128 | 512 | 1024: gemm_w4 (one wave per
+# SIMD), DMA spread over the MFMA groups, 4 row tiles per L2 group, fragment reads early
+# in each half (profiles/r4_gemm_w4.md)
+DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,1672").split(","))
 DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 
@@ -514,8 +517,10 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
             del act
         plan[(N, K)] = (quantum, table, algos, dense, swi)
         report.append(("lt:" + name, J * quantum, N, K, J, f"{n_lt}/{J} buckets", 0.0))
+        w4 = sum(1 for c in dense if c >= 0 and c & 8)
+        w4s = sum(1 for c in swi if c >= 0 and c & 8)
         report.append(("dense:" + name, J * quantum, N, K, J,
-                       f"{n_dense}/{J} buckets, swiglu {n_swi}/{J}", 0.0))
+                       f"{n_dense}/{J} buckets (w4 {w4}), swiglu {n_swi}/{J} (w4 {w4s})", 0.0))
         for j, parts in enumerate(table):
             if parts is not None:
                 t_split = sum(times[c] for c in parts)
