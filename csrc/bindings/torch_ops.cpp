@@ -46,6 +46,10 @@ void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, i
 void launch_attn_decode_reduce(const float*, const float*, bf16_t*, int64_t, int, int, int,
                                hipStream_t);
 bool gemv_merge_fits(int, int, int, int);
+bool gemv_push_fits(int, int, int, int, int);
+void launch_gemv_push_norm(const bf16_t*, int64_t, const bf16_t*, int, int, int, int, float*,
+                           unsigned*, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
+                           unsigned*, char* const*, int, int, hipStream_t);
 void launch_gemv_splitk_merge(const float*, const float*, int, const bf16_t*, int, int, bf16_t*,
                               int64_t, int, int, float*, unsigned*, bf16_t*, int64_t,
                               const bf16_t*, bf16_t*, int64_t, float, unsigned*, hipStream_t);
@@ -900,6 +904,45 @@ void car_allreduce_add_norm(const Tensor& inp, const Tensor& residual, const Ten
                                      (int)d, (float)eps, cur_stream());
 }
 
+// TP row-parallel GEMV + custom all-reduce (push form) + residual-add RMSNorm in one
+// launch (csrc/comm/gemv_push.hip): residual <- bf16(allreduce(x . w^T) + residual),
+// out <- rmsnorm(residual) * norm_w, bit-identical to gemv_splitk + car_allreduce_add_norm
+// (algo 2).  counter: the norm ticket (ops.norm_counter), left at zero.
+void gemv_push_norm(const Tensor& x, const Tensor& w, const Tensor& part, const Tensor& tile_cnt,
+                    int64_t cfg, const Tensor& residual, const Tensor& norm_w, double eps,
+                    const Tensor& out, const Tensor& counter, c10::IntArrayRef bases,
+                    int64_t rank, int64_t capacity_bytes) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_ROWMAJOR(x); CHECK_I32(tile_cnt);
+  CHECK_BF16(residual); CHECK_BF16(norm_w); CHECK_BF16(out); CHECK_I32(counter);
+  CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemv_push_norm: w must be contiguous [N, K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), KS = 2 << (cfg & 3);
+  const int world = (int)bases.size();
+  TORCH_CHECK(rfq::gemv_push_fits(world, (int)M, (int)N, (int)K, (int)cfg) && w.size(1) == K,
+              "gemv_push_norm: 1 <= M <= 4, N % 16 == 0, N <= 8192, K % 128 == 0, K / 128 >= KS, "
+              "no persistent cfg, world <= 8");
+  TORCH_CHECK(rank >= 0 && rank < world, "gemv_push_norm: rank");
+  TORCH_CHECK(rfq::car_push_fits(world, (int)M, (int)N, capacity_bytes),
+              "gemv_push_norm: push slots exceed the custom all-reduce buffer");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "gemv_push_norm: alignment");
+  TORCH_CHECK(residual.size(0) == M && residual.size(1) == N && out.size(0) == M &&
+                  out.size(1) == N && norm_w.numel() == N && residual.stride(0) % 8 == 0 &&
+                  out.stride(0) % 8 == 0,
+              "gemv_push_norm: residual / out [M, N], norm_w [N]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
+              "gemv_push_norm: fp32 partials workspace of KS*M*N floats");
+  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, "gemv_push_norm: tile counters");
+  TORCH_CHECK(counter.is_cuda() && counter.numel() >= 1, "gemv_push_norm: counter");
+  char* b[8];
+  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
+  rfq::launch_gemv_push_norm(bp(x), x.stride(0), bp(w), (int)N, (int)K, (int)M, (int)cfg,
+                             part.data_ptr<float>(),
+                             reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), bpm(residual),
+                             residual.stride(0), bp(norm_w), bpm(out), out.stride(0), (float)eps,
+                             reinterpret_cast<unsigned*>(counter.data_ptr()), b, (int)rank, world,
+                             cur_stream());
+}
+
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
                const Tensor& inv_pos, const Tensor& expert_of_block,
                const Tensor& expert_offsets, const Tensor& num_blocks) {
@@ -1055,6 +1098,9 @@ TORCH_LIBRARY(rfq_amd, m) {
         "float eps, Tensor(e!)? out, Tensor(f!)? counter) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
+  m.def("gemv_push_norm(Tensor x, Tensor w, Tensor(a!) part, Tensor(b!) tile_cnt, int cfg, "
+        "Tensor(c!) residual, Tensor norm_w, float eps, Tensor(d!) out, Tensor(e!) counter, "
+        "int[] bases, int rank, int capacity_bytes) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
   m.def("car_allreduce_add_norm(Tensor inp, Tensor(a!) residual, Tensor w, float eps, "
@@ -1128,6 +1174,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("qkv_attn", &qkv_attn);
   m.impl("attn_decode_merge", &attn_decode_merge);
   m.impl("gemv_splitk_merge", &gemv_splitk_merge);
+  m.impl("gemv_push_norm", &gemv_push_norm);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);

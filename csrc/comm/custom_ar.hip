@@ -26,59 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include "../kernels/common.h"
+#include "car_core.h"
 
 namespace rfq {
-
-constexpr int kCarMaxRanks = 8;
-constexpr int kCarMaxBlocks = 64;
-constexpr int kCarThreads = 512;
-
-struct CarSignal {
-  uint32_t start[kCarMaxBlocks][kCarMaxRanks];
-  uint32_t mid[kCarMaxBlocks][kCarMaxRanks];     // two-shot: reduced slices published
-  uint32_t end[kCarMaxBlocks][kCarMaxRanks];
-  uint32_t push[2][kCarMaxBlocks][kCarMaxRanks]; // push one-shot: row published, by parity
-  uint32_t counter[kCarMaxBlocks];
-  uint32_t error;
-  uint32_t info;             // first timeout: 0x80000000 | phase << 24 | block << 8 | peer
-  uint32_t pad[62];
-};
-
-constexpr int64_t kCarDataOffset = (sizeof(CarSignal) + 4095) / 4096 * 4096;
-
-struct CarPeers {
-  char* base[kCarMaxRanks];  // region base of every rank (own included)
-};
-
-__device__ __forceinline__ void car_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Spins are bounded in wall time (the 100 MHz s_memrealtime clock), not in
-// iterations: a peer whose queue the hardware scheduler has not mapped yet (more GPU
-// processes than concurrent process slots, e.g. 8 ranks + a launcher sharing one
-// device) is waited for the same 2 s however slow each poll is.  A timeout records
-// the first failing (phase, block, peer) in `info` for the host's diagnostics.
-constexpr uint64_t kCarSpinTicks = 200000000ull;           // 2 s at 100 MHz
-enum : uint32_t { kCarStart = 1, kCarMid = 2, kCarEnd = 3, kCarPush = 4 };
-
-// A region whose error counter is set (a peer went silent before) fails every wait at
-// once: after the first timeout a lost peer costs no further 2 s spins -- the runner
-// sees the error behind that step and the replica restarts on RCCL (router.py).
-__device__ __forceinline__ bool car_wait(CarSignal* self, uint32_t* p, uint32_t v,
-                                         uint32_t phase, int b, int peer) {
-  if (__hip_atomic_load(&self->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
-    return false;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == v) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > kCarSpinTicks) {
-      atomicCAS(&self->info, 0u, 0x80000000u | (phase << 24) | ((uint32_t)b << 8) | (uint32_t)peer);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
 
 __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
     CarPeers peers, int rank, int world, const bf16_t* __restrict__ in,
@@ -324,8 +274,6 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
   }
 }
 
-constexpr int kCarPushRows = 16;      // decode rows of the push form
-constexpr int kCarPushD = 8192;       // max row width of the push form (bf16)
 
 // Push one-shot all-reduce + residual-add RMSNorm for decode rows (the latency path's
 // 160 all-reduces per Llama-3-70B step at TP=8).  One xGMI hop instead of the staged
@@ -361,29 +309,17 @@ __global__ __launch_bounds__(256) void car_push_add_norm_kernel(
   __syncthreads();
   const uint32_t c = cnt_s;
   const int par = (int)(c & 1u);
-  // slot (par, src, row b) of a region: a fixed home per (parity, source rank, row)
-  // whatever the call's shape, so a call of another shape on a faster rank can never
-  // write into slots a slower rank is still reading (parity alternates per row b)
-  auto slot = [&](int p, int src) {
-    return reinterpret_cast<s16x8*>(peers.base[p] + kCarDataOffset) +
-           (((int64_t)par * kCarMaxRanks + src) * kCarPushRows + b) * (kCarPushD / 8);
-  };
   const s16x8* src = reinterpret_cast<const s16x8*>(in) + (int64_t)b * nchunk;
-  s16x8* rr = reinterpret_cast<s16x8*>(residual + b * res_stride);
-  const s16x8* wr = reinterpret_cast<const s16x8*>(w);
   s16x8 xv[NCH], rv[NCH], wv[NCH];
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int ch = tid + k * 256;
-    if (ch < nchunk) {
-      xv[k] = src[ch];
-      rv[k] = rr[ch];
-      wv[k] = wr[ch];
-    }
+    if (ch < nchunk) xv[k] = src[ch];
   }
+  car_push_preload<NCH>(b, residual, res_stride, w, d, rv, wv);
   // 1. push the row into every rank's slot [par][rank][b] (own region included)
   for (int p = 0; p < world; ++p) {
-    s16x8* dst = slot(p, rank);
+    s16x8* dst = car_push_slot(peers.base[p], par, rank, b);
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int ch = tid + k * 256;
@@ -400,46 +336,9 @@ __global__ __launch_bounds__(256) void car_push_add_norm_kernel(
     if (!car_wait(self, &self->push[par][b][tid], c, kCarPush, b, tid)) fail_s = 1;
   }
   __syncthreads();
-  // 3. sum row b over the ranks (rank order, fp32, rounded to bf16 = the all-reduce
-  //    output), add the residual, round, normalise
-  float v[NCH][8];
-  float ss = 0.f;
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int ch = tid + k * 256;
-    if (ch < nchunk) {
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p < world; ++p) {
-        const s16x8 pv = slot(rank, p)[ch];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += bf2f_s(pv[j]);
-      }
-      float a[8], r[8];
-      unpack8(pack8(acc), a);
-      unpack8(rv[k], r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += r[j];
-      const s16x8 packed = pack8(a);
-      rr[ch] = packed;
-      unpack8(packed, v[k]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
-    }
-  }
-  ss = block_sum(ss, scratch);
-  const float rs = rsqrtf(ss / (float)d + eps);
-  s16x8* orow = reinterpret_cast<s16x8*>(out + b * out_stride);
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int ch = tid + k * 256;
-    if (ch < nchunk) {
-      float wf[8], o[8];
-      unpack8(wv[k], wf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * rs * wf[j];
-      orow[ch] = pack8(o);
-    }
-  }
+  // 3. sum row b over the ranks, add the residual, normalise
+  car_push_sum_norm_row<NCH>(peers.base[rank], par, world, b, residual, res_stride, rv, wv, out,
+                             out_stride, d, eps, scratch);
   if (tid == 0) {
     self->counter[b] = c;
     if (fail_s) atomicAdd(&self->error, 1u);

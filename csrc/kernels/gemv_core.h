@@ -3,6 +3,7 @@
 // QKV + RoPE + KV-append + decode-attention launch of the latency path).
 #pragma once
 #include "common.h"
+#include "../comm/car_core.h"
 
 namespace rfq {
 
@@ -148,7 +149,62 @@ struct RopeEpi {
 //             +16) of one head (RopeEpi): NeoX RoPE on q / k, q to Y, k / v appended
 //             to the paged cache.  The TP = 8 QKV shard (N = 1,280) has only 40 such
 //             pairs: split K is what lets it use more than 40 CUs.
-enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
+//   kGvPush   (TP row-parallel o / down, M <= kGvPushMaxM) the tile's bf16 outputs go
+//             straight into slot [parity][rank][row] of every TP rank's custom
+//             all-reduce staging (remote stores, car_core.h); each workgroup releases
+//             them at system scope before its ticket on ep.counter, and the grid's last
+//             one raises this rank's flag on every peer, waits for every peer's flag and
+//             runs the all-reduce sum + residual-add RMSNorm of car_push_add_norm_kernel
+//             (car_push_sum_norm_row) -- the o / down GEMV, the all-reduce and the norm
+//             in one launch, bit-identical to gemv_splitk + the push all-reduce.
+enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3, kGvPush = 4 };
+constexpr int kGvPushMaxM = 4;
+
+// kGvPush: the custom all-reduce regions (every rank's base, own included).
+struct PushEpi {
+  char* base[kCarMaxRanks];
+  int rank, world;
+};
+
+// The all-reduce tail of kGvPush, run by the grid's last workgroup once every tile of
+// this rank has pushed its rows: raise flag push[par_b][b][rank] on every peer for the
+// M rows, wait for every peer's flags (bounded, car_wait), then per row the rank-order
+// sum + residual-add RMSNorm of the push all-reduce (car_push_sum_norm_row: the same
+// code, so bit-identical), and advance the row counters.
+__device__ __forceinline__ void gemv_push_tail(const PushEpi& pe, const NormEpi& ep, int M, int d,
+                                            float* scratch) {
+  CarSignal* self = reinterpret_cast<CarSignal*>(pe.base[pe.rank]);
+  const int tid = threadIdx.x;
+  __shared__ uint32_t cnt_s[kGvPushMaxM];
+  __shared__ int fail_s;
+  if (tid < M) cnt_s[tid] = self->counter[tid] + 1;
+  if (tid == 0) fail_s = 0;
+  __syncthreads();
+  const int nf = pe.world * M;
+  if (tid < nf) {
+    const int p = tid % pe.world, b = tid / pe.world;
+    const uint32_t c = cnt_s[b];
+    CarSignal* peer = reinterpret_cast<CarSignal*>(pe.base[p]);
+    car_store(&peer->push[c & 1u][b][pe.rank], c);
+  }
+  constexpr int NCH = 4;                     // d <= 8192 = 8 * 256 * 4
+  s16x8 rv[NCH], wv[NCH];
+  car_push_preload<NCH>(0, ep.residual, ep.res_stride, ep.w, d, rv, wv);
+  if (tid < nf) {
+    const int p = tid % pe.world, b = tid / pe.world;
+    const uint32_t c = cnt_s[b];
+    if (!car_wait(self, &self->push[c & 1u][b][p], c, kCarPush, b, p)) fail_s = 1;
+  }
+  __syncthreads();
+  for (int b = 0; b < M; ++b) {
+    if (b > 0) car_push_preload<NCH>(b, ep.residual, ep.res_stride, ep.w, d, rv, wv);
+    car_push_sum_norm_row<NCH>(pe.base[pe.rank], (int)(cnt_s[b] & 1u), pe.world, b,
+                               ep.residual, ep.res_stride, rv, wv, ep.out, ep.out_stride, d,
+                               ep.eps, scratch);
+  }
+  if (tid < M) self->counter[tid] = cnt_s[tid];
+  if (tid == 0 && fail_s) atomicAdd(&self->error, 1u);
+}
 
 //
 // TL (cfg bit 4): W is stored in the decode-tiled layout (ops.tile_weight): for
@@ -193,10 +249,10 @@ __device__ __forceinline__ void gemv_splitk_unit(
     const bf16_t* __restrict__ W, int K, bf16_t* __restrict__ Y, int64_t ldy, int M, int KS,
     float* __restrict__ part, int Nn, unsigned* __restrict__ tile_cnt, const NormEpi& ep,
     const RopeEpi& re, int up_off, unsigned* __restrict__ done = nullptr,
-    AttnMerge am = AttnMerge{}) {
+    AttnMerge am = AttnMerge{}, PushEpi pe = PushEpi{}) {
   static_assert(!PUB || EPI == kGvRope, "PUB: the rope epilogue only");
   static_assert(!AM || EPI == kGvPlain || EPI == kGvNorm, "AM: plain / norm epilogues only");
-  constexpr int NT = EPI >= kGvSwi ? 2 : 1;
+  constexpr int NT = (EPI == kGvSwi || EPI == kGvRope) ? 2 : 1;
   __shared__ f32x4 red[NW][NT][64];
   __shared__ float nscratch[17];
   __shared__ __attribute__((aligned(16))) bf16_t xs[AM ? kAmLdsElems : 8];
@@ -225,6 +281,7 @@ __device__ __forceinline__ void gemv_splitk_unit(
     wp[a] = TL ? W + (int64_t)(row0[a] >> 4) * (K >> 7) * 2048 + lane * 8
                : W + (int64_t)(row0[a] + r) * K + g * 8;
   const bool xv = r < M;
+
   // AM: X rows live in LDS as [M][nks * 128] (slice-relative k); else in global memory
   const bf16_t* xp = AM ? xs + (int64_t)(xv ? r : 0) * nks * 128 - sl0 * 128 + g * 8
                         : X + (int64_t)(xv ? r : 0) * ldx + g * 8;
@@ -455,6 +512,19 @@ __device__ __forceinline__ void gemv_splitk_unit(
           *reinterpret_cast<uint2*>(dst + 64 + d0) = v2;
         }
       }
+    } else if constexpr (EPI == kGvPush) {
+      // the tile's bf16 outputs (= the GEMV's Y) into slot [parity][rank][r] of every
+      // rank's staging: remote stores over xGMI, own region included
+      uint2 v;
+      v.x = pack_bf16x2(s[0][0], s[0][1]);
+      v.y = pack_bf16x2(s[0][2], s[0][3]);
+      // row r's all-reduce call counter + 1 (read by the tile's final workgroup only)
+      const uint32_t push_c = reinterpret_cast<const CarSignal*>(pe.base[pe.rank])->counter[r] + 1;
+      const int par = (int)(push_c & 1u);
+      for (int p = 0; p < pe.world; ++p) {
+        bf16_t* dst = reinterpret_cast<bf16_t*>(car_push_slot(pe.base[p], par, pe.rank, r));
+        *reinterpret_cast<uint2*>(dst + row0[0] + g * 4) = v;
+      }
     } else {
       uint2 v;
       v.x = pack_bf16x2(s[0][0], s[0][1]);
@@ -476,6 +546,27 @@ __device__ __forceinline__ void gemv_splitk_unit(
         __hip_atomic_fetch_add(done + 32 * grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+  }
+  if constexpr (EPI == kGvPush) {
+    // drain the pushed rows, count the tile; the grid's last workgroup (every tile's
+    // rows acknowledged by every peer's memory) runs the all-reduce tail.  No per-
+    // workgroup fence: the staging is uncached (hipDeviceMallocUncached), so there is no
+    // dirty L2 line to write back, and a store's vmcnt acknowledgement is its completion
+    // at the target -- a system-scope release here (an L2 writeback per workgroup) made
+    // the launch 5-10x slower (profiles/r4_gemv_push.md).  The flags that publish the
+    // rows are release stores (car_store).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev =
+          __hip_atomic_fetch_add(ep.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nscratch[16] = (prev == (unsigned)ntile - 1) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (nscratch[16] == 0.f) return;
+    if (threadIdx.x == 0)
+      __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gemv_push_tail(pe, ep, M, ntile * 16, nscratch);
   }
   if constexpr (EPI == kGvNorm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

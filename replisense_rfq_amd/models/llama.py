@@ -222,8 +222,10 @@ class DecoderLM:
                 else:
                     o = ops.linear_merge(po, pm, m.decode_splits, lw["o"], T, mcfg)
                     self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
-            elif not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
-                                                   x)):
+            elif not ((fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"],
+                                                    eps, x))
+                      or self.tp.linear_add_norm_(attn, lw["o"], residual, lw["mlp_norm"], eps,
+                                                  x)):
                 o = ops.linear(attn, lw["o"])
                 self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
@@ -236,6 +238,9 @@ class DecoderLM:
                 act = ops.linear_swiglu(x, lw["gate_up"]) if T <= ops.NORM_FUSE_MAX_M else None
                 if act is not None:
                     if fuse and ops.linear_add_norm(act, lw["down"], residual, nxt, eps, x):
+                        continue
+                    # TP: down + all-reduce + norm in one launch (RFQ_GEMV_PUSH=1)
+                    if self.tp.linear_add_norm_(act, lw["down"], residual, nxt, eps, x):
                         continue
                     mo = ops.linear(act, lw["down"])
                 else:

@@ -330,6 +330,30 @@ def linear_merge(part_o, part_ml, S: int, w, M: int, cfg: int, norm=None) -> tor
     return y
 
 
+GEMV_PUSH_MAX_M = 4
+PUSH_DEFAULT_CFG = 8                   # KS 2, 4 waves, U 2 (+ tiled / nt when available)
+
+
+def gemv_push_fits(world: int, M: int, N: int, K: int, cfg: int) -> bool:
+    """Host mirror of csrc/comm/gemv_push.hip gemv_push_fits."""
+    KS = 2 << (cfg & 3)
+    return (1 <= world <= 8 and 1 <= M <= GEMV_PUSH_MAX_M and N % 16 == 0 and N <= 8192
+            and K % 128 == 0 and K // 128 >= KS and not cfg & SPLITK_PERSIST)
+
+
+def push_gemv_cfg(M: int, N: int, K: int, w: torch.Tensor) -> int:
+    """Split-K GEMV cfg (low 7 bits) for the fused GEMV + all-reduce: the linear plan's
+    split-K entry for this shape, else KS 2 / 4 waves / U 2 on the tiled layout with
+    non-temporal loads when the weight has a tiled copy (row-major otherwise); -1 when
+    the weight only exists tiled and no tiled cfg is known."""
+    c = linear_plan(M, N, K) if _LINEAR_PLAN else -1
+    if c >= 0 and c & SPLITK_BIT:
+        return c & 127
+    if tiled_of(w) is not None:
+        return PUSH_DEFAULT_CFG | SPLITK_TILED | SPLITK_NT
+    return -1 if tiled_only(w) else PUSH_DEFAULT_CFG
+
+
 # (M, F, K) -> skinny cfg of the gate|up projection with the SwiGLU epilogue
 # (gemm_skinny.hip SWI: out [M, F] = silu(x Wg^T) * (x Wu^T)), or absent = unfused.
 _SWI_PLAN: dict[tuple[int, int, int], int] = {}
