@@ -32,10 +32,11 @@ FUSE_NORM = os.environ.get("RFQ_CAR_NORM", "1") != "0"
 CAR_NORM_ALGO = 1 if os.environ.get("RFQ_CAR_PUSH", "1") == "0" else 0
 
 # RFQ_GEMV_PUSH=1: the row-parallel o / down GEMV pushes its rows into the peers' slots and
-# runs the all-reduce + norm in its own last workgroup (linear_add_norm_).  Off by default
-# until it has run over xGMI: on one GPU it is bit-identical and faster
-# (profiles/r4_gemv_push.md), but its cross-device ordering (many workgroups' remote stores
-# released before one flag) is only exercised by ranks sharing one device here.
+# runs the all-reduce + norm in its own last workgroup (linear_add_norm_).  Off by default:
+# bit-identical at world 2/4/8, but measured slower than the GEMV followed by the push
+# kernel (16 -> 21 µs for the TP=8 o projection at one row, profiles/r4_gemv_push.md): the
+# last workgroup's chain of dependent round trips (ticket, counter, flag, remote slots)
+# costs more than the launch boundary it removes.
 GEMV_PUSH = os.environ.get("RFQ_GEMV_PUSH", "0") == "1"
 
 class CustomAllReduce:
