@@ -61,7 +61,11 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 // EARLY: the 16 fragment reads of a half go out two per group in its first 8 groups (the
 // last one then has 8 groups = 32 MFMAs to land before the next half's lgkmcnt(0));
 // otherwise one per group over all 16.
-template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false>
+// MF: 16 = mfma_f32_16x16x32_bf16 (a wave's quadrant = 8 x 8 accumulators of 16 x 16),
+// 32 = mfma_f32_32x32x16_bf16 (4 x 4 of 32 x 32).  A 32x32x16 MFMA holds the SIMD for 32
+// cycles, twice the 16x16x32's 16, so a DMA piece's issue (~16-23 cycles) hides behind
+// one MFMA instead of stalling the pipe.
+template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false, int MF = 16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
@@ -135,15 +139,30 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   // ---- fragment addresses: W subtile i = image rows 128 wn + 16 i + rr, X subtile j =
   // rows 128 wm + 16 j + rr; k-half h reads chunk 4 h + kq at (4 h + kq) ^ ((rr >> 1) & 7);
   // subtile steps of 2 KB are ds_read immediates
+  // MF 32: 32-row subtiles (4 KB apart), lane l reads row l & 31, chunk 4 h + 2 ks + (l >> 5)
+  // of k-half h, k-step ks
   const int sw = (rr >> 1) & 7;
-  const int lo0 = rr * 128 + 16 * (kq ^ sw), lo1 = rr * 128 + 16 * ((4 + kq) ^ sw);
+  const int r32 = lane & 31, k32 = lane >> 5, sw32 = (r32 >> 1) & 7;
+  const int lo[2][2] = {
+      {MF == 16 ? rr * 128 + 16 * (kq ^ sw) : r32 * 128 + 16 * (k32 ^ sw32),
+       MF == 16 ? 0 : r32 * 128 + 16 * ((2 + k32) ^ sw32)},
+      {MF == 16 ? rr * 128 + 16 * ((4 + kq) ^ sw) : r32 * 128 + 16 * ((4 + k32) ^ sw32),
+       MF == 16 ? 0 : r32 * 128 + 16 * ((6 + k32) ^ sw32)}};
   const int wo = 16384 * wn, xo = kW4Img * 2 + 16384 * wm;
+  constexpr int SUB = MF == 16 ? 2048 : 4096;       // bytes between subtiles
 
-  f32x4 acc[8][8];                                  // [W subtile i][X subtile j]
+  f32x4 acc[MF == 16 ? 8 : 1][MF == 16 ? 8 : 1];   // MF 16: [W subtile i][X subtile j]
+  f32x16 acc32[MF == 32 ? 4 : 1][MF == 32 ? 4 : 1];  // MF 32: [W subtile i][X subtile j]
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < (MF == 16 ? 8 : 1); ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < (MF == 16 ? 8 : 1); ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (MF == 32 ? 4 : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (MF == 32 ? 4 : 1); ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc32[i][j][q] = 0.f;
 
   s16x8 f0[16], f1[16];      // fragments of k-half 0 / 1 of a K-tile: [0..7] W_i, [8..15] X_j
 
@@ -164,14 +183,23 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
                   int s3, int k3) {
     constexpr bool rd = decltype(RD)::value, dm = decltype(DM)::value;
     constexpr int nh = decltype(NH)::value;
-    w4_lds_c* const pw = lds + rs * kW4StageB + wo + (nh ? lo1 : lo0);
-    w4_lds_c* const px = lds + rs * kW4StageB + xo + (nh ? lo1 : lo0);
+    w4_lds_c* const pw = lds + rs * kW4StageB + wo + lo[nh][0];
+    w4_lds_c* const px = lds + rs * kW4StageB + xo + lo[nh][0];
+    w4_lds_c* const pw1 = lds + rs * kW4StageB + wo + lo[nh][1];   // MF 32, k-step 1
+    w4_lds_c* const px1 = lds + rs * kW4StageB + xo + lo[nh][1];
 #define W4_MFMA(G, JJ)                                                                     \
     {                                                                                     \
-      const int i = (G) >> 1, j = ((G) & 1) * 4 + (JJ);                                   \
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),              \
-                                                          as_bf16x8(cur[8 + j]), acc[i][j], \
-                                                          0, 0, 0);                       \
+      if constexpr (MF == 16) {                                                           \
+        const int i = (G) >> 1, j = ((G) & 1) * 4 + (JJ);                                 \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),            \
+                                                            as_bf16x8(cur[8 + j]),        \
+                                                            acc[i][j], 0, 0, 0);          \
+      } else if constexpr ((JJ) < 2) {          /* (i, j) = (G / 4, G % 4), k-step JJ */ \
+        const int i = (G) >> 2, j = (G) & 3;                                              \
+        acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(                            \
+            as_bf16x8(cur[2 * i + (JJ)]), as_bf16x8(cur[8 + 2 * j + (JJ)]), acc32[i][j],   \
+            0, 0, 0);                                                                     \
+      }                                                                                   \
     }
     /* [MFMA, DMA piece, MFMA, fragment read, MFMA, MFMA]: a DMA piece's issue (~16-23   \
        cycles of the texture path) starts right behind an MFMA, so it overlaps that      \
@@ -179,8 +207,13 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
 #define W4_FRAG(F)                                                                        \
     {                                                                                     \
       if constexpr (rd && !(ABL & 2)) {                                                   \
-        if constexpr ((F) < 8) W4_READ(nxt[F], pw, 2048 * ((F) & 7));                     \
-        else W4_READ(nxt[F], px, 2048 * ((F) & 7));                                       \
+        if constexpr (MF == 16) {                                                         \
+          if constexpr ((F) < 8) W4_READ(nxt[F], pw, SUB * ((F) & 7));                    \
+          else W4_READ(nxt[F], px, SUB * ((F) & 7));                                      \
+        } else {                    /* F = 2 subtile + k-step (W 0..7, X 8..15) */       \
+          if constexpr ((F) < 8) W4_READ(nxt[F], ((F) & 1) ? pw1 : pw, SUB * ((F) >> 1)); \
+          else W4_READ(nxt[F], ((F) & 1) ? px1 : px, SUB * (((F) & 7) >> 1));             \
+        }                                                                                 \
       }                                                                                   \
       if constexpr (rd && (ABL & 2)) asm volatile("" : "+v"(nxt[F]));                     \
     }
@@ -250,15 +283,26 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  {
-    w4_lds_c* const pw = lds + wo + lo0;
-    w4_lds_c* const px = lds + xo + lo0;
+  if constexpr (MF == 16) {
+    w4_lds_c* const pw = lds + wo + lo[0][0];
+    w4_lds_c* const px = lds + xo + lo[0][0];
     W4_READ(f0[0], pw, 0);     W4_READ(f0[1], pw, 2048);  W4_READ(f0[2], pw, 4096);
     W4_READ(f0[3], pw, 6144);  W4_READ(f0[4], pw, 8192);  W4_READ(f0[5], pw, 10240);
     W4_READ(f0[6], pw, 12288); W4_READ(f0[7], pw, 14336);
     W4_READ(f0[8], px, 0);     W4_READ(f0[9], px, 2048);  W4_READ(f0[10], px, 4096);
     W4_READ(f0[11], px, 6144); W4_READ(f0[12], px, 8192); W4_READ(f0[13], px, 10240);
     W4_READ(f0[14], px, 12288); W4_READ(f0[15], px, 14336);
+  } else {
+    w4_lds_c* const pw = lds + wo + lo[0][0];
+    w4_lds_c* const px = lds + xo + lo[0][0];
+    w4_lds_c* const pw1 = lds + wo + lo[0][1];
+    w4_lds_c* const px1 = lds + xo + lo[0][1];
+    W4_READ(f0[0], pw, 0);      W4_READ(f0[1], pw1, 0);     W4_READ(f0[2], pw, 4096);
+    W4_READ(f0[3], pw1, 4096);  W4_READ(f0[4], pw, 8192);   W4_READ(f0[5], pw1, 8192);
+    W4_READ(f0[6], pw, 12288);  W4_READ(f0[7], pw1, 12288);
+    W4_READ(f0[8], px, 0);      W4_READ(f0[9], px1, 0);     W4_READ(f0[10], px, 4096);
+    W4_READ(f0[11], px1, 4096); W4_READ(f0[12], px, 8192);  W4_READ(f0[13], px1, 8192);
+    W4_READ(f0[14], px, 12288); W4_READ(f0[15], px1, 12288);
   }
 
   // ---- K-tile t: half 0 (MFMAs on f0, reads of half 1 into f1, same stage), the
@@ -281,7 +325,9 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   mid();
   half(f1, f0, F_{}, H0{}, 0, F_{}, 0, 0);
 
-  // ---- epilogue.  Lane holds out[row0 + 128 wm + 16 j + rr][n0 + 16 i + 4 kq + 0..3]
+  // ---- epilogue.  MF 16: lane holds out[row0 + 128 wm + 16 j + rr][n0 + 16 i + 4 kq + 0..3];
+  // MF 32: out[row0 + 128 wm + 32 j + (l & 31)][n0 + 32 i + 4 (l >> 5) + 8 vq + 0..3]
+  if constexpr (MF == 16) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int trow = 128 * wm + 16 * j + rr;
@@ -311,6 +357,42 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
         *reinterpret_cast<uint2*>(orow + tn * kW4N + 128 * wn + 16 * i + 4 * kq) = v;
       }
     }
+  }
+  } else {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int trow = 128 * wm + 32 * j + r32;
+    if (trow >= m_valid) continue;
+    bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
+    if constexpr (EPI == kW4Swiglu) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int vq = 0; vq < 4; ++vq) {
+          float o[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float gf = bf2f(f2bf(acc32[i][j][4 * vq + u]));
+            const float sg = gf / (1.f + __expf(-gf));
+            o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc32[2 + i][j][4 * vq + u]));
+          }
+          uint2 v;
+          v.x = pack_bf16x2(o[0], o[1]);
+          v.y = pack_bf16x2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(orow + tn * 128 + 64 * wn + 32 * i + 4 * k32 + 8 * vq) = v;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int vq = 0; vq < 4; ++vq) {
+          uint2 v;
+          v.x = pack_bf16x2(acc32[i][j][4 * vq + 0], acc32[i][j][4 * vq + 1]);
+          v.y = pack_bf16x2(acc32[i][j][4 * vq + 2], acc32[i][j][4 * vq + 3]);
+          *reinterpret_cast<uint2*>(orow + tn * kW4N + 128 * wn + 32 * i + 4 * k32 + 8 * vq) = v;
+        }
+    }
+  }
   }
 }
 #undef W4_READ
@@ -343,7 +425,16 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
 #undef W4_ABL
     return;
   }
-  const bool spread = abl & 8, early = abl & 64;
+  const bool spread = abl & 8, early = abl & 64, mf32 = abl & 128;
+  if (spread && early && mf32) {
+    if (swiglu)
+      gemm_w4_kernel<kW4Swiglu, 0, true, true, 32><<<grid, 256, kW4Lds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    else
+      gemm_w4_kernel<kW4Store, 0, true, true, 32><<<grid, 256, kW4Lds, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    return;
+  }
   if (spread && early) {
     if (swiglu)
       gemm_w4_kernel<kW4Swiglu, 0, true, true><<<grid, 256, kW4Lds, s>>>(

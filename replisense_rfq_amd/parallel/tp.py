@@ -100,10 +100,15 @@ class TPContext:
             t = torch.full((2, 4096), float(self.rank + 1), dtype=torch.bfloat16, device="cuda")
             r, o = torch.zeros_like(t), torch.empty_like(t)
             if car.eligible_norm(t, r, o):       # the fused decode epilogue, same vote
-                car.all_reduce_add_norm_(t, r, torch.ones(4096, dtype=torch.bfloat16,
-                                                          device="cuda"), 1e-5, o)
-                if not bool((r.float() == want).all().item()):
-                    why.append("add-norm residual")
+                # three calls: the push form alternates its slot / flag parity per call
+                ones = torch.ones(4096, dtype=torch.bfloat16, device="cuda")
+                for k in range(3):
+                    t.fill_(float(self.rank + 1 + k))
+                    r.zero_()
+                    car.all_reduce_add_norm_(t, r, ones, 1e-5, o)
+                    if not bool((r.float() == want + k * self.world).all().item()):
+                        why.append(f"add-norm residual (call {k})")
+                        break
             if car.errors():
                 why.append(f"{car.errors()} flag timeouts ({car.error_info()})")
         except RuntimeError as e:
