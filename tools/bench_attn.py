@@ -62,6 +62,62 @@ def run(B, C, P, shared, Hq=32, Hkv=8, q=1, tiles=2, splits=2, iters=20):
     return us, kv_bytes / us / 1e6
 
 
+def run_cascade(B, C, P, Hq=32, Hkv=8, q=1, tiles=2, iters=20):
+    """Throughput-shape decode attention (one split) over a shared prompt prefix: the
+    per-sequence kernel reading the prefix pages once per sequence (L2 hits) vs the
+    cascade form (attn_decode_shared: prefix pass once per 8 rows + suffix pass that
+    merges it).  Meta pass excluded (the engine runs it once per step, layer 0).
+    Returns (per-sequence µs, cascade µs, max |diff|)."""
+    dev = torch.device("cuda")
+    pages_per = (C + 31) // 32
+    pp = P // 32
+    uniq = pages_per - pp
+    nblocks = pp + B * uniq + 1
+    k = torch.randn(nblocks, Hkv, 32, 128, device=dev, dtype=torch.bfloat16)
+    v = torch.randn_like(k)
+    bt = torch.empty(B, pages_per, dtype=torch.int32)
+    nxt = pp
+    for b in range(B):
+        bt[b, :pp] = torch.arange(pp)
+        bt[b, pp:] = torch.arange(nxt, nxt + uniq)
+        nxt += uniq
+    bt = bt.to(dev)
+    G = Hq // Hkv
+    T = B * q
+    qs = torch.arange(0, T, q, dtype=torch.int32, device=dev)
+    ql = torch.full((B,), q, dtype=torch.int32, device=dev)
+    kvl = torch.full((B,), C, dtype=torch.int32, device=dev)
+    items = ((q * G + 15) // 16 + tiles - 1) // tiles
+    ws = torch.arange(B, dtype=torch.int32, device=dev).repeat_interleave(items)
+    wct = torch.arange(items, dtype=torch.int32, device=dev).repeat(B)
+    qt = torch.randn(T, Hq * 128, device=dev, dtype=torch.bfloat16)
+    out_a, out_b = torch.empty_like(qt), torch.empty_like(qt)
+    wsi = torch.empty(2 + B + T, dtype=torch.int32, device=dev)
+    pre_o = torch.empty(T * Hq * 128, device=dev)
+    pre_ml = torch.empty(T * Hq * 2, device=dev)
+    sc = 1 / math.sqrt(128)
+    fa = lambda: ops.attn_decode(qt, k, v, bt, qs, ql, kvl, ws, wct, out_a, out_a, out_a,  # noqa
+                                 Hq, Hkv, sc, 1, tiles)
+    fb = lambda: ops.attn_decode_shared(qt, k, v, bt, qs, ql, kvl, ws, wct, out_b, wsi,  # noqa
+                                        pre_o, pre_ml, Hq, Hkv, sc, tiles, False)
+    ops.attn_decode_shared(qt, k, v, bt, qs, ql, kvl, ws, wct, out_b, wsi, pre_o, pre_ml,
+                           Hq, Hkv, sc, tiles, True)
+    fa()
+    torch.cuda.synchronize()
+    diff = (out_a.float() - out_b.float()).abs().max().item()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = []
+    for f in (fa, fb, fa, fb):
+        f()
+        e0.record()
+        for _ in range(iters):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / iters * 1e3)
+    return min(res[0], res[2]), min(res[1], res[3]), diff
+
+
 def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1):
     """Batch-1 decode attention as the latency path runs it: L layers with their own
     KV caches, the L (split kernel [+ reduce]) launches captured in one hipGraph;
@@ -153,6 +209,15 @@ def main():
                 row["s16_w8_us"] = round(run_latency(C, Hq, Hkv, 16, L=L, waves=8), 2)
                 row["s32_w8_us"] = round(run_latency(C, Hq, Hkv, 32, L=L, waves=8), 2)
                 print(json.dumps(row), flush=True)
+        return
+    if os.environ.get("CASCADE"):
+        # the headline's operating point: ~1,536 decode rows, 407-token shared prompt
+        # prefix (13 pages), ~815-token contexts; extend rows q 3-9 (jump-forward)
+        for B, C, P, q in [(1536, 832, 416, 1), (1536, 832, 416, 3), (2048, 800, 416, 1),
+                           (1024, 1024, 416, 1)]:
+            a, b, d = run_cascade(B, C, P, q=q)
+            print(json.dumps({"B": B, "ctx": C, "prefix": P, "q": q, "per_seq_us": round(a, 1),
+                              "cascade_us": round(b, 1), "max_diff": d}), flush=True)
         return
     if os.environ.get("TILES_AB"):
         # column tiles per work item: 1 (138 VGPRs) vs 2 (242 VGPRs, fewer waves per SIMD)
