@@ -1,13 +1,11 @@
-set -euo pipefail
-cd $GRAFT_REPO_ROOT
+set -e
+cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/kernels/test_kernels_gpu.py -k "gemm_dense" > gpurun_out/t_gemm.log 2>&1 || { tail -40 gpurun_out/t_gemm.log; exit 1; }
-tail -1 gpurun_out/t_gemm.log
-timeout -k 10 600 python -u tools/bench_gemm_dense.py --cfg 3720 --cfgs 2,1672,3720 --ms 2048,4096,7168 --shapes gate_up,down,qkv,o,gate_up+swiglu --rounds 3 --out gpurun_out/gemm_w4_mf32.md > gpurun_out/gemm_w4_mf32.jsonl 2> gpurun_out/gemm_w4_mf32.err
-python - <<'PY'
-import json
-for l in open('gpurun_out/gemm_w4_mf32.jsonl'):
-    try: d=json.loads(l)
-    except Exception: continue
-    print(d['shape'], d['M'], d['us'], d['ok'])
-PY
+A="--steps 8 --warmup 3 --latency-runs 0 --phases none"
+val() { python -c "import json,sys;print(sys.argv[1], json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['value'])" "$1"; }
+for r in 1 2; do
+  timeout -k 10 420 python -u bench.py $A > gpurun_out/ab_off_$r.json 2> gpurun_out/ab_off_$r.err
+  val gpurun_out/ab_off_$r.json
+  RFQ_SHARED_PREFIX_MIN_ROWS=64 timeout -k 10 420 python -u bench.py $A > gpurun_out/ab_on_$r.json 2> gpurun_out/ab_on_$r.err
+  val gpurun_out/ab_on_$r.json
+done
