@@ -220,70 +220,111 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
     Bounded: a watchdog on every rank ends the process after ``--tp-latency-budget``
     seconds (rank 0 first prints the JSON line with whatever the phase measured so
     far, marked ``timeout``); an exception on any rank is reported instead of failing
-    the whole bench."""
+    the whole bench.  A custom all-reduce flag timeout on any rank (never seen on this
+    node's xGMI before the run) re-forms the group once on RCCL all-reduces and measures
+    again; ``car_fallback`` says why."""
+    import gc
+
     import torch
 
     from replisense_rfq_amd.engine.engine import LLMEngine
     from replisense_rfq_amd.utils.config import EngineConfig
+    from replisense_rfq_amd.utils.faults import CustomAllReduceError
 
     res = {"model": model, "parallelism": f"tp{wctx.world}"}
     timer = threading.Timer(args.tp_latency_budget, lambda: on_timeout(res))
     timer.daemon = True
     timer.start()
     t0 = time.perf_counter()
-    try:
-        nseq = max(8, args.tp_in_flight)
-        buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256) if b <= nseq)
-        cfg = EngineConfig.from_env(
-            model=model, tp=wctx.world, seed=args.seed, max_num_seqs=nseq,
-            max_kv_blocks=max(4096, nseq * 48), graph_buckets=buckets,
-            use_graphs=not args.no_graphs, jump_forward=not args.no_jump_forward,
-            prefix_cache=not args.no_prefix_cache)
-        eng = LLMEngine(cfg, tp=wctx)
-        res["init_s"] = round(time.perf_counter() - t0, 1)
-        res["custom_allreduce"] = wctx.car is not None
-        # why the custom xGMI all-reduce is (not) in use: "ok", "set-up failed ...",
-        # "self-test failed ...", or off on CPU / by config
-        res["car_status"] = wctx.car_status or ("ok" if wctx.car is not None else
-                                                "off" if not cfg.custom_allreduce else
-                                                "not enabled on this device")
-        if wctx.rank == 0:
-            try:
-                lat, detail = latency(eng, 0, args.tp_latency_runs)
-                res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
-                res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
-                res["single_stream"] = _single_stream(detail)
-                res["runs"] = len(lat)
-                if args.tp_docs > 0:
-                    stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
-                    warm = max(1, args.tp_in_flight // 2)
-                    stream.run_until(warm)
-                    stream.clear_window()
-                    if eng.device.type == "cuda":
-                        torch.cuda.synchronize()
-                    t1 = time.perf_counter()
-                    stream.run_until(warm + args.tp_docs)
-                    if eng.device.type == "cuda":
-                        torch.cuda.synchronize()
-                    dt = time.perf_counter() - t1
-                    res["docs_per_s"] = round(args.tp_docs / dt, 3)
-                    res["docs"], res["in_flight"] = args.tp_docs, args.tp_in_flight
-                    res["per_doc"] = {k: round(v, 2)
-                                      for k, v in validate(eng, stream.finished).items()}
-                    stream.close()
-            finally:
-                if wctx.enabled:
-                    eng.shutdown()
-        else:
-            eng.worker_loop()
-        if eng.device.type == "cuda":
-            torch.cuda.synchronize()
-        res["status"] = "ok"
-    except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never fatal
-        res["status"] = f"error: {type(e).__name__}: {str(e)[:300]}"
+    for attempt in range(2):
+        car_err = None
+        eng = None
+        try:
+            nseq = max(8, args.tp_in_flight)
+            buckets = tuple(b for b in (1, 2, 4, 8, 16, 32, 64, 128, 256) if b <= nseq)
+            cfg = EngineConfig.from_env(
+                model=model, tp=wctx.world, seed=args.seed, max_num_seqs=nseq,
+                max_kv_blocks=max(4096, nseq * 48), graph_buckets=buckets,
+                use_graphs=not args.no_graphs, jump_forward=not args.no_jump_forward,
+                prefix_cache=not args.no_prefix_cache)
+            if attempt:
+                cfg.custom_allreduce = False
+            eng = LLMEngine(cfg, tp=wctx)
+            res["init_s"] = round(time.perf_counter() - t0, 1)
+            res["custom_allreduce"] = wctx.car is not None
+            # why the custom xGMI all-reduce is (not) in use: "ok", "set-up failed ...",
+            # "self-test failed ...", a runtime fallback, or off on CPU / by config
+            res["car_status"] = wctx.car_status or ("ok" if wctx.car is not None else
+                                                    "off" if not cfg.custom_allreduce else
+                                                    "not enabled on this device")
+            if wctx.rank == 0:
+                try:
+                    lat, detail = latency(eng, 0, args.tp_latency_runs)
+                    res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
+                    res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
+                    res["single_stream"] = _single_stream(detail)
+                    res["runs"] = len(lat)
+                    if args.tp_docs > 0:
+                        stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
+                        warm = max(1, args.tp_in_flight // 2)
+                        stream.run_until(warm)
+                        stream.clear_window()
+                        if eng.device.type == "cuda":
+                            torch.cuda.synchronize()
+                        t1 = time.perf_counter()
+                        stream.run_until(warm + args.tp_docs)
+                        if eng.device.type == "cuda":
+                            torch.cuda.synchronize()
+                        dt = time.perf_counter() - t1
+                        res["docs_per_s"] = round(args.tp_docs / dt, 3)
+                        res["docs"], res["in_flight"] = args.tp_docs, args.tp_in_flight
+                        res["per_doc"] = {k: round(v, 2)
+                                          for k, v in validate(eng, stream.finished).items()}
+                        stream.close()
+                finally:
+                    if wctx.enabled:
+                        eng.shutdown()
+            elif eng.worker_loop(tolerate_car_errors=True):
+                car_err = "custom all-reduce flag timeouts on a follower rank"
+            if eng.device.type == "cuda":
+                torch.cuda.synchronize()
+            res["status"] = "ok"
+        except CustomAllReduceError as e:
+            car_err = f"{type(e).__name__}: {str(e)[:200]}"
+            res["status"] = f"error: {car_err}"
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never fatal
+            res["status"] = f"error: {type(e).__name__}: {str(e)[:300]}"
+        eng = None
+        if attempt == 0 and wctx.enabled and _any_rank(wctx, car_err is not None):
+            # a custom all-reduce flag timed out on some rank (its sums may be stale):
+            # every rank drops the custom kernels and the group measures again on RCCL
+            note = car_err or "custom all-reduce flag timeouts on a peer rank"
+            res.clear()
+            res.update({"model": model, "parallelism": f"tp{wctx.world}",
+                        "car_fallback": note})
+            if wctx.car is not None:
+                wctx.car.close()
+                wctx.car = None
+            wctx.car_status = "runtime flag timeouts: group re-formed on RCCL"
+            gc.collect()
+            if torch.cuda.is_available():
+                torch.cuda.empty_cache()
+            continue
+        break
     timer.cancel()
     res["phase_s"] = round(time.perf_counter() - t0, 1)
     return res
+
+
+def _any_rank(wctx, flag: bool) -> bool:
+    """True on every rank of the TP group if ``flag`` is set on any of them."""
+    import torch
+    import torch.distributed as dist
+
+    dev = "cuda" if dist.get_backend(wctx.group) == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=wctx.group)
+    return int(t.item()) == 1
 
 
 def main():

@@ -32,7 +32,7 @@ from ..models.config import get_config
 from ..models.llama import DecoderLM
 from ..parallel.tp import SINGLE, TPContext
 from ..utils.config import EngineConfig
-from ..utils.faults import FaultInjector
+from ..utils.faults import CustomAllReduceError, FaultInjector
 from ..utils.trace import trace_range
 from .grammar import PROFILE_REFERENCE, PROFILE_SYNTHETIC, get_grammar
 from .kv_cache import KVCache
@@ -129,7 +129,13 @@ class LLMEngine:
         self.faults = FaultInjector()
         self.pinned_blocks = 0
         if self.cfg.prefix_cache and self.cfg.warm_prefix and tp.rank == 0:
-            self.warm_prefix()
+            try:
+                self.warm_prefix()
+            except BaseException:
+                # the followers are mirroring the warm-up: release them before the
+                # caller sees the failure (it may rebuild the group, bench.py)
+                self.runner.stop_workers()
+                raise
 
     def warm_prefix(self, ids: list[int] | None = None) -> int:
         """prefill the shared system + template prefix once
@@ -309,10 +315,23 @@ class LLMEngine:
         return self.tokenizer.decode(seq.output_ids)
 
     # ------------------------------------------------------------------- TP
-    def worker_loop(self) -> None:
-        """Non-zero TP ranks: mirror rank 0's steps until told to stop."""
-        while self.runner.worker_step():
-            pass
+    def worker_loop(self, tolerate_car_errors: bool = False) -> bool:
+        """Non-zero TP ranks: mirror rank 0's steps until told to stop.
+
+        ``tolerate_car_errors``: a custom all-reduce flag timeout on this rank (raised
+        after the step's device work, so the rank is still in step with rank 0) is
+        recorded and mirroring continues; rank 0, whose own all-reduces then time out
+        on this rank's silent kernels, ends the group and the caller decides (bench.py
+        re-forms it on RCCL).  Returns True if such an error was seen."""
+        failed = False
+        while True:
+            try:
+                if not self.runner.worker_step():
+                    return failed
+            except CustomAllReduceError:
+                if not tolerate_car_errors:
+                    raise
+                failed = True
 
     def shutdown(self) -> None:
         self.runner.stop_workers()

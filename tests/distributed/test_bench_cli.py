@@ -276,3 +276,24 @@ def test_bench_default_gpus8_flow_gloo():
     assert tpl["parallelism"] == "tp8" and tpl["p50_parse_text_latency_s"] > 0
     assert isinstance(tpl["car_status"], str) and tpl["car_status"]
     assert "status" in out["engine"]["affinity"]
+
+
+def test_bench_tp_latency_car_fallback():
+    """A custom all-reduce flag timeout in the TP phase (injected on rank 0: RFQ_FAULT
+    car_error fires only while the custom all-reduce is configured) re-forms the group
+    on RCCL-path all-reduces and measures again: the phase still reports its numbers,
+    says why it fell back, and the DP docs/s fields stand."""
+    os.environ["RFQ_FAULT"] = "car_error:3"
+    try:
+        out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                    "--model", "tiny-llama", "--tp-latency-model", "tiny-llama-tp",
+                    "--tp-latency-runs", "2", "--tp-docs", "2", "--tp-in-flight", "2"] + SMALL)
+    finally:
+        os.environ.pop("RFQ_FAULT", None)
+    tpl = out["tp_latency"]
+    assert tpl["status"] == "ok", tpl
+    assert "injected flag timeout" in tpl["car_fallback"], tpl
+    assert tpl["custom_allreduce"] is False and "re-formed on RCCL" in tpl["car_status"]
+    assert tpl["runs"] == 2 and tpl["p50_parse_text_latency_s"] > 0
+    assert tpl["docs"] == 2 and tpl["per_doc"]["valid"] == 1.0
+    assert out["value"] > 0
