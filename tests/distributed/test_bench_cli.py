@@ -297,3 +297,31 @@ def test_bench_tp_latency_car_fallback():
     assert tpl["runs"] == 2 and tpl["p50_parse_text_latency_s"] > 0
     assert tpl["docs"] == 2 and tpl["per_doc"]["valid"] == 1.0
     assert out["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_tp_latency_car_fallback_one_gpu():
+    """The RCCL fallback on the GPU path: two ranks share one MI355X over gloo with the
+    custom IPC all-reduce live; an injected flag timeout on rank 0 makes every rank close
+    its custom all-reduce region and rebuild the TP engine without it."""
+    import torch
+
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    env_extra = {"RFQ_DIST_BACKEND": "gloo", "RFQ_FAULT": "car_error:3"}
+    os.environ.update(env_extra)
+    try:
+        out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                    "--model", "tiny-llama", "--kv-fraction", "0.05", "--no-graphs",
+                    "--tp-latency-model", "tiny-llama-tp", "--tp-latency-runs", "2",
+                    "--tp-docs", "4", "--tp-in-flight", "2"] + SMALL,
+                   timeout=380)
+    finally:
+        for k in env_extra:
+            os.environ.pop(k, None)
+    tpl = out["tp_latency"]
+    assert tpl["status"] == "ok", tpl
+    assert "injected flag timeout" in tpl["car_fallback"], tpl
+    assert tpl["custom_allreduce"] is False and tpl["p50_parse_text_latency_s"] > 0
+    assert tpl["per_doc"]["valid"] == 1.0
