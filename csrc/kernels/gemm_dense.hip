@@ -457,9 +457,10 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   // its diagnostic timing builds (WRONG results): 16 no DMA, 32 no fragment reads, 64 no
   // waits / barriers in the K loop; 128: the DMA pieces spread over all 16 MFMA groups;
   // bits 8-9: row tiles per L2 group (16, 8, 4, 32); bit 10 (with 128): fragment reads
-  // early in each half; bit 11 (with 128 | 1024): the 32x32x16 MFMA form
+  // early in each half; bit 11 (with 128 | 1024): the 32x32x16 MFMA form; bit 12 (with
+  // 128 | 1024, not 2048): the weight image in three LDS slots, the activations in two
   if (cfg & 8) {
-    launch_gemm_w4(x, ldx, w, ldw, out, ldo, M, n_out, K, up_off, swiglu, (cfg >> 4) & 255, s);
+    launch_gemm_w4(x, ldx, w, ldw, out, ldo, M, n_out, K, up_off, swiglu, (cfg >> 4) & 511, s);
     return;
   }
   // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile;

@@ -65,7 +65,12 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 // 32 = mfma_f32_32x32x16_bf16 (4 x 4 of 32 x 32).  A 32x32x16 MFMA holds the SIMD for 32
 // cycles, twice the 16x16x32's 16, so a DMA piece's issue (~16-23 cycles) hides behind
 // one MFMA instead of stalling the pipe.
-template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false, int MF = 16>
+// W3 (MF 16 with SPREAD + EARLY): the W image gets three LDS slots and the X image two
+// (160 KB): W pieces go out two K-tiles ahead of their first reader instead of one
+// (the weights are the operand that misses L2; a panel of activations is shared by
+// every weight tile of its row group).
+template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false, int MF = 16,
+          bool W3 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
@@ -121,13 +126,18 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     }
     w_soff[q] = __builtin_amdgcn_readfirstlane(n0 * (int)ldw * 2);
   }
+  // operand image bases: W3: W slots 0..2 then X slots 0..1; else stage s = {W, X}
+  auto wbase = [&](int slot) { return W3 ? lds + slot * (kW4Img * 2) : lds + slot * kW4StageB; };
+  auto xbase = [&](int slot) {
+    return W3 ? lds + 3 * (kW4Img * 2) + slot * (kW4Img * 2) : lds + slot * kW4StageB + kW4Img * 2;
+  };
   auto dma_w = [&](int q, int stage, int k0) {      // k0: element offset of the K-tile
-    w4_lds_c* const st = lds + stage * kW4StageB;
+    w4_lds_c* const st = wbase(stage);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(st + (8 * wid + q) * 1024), 16,
                                              w_voff[q & 1], w_soff[q] + 2 * k0, 0, 0);
   };
   auto dma_x = [&](int q, int stage, int k0) {
-    w4_lds_c* const st = lds + stage * kW4StageB + kW4Img * 2;
+    w4_lds_c* const st = xbase(stage);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(st + (8 * wid + q) * 1024), 16,
                                              x_voff[q], 2 * k0, 0, 0);
   };
@@ -148,7 +158,7 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
        MF == 16 ? 0 : r32 * 128 + 16 * ((2 + k32) ^ sw32)},
       {MF == 16 ? rr * 128 + 16 * ((4 + kq) ^ sw) : r32 * 128 + 16 * ((4 + k32) ^ sw32),
        MF == 16 ? 0 : r32 * 128 + 16 * ((6 + k32) ^ sw32)}};
-  const int wo = 16384 * wn, xo = kW4Img * 2 + 16384 * wm;
+  const int wo = 16384 * wn, xo = 16384 * wm;
   constexpr int SUB = MF == 16 ? 2048 : 4096;       // bytes between subtiles
 
   f32x4 acc[MF == 16 ? 8 : 1][MF == 16 ? 8 : 1];   // MF 16: [W subtile i][X subtile j]
@@ -179,14 +189,17 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   // One k-half: 64 MFMAs on `cur`, 16 fragment reads into `nxt` (k-half NH of the K-tile
   // in stage RS), and (DM) the 16 DMA pieces of K-tile k3 into stage S3, two per group in
   // the first 8 groups.
+  // W3: rs = W slot, rx = X slot, s3 / k3 the X DMA's slot / K-tile, DW / sw / kw the
+  // W DMA's; otherwise rs = rx = the stage and one DMA (s3, k3) covers both images.
   auto half = [&](s16x8 (&cur)[16], s16x8 (&nxt)[16], auto RD, auto NH, int rs, auto DM,
-                  int s3, int k3) {
+                  int s3, int k3, int rx, auto DW, int sw, int kw) {
     constexpr bool rd = decltype(RD)::value, dm = decltype(DM)::value;
+    constexpr bool dw = decltype(DW)::value;
     constexpr int nh = decltype(NH)::value;
-    w4_lds_c* const pw = lds + rs * kW4StageB + wo + lo[nh][0];
-    w4_lds_c* const px = lds + rs * kW4StageB + xo + lo[nh][0];
-    w4_lds_c* const pw1 = lds + rs * kW4StageB + wo + lo[nh][1];   // MF 32, k-step 1
-    w4_lds_c* const px1 = lds + rs * kW4StageB + xo + lo[nh][1];
+    w4_lds_c* const pw = wbase(rs) + wo + lo[nh][0];
+    w4_lds_c* const px = xbase(rx) + xo + lo[nh][0];
+    w4_lds_c* const pw1 = wbase(rs) + wo + lo[nh][1];   // MF 32, k-step 1
+    w4_lds_c* const px1 = xbase(rx) + xo + lo[nh][1];
 #define W4_MFMA(G, JJ)                                                                     \
     {                                                                                     \
       if constexpr (MF == 16) {                                                           \
@@ -224,7 +237,8 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
       if constexpr (dm && !(ABL & 1)) {                                                   \
         if constexpr (SPREAD) {                 /* X first: fewer blocks share it */     \
           if constexpr ((G) < 8) dma_x(G, s3, k3);                                        \
-          else dma_w((G) & 7, s3, k3);                                                    \
+          else if constexpr (!W3) dma_w((G) & 7, s3, k3);                                 \
+          else if constexpr (dw) dma_w((G) & 7, sw, kw);                                  \
         } else if constexpr ((G) < 8) {                                                   \
           dma(G, s3, k3);                                                                 \
         }                                                                                 \
@@ -255,9 +269,11 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   // the boundary inside K-tile t: K-tile t+1's DMA (own pieces) landed, k-half 1's
   // fragments landed, one barrier (every wave: the same, and done reading stage t's
   // image, which K-tile t+2's DMA overwrites next)
-  auto mid = [&]() {
+  auto mid = [&](auto VM8) {
     if constexpr (!(ABL & 4)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // W3: the 8 youngest pieces are the W DMA two K-tiles ahead: leave them in flight
+      if constexpr (decltype(VM8)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wait_frags(f1);
       __builtin_amdgcn_s_barrier();
     } else {
@@ -272,6 +288,22 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   using H1 = std::integral_constant<int, 1>;
   const int nk = K / 64;
   // ---- prologue: K-tiles 0 and 1 in flight, tile 0 landed, its k-half 0 read
+  // (W3: W tiles 0-2 and X tiles 0-1, issued W0 X0 X1 W1 W2 for the counted waits)
+  if constexpr (W3) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(q, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma_x(q, 1, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma_w(q, 1, 64);
+    if (nk > 2) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dma_w(q, 2, 128);
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    }
+  } else {
 #pragma unroll
   for (int q = 0; q < 8; ++q) dma(q, 0, 0);
   if (nk > 1) {
@@ -281,11 +313,12 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (MF == 16) {
-    w4_lds_c* const pw = lds + wo + lo[0][0];
-    w4_lds_c* const px = lds + xo + lo[0][0];
+    w4_lds_c* const pw = wbase(0) + wo + lo[0][0];
+    w4_lds_c* const px = xbase(0) + xo + lo[0][0];
     W4_READ(f0[0], pw, 0);     W4_READ(f0[1], pw, 2048);  W4_READ(f0[2], pw, 4096);
     W4_READ(f0[3], pw, 6144);  W4_READ(f0[4], pw, 8192);  W4_READ(f0[5], pw, 10240);
     W4_READ(f0[6], pw, 12288); W4_READ(f0[7], pw, 14336);
@@ -293,10 +326,10 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     W4_READ(f0[11], px, 6144); W4_READ(f0[12], px, 8192); W4_READ(f0[13], px, 10240);
     W4_READ(f0[14], px, 12288); W4_READ(f0[15], px, 14336);
   } else {
-    w4_lds_c* const pw = lds + wo + lo[0][0];
-    w4_lds_c* const px = lds + xo + lo[0][0];
-    w4_lds_c* const pw1 = lds + wo + lo[0][1];
-    w4_lds_c* const px1 = lds + xo + lo[0][1];
+    w4_lds_c* const pw = wbase(0) + wo + lo[0][0];
+    w4_lds_c* const px = xbase(0) + xo + lo[0][0];
+    w4_lds_c* const pw1 = wbase(0) + wo + lo[0][1];
+    w4_lds_c* const px1 = xbase(0) + xo + lo[0][1];
     W4_READ(f0[0], pw, 0);      W4_READ(f0[1], pw1, 0);     W4_READ(f0[2], pw, 4096);
     W4_READ(f0[3], pw1, 4096);  W4_READ(f0[4], pw, 8192);   W4_READ(f0[5], pw1, 8192);
     W4_READ(f0[6], pw, 12288);  W4_READ(f0[7], pw1, 12288);
@@ -309,21 +342,49 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   // boundary, half 1 (MFMAs on f1, reads of K-tile t+1's half 0 into f0, DMA of t+2
   // into this stage)
   int t = 0;
+  using V8 = std::true_type;
+  if constexpr (W3) {
+    // K-tile t: half 0 on slot t % 3 / t % 2; mid leaves W(t+2) in flight; half 1 reads
+    // tile t+1 and issues X(t+2) into X slot t % 2 and W(t+3) into W slot t % 3
+    for (; t + 3 < nk; ++t) {
+      wait_frags(f0);
+      half(f0, f1, T_{}, H1{}, t % 3, F_{}, 0, 0, t & 1, F_{}, 0, 0);
+      mid(V8{});
+      half(f1, f0, T_{}, H0{}, (t + 1) % 3, T_{}, t & 1, (t + 2) * 64, (t + 1) & 1, T_{},
+           t % 3, (t + 3) * 64);
+    }
+    if (t + 2 < nk) {          // nk >= 4: X(t+2) still to come, no W
+      wait_frags(f0);
+      half(f0, f1, T_{}, H1{}, t % 3, F_{}, 0, 0, t & 1, F_{}, 0, 0);
+      mid(V8{});
+      half(f1, f0, T_{}, H0{}, (t + 1) % 3, T_{}, t & 1, (t + 2) * 64, (t + 1) & 1, F_{}, 0, 0);
+      ++t;
+    }
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, t % 3, F_{}, 0, 0, t & 1, F_{}, 0, 0);
+    mid(F_{});
+    half(f1, f0, T_{}, H0{}, (t + 1) % 3, F_{}, 0, 0, (t + 1) & 1, F_{}, 0, 0);
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, (t + 1) % 3, F_{}, 0, 0, (t + 1) & 1, F_{}, 0, 0);
+    mid(F_{});
+    half(f1, f0, F_{}, H0{}, 0, F_{}, 0, 0, 0, F_{}, 0, 0);
+  } else {
   for (; t + 2 < nk; ++t) {
     wait_frags(f0);
-    half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0);
-    mid();
-    half(f1, f0, T_{}, H0{}, (t + 1) & 1, T_{}, t & 1, (t + 2) * 64);
+    half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0, t & 1, F_{}, 0, 0);
+    mid(F_{});
+    half(f1, f0, T_{}, H0{}, (t + 1) & 1, T_{}, t & 1, (t + 2) * 64, (t + 1) & 1, F_{}, 0, 0);
   }
   // the last two K-tiles (nk is even): no more DMA
   wait_frags(f0);
-  half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0);
-  mid();
-  half(f1, f0, T_{}, H0{}, (t + 1) & 1, F_{}, 0, 0);
+  half(f0, f1, T_{}, H1{}, t & 1, F_{}, 0, 0, t & 1, F_{}, 0, 0);
+  mid(F_{});
+  half(f1, f0, T_{}, H0{}, (t + 1) & 1, F_{}, 0, 0, (t + 1) & 1, F_{}, 0, 0);
   wait_frags(f0);
-  half(f0, f1, T_{}, H1{}, (t + 1) & 1, F_{}, 0, 0);
-  mid();
-  half(f1, f0, F_{}, H0{}, 0, F_{}, 0, 0);
+  half(f0, f1, T_{}, H1{}, (t + 1) & 1, F_{}, 0, 0, (t + 1) & 1, F_{}, 0, 0);
+  mid(F_{});
+  half(f1, f0, F_{}, H0{}, 0, F_{}, 0, 0, 0, F_{}, 0, 0);
+  }
 
   // ---- epilogue.  MF 16: lane holds out[row0 + 128 wm + 16 j + rr][n0 + 16 i + 4 kq + 0..3];
   // MF 32: out[row0 + 128 wm + 32 j + (l & 31)][n0 + 32 i + 4 (l >> 5) + 8 vq + 0..3]
@@ -426,6 +487,16 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
     return;
   }
   const bool spread = abl & 8, early = abl & 64, mf32 = abl & 128;
+  if (spread && early && !mf32 && (abl & 256)) {   // W image in three LDS slots
+    constexpr int lds3 = 5 * kW4Img * 2;           // 160 KB
+    if (swiglu)
+      gemm_w4_kernel<kW4Swiglu, 0, true, true, 16, true><<<grid, 256, lds3, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    else
+      gemm_w4_kernel<kW4Store, 0, true, true, 16, true><<<grid, 256, lds3, s>>>(
+          x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr);
+    return;
+  }
   if (spread && early && mf32) {
     if (swiglu)
       gemm_w4_kernel<kW4Swiglu, 0, true, true, 32><<<grid, 256, kW4Lds, s>>>(

@@ -921,7 +921,8 @@ def test_skinny_gemm_short_k_tail(gpu, M, cfg, N, K):
     _close(y, x.float() @ w.float().t(), 2e-2, 1e-2, f"skinny tail M={M} cfg={cfg} K={K}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128, 8 | 128 | 512 | 1024, 8 | 128 | 512 | 1024 | 2048])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128, 8 | 128 | 512 | 1024, 8 | 128 | 512 | 1024 | 2048,
+                                 8 | 128 | 512 | 1024 | 4096])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 128), (256, 768, 1024),
                                    (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096),
@@ -946,7 +947,7 @@ def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128 | 512 | 1024 | 2048])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128 | 512 | 1024 | 2048, 8 | 128 | 512 | 1024 | 4096])
 def test_gemm_dense_identity_asymmetric(gpu, cfg):
     """A = I with an asymmetric B catches a transposed C write (§3)."""
     K = 256
