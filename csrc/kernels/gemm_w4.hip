@@ -456,6 +456,295 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
   }
   }
 }
+
+// Persistent form of the tuned kernel (cfg 5768 + bit 13; K % 256 == 0): one workgroup
+// per CU walks output tiles id, id + G, ... (G = grid), with one K-tile pipeline running
+// straight across tile boundaries: during the last three K-tiles of a tile the weight /
+// activation pieces of the NEXT tile's K-tiles 0-2 are issued into the slots that free
+// up, and the last half reads the next tile's first fragments, so the next tile's
+// prologue latency and this tile's epilogue stores overlap instead of adding up.  (The
+// non-persistent kernel pays ~80 µs of per-tile prologue + epilogue per launch on the
+// gate|up shape: the intercept of its time-vs-K line, where hipBLASLt's is ~0;
+// profiles/r4_gemm_w4.md.)  The last tile's "next" pieces re-read its own K-tiles 0-2
+// (harmless; drained before exit).  Slots: W 3 (g % 3, g = K-tile counter over all the
+// workgroup's tiles), X 2 (g % 2), 160 KB.
+template <int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
+                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
+                     int tiles_m, int tiles_n, int group_m) {
+  extern __shared__ __attribute__((aligned(16))) char smem_w4[];
+  w4_lds_c* const lds = (w4_lds_c*)smem_w4;
+  const int nwg = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int rr = lane & 15, kq = lane >> 4;
+  const int lrow = lane >> 3, lch = lane & 7;
+  auto src_chunk = [&](int p) { return lch ^ (((8 * p + lrow) >> 1) & 7); };
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
+  const int w_voff[2] = {(lrow * (int)ldw + 8 * src_chunk(0)) * 2,
+                         (lrow * (int)ldw + 8 * src_chunk(1)) * 2};
+  // tile id -> (row tile, weight tile): the same XCD remap and L2 groups as the
+  // one-tile kernel (G % 8 == 0, so id & 7 is this workgroup's XCD for every id)
+  auto tile_of = [&](int id, int& tm, int& tn) {
+    const int q8 = nwg >> 3, r8 = nwg & 7, xg = id & 7;
+    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (id >> 3);
+    const int per_group = group_m * tiles_n;
+    const int gid = wg / per_group, first_m = gid * group_m;
+    const int gm = min(tiles_m - first_m, group_m);
+    const int rin = wg - gid * per_group;
+    tm = first_m + rin % gm;
+    tn = rin / gm;
+  };
+  // a tile's DMA offsets: X rows (clamped to M - 1) with the tile's row offset folded in,
+  // W piece rows in SGPRs
+  auto addrs = [&](int id, int (&xv)[8], int (&ws)[8]) {
+    int tm, tn;
+    tile_of(id, tm, tn);
+    const int row0 = tm * kW4M, mv = min(M - row0, kW4M);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int p = 8 * wid + q;
+      xv[q] = ((row0 + min(8 * p + lrow, mv - 1)) * (int)ldx + 8 * src_chunk(p)) * 2;
+      int n0;
+      if constexpr (EPI == kW4Swiglu) {
+        const int i = (p >> 1) & 7, wc = p >> 4;
+        n0 = (i < 4 ? 0 : up_off) + tn * 128 + 64 * wc + 16 * (i & 3) + 8 * (p & 1);
+      } else {
+        n0 = tn * kW4N + 8 * p;
+      }
+      ws[q] = __builtin_amdgcn_readfirstlane(n0 * (int)ldw * 2);
+    }
+  };
+  auto wbase = [&](int slot) { return lds + slot * (kW4Img * 2); };
+  auto xbase = [&](int slot) { return lds + 3 * (kW4Img * 2) + slot * (kW4Img * 2); };
+  int xv_c[8], ws_c[8], xv_n[8], ws_n[8];
+  auto dma_w = [&](int q, int slot, int k0, const int (&ws)[8]) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(wbase(slot) + (8 * wid + q) * 1024),
+                                             16, w_voff[q & 1], ws[q] + 2 * k0, 0, 0);
+  };
+  auto dma_x = [&](int q, int slot, int k0, const int (&xv)[8]) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void_t*)(xbase(slot) + (8 * wid + q) * 1024),
+                                             16, xv[q], 2 * k0, 0, 0);
+  };
+
+  const int sw = (rr >> 1) & 7;
+  const int lo0 = rr * 128 + 16 * (kq ^ sw), lo1 = rr * 128 + 16 * ((4 + kq) ^ sw);
+  const int wo = 16384 * wn, xo = 16384 * wm;
+  constexpr int SUB = 2048;
+  f32x4 acc[8][8];
+  s16x8 f0[16], f1[16];
+  auto wait_frags = [&](s16x8 (&f)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]),
+                   "+v"(f[6]), "+v"(f[7]), "+v"(f[8]), "+v"(f[9]), "+v"(f[10]), "+v"(f[11]),
+                   "+v"(f[12]), "+v"(f[13]), "+v"(f[14]), "+v"(f[15]));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // One k-half: 64 MFMAs on `cur`; RD: 16 fragment reads of k-half NH from W slot rs / X
+  // slot rx into `nxt`; DX: X pieces of K-tile kx into X slot sx (NX: the next tile's),
+  // DW: W pieces of K-tile kw into W slot sw (NW: the next tile's).
+  auto half = [&](s16x8 (&cur)[16], s16x8 (&nxt)[16], auto RD, auto NH, int rs, int rx,
+                  auto DX, auto NXX, int sx, int kx, auto DW, auto NXW, int swl, int kw) {
+    constexpr bool rd = decltype(RD)::value, dx = decltype(DX)::value;
+    constexpr bool dw = decltype(DW)::value, nxx = decltype(NXX)::value;
+    constexpr bool nxw = decltype(NXW)::value;
+    constexpr int nh = decltype(NH)::value;
+    w4_lds_c* const pw = wbase(rs) + wo + (nh ? lo1 : lo0);
+    w4_lds_c* const px = xbase(rx) + xo + (nh ? lo1 : lo0);
+#define W4P_MFMA(G_, JJ)                                                                   \
+    {                                                                                     \
+      const int i = (G_) >> 1, j = ((G_) & 1) * 4 + (JJ);                                \
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(cur[i]),              \
+                                                          as_bf16x8(cur[8 + j]), acc[i][j], \
+                                                          0, 0, 0);                        \
+    }
+#define W4P_FRAG(F)                                                                       \
+    {                                                                                     \
+      if constexpr (rd) {                                                                 \
+        if constexpr ((F) < 8) W4_READ(nxt[F], pw, SUB * ((F) & 7));                      \
+        else W4_READ(nxt[F], px, SUB * ((F) & 7));                                        \
+      }                                                                                   \
+    }
+#define W4P_GROUP(G_)                                                                     \
+    {                                                                                     \
+      W4P_MFMA(G_, 0)                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr ((G_) < 8) {                                                           \
+        if constexpr (dx) dma_x(G_, sx, kx, nxx ? xv_n : xv_c);                           \
+      } else if constexpr (dw) {                                                          \
+        dma_w((G_) & 7, swl, kw, nxw ? ws_n : ws_c);                                      \
+      }                                                                                   \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      W4P_MFMA(G_, 1)                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr ((G_) < 8) W4P_FRAG(2 * (G_));                                         \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      W4P_MFMA(G_, 2)                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      if constexpr ((G_) < 8) W4P_FRAG(2 * (G_) + 1);                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+      W4P_MFMA(G_, 3)                                                                     \
+      __builtin_amdgcn_sched_barrier(0);                                                  \
+    }
+    W4P_GROUP(0) W4P_GROUP(1) W4P_GROUP(2) W4P_GROUP(3) W4P_GROUP(4) W4P_GROUP(5)
+    W4P_GROUP(6) W4P_GROUP(7) W4P_GROUP(8) W4P_GROUP(9) W4P_GROUP(10) W4P_GROUP(11)
+    W4P_GROUP(12) W4P_GROUP(13) W4P_GROUP(14) W4P_GROUP(15)
+#undef W4P_GROUP
+#undef W4P_MFMA
+#undef W4P_FRAG
+  };
+  // K-tile boundary: VM8 leaves the 8 youngest pieces (the W DMA two K-tiles ahead) in
+  // flight; after an epilogue (its stores are younger) everything is waited for
+  auto mid = [&](auto VM8) {
+    if constexpr (decltype(VM8)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_frags(f1);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  const int nk = K / 64;                          // >= 4, even
+
+  int id = blockIdx.x;
+  if (id >= nwg) return;
+  addrs(id, xv_c, ws_c);
+  addrs(id + G < nwg ? id + G : id, xv_n, ws_n);
+  // ---- first tile's prologue: W0 X0 X1 W1 W2 (slots W 0-2, X 0-1)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_w(q, 0, 0, ws_c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_x(q, 0, 0, xv_c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_x(q, 1, 64, xv_c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_w(q, 1, 64, ws_c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dma_w(q, 2, 128, ws_c);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    w4_lds_c* const pw = wbase(0) + wo + lo0;
+    w4_lds_c* const px = xbase(0) + xo + lo0;
+    W4_READ(f0[0], pw, 0);     W4_READ(f0[1], pw, 2048);  W4_READ(f0[2], pw, 4096);
+    W4_READ(f0[3], pw, 6144);  W4_READ(f0[4], pw, 8192);  W4_READ(f0[5], pw, 10240);
+    W4_READ(f0[6], pw, 12288); W4_READ(f0[7], pw, 14336);
+    W4_READ(f0[8], px, 0);     W4_READ(f0[9], px, 2048);  W4_READ(f0[10], px, 4096);
+    W4_READ(f0[11], px, 6144); W4_READ(f0[12], px, 8192); W4_READ(f0[13], px, 10240);
+    W4_READ(f0[14], px, 12288); W4_READ(f0[15], px, 14336);
+  }
+  int wofs = 0;                                   // W slot of this tile's K-tile 0
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K-tile 0 (its boundary waits for everything: the previous epilogue's stores are
+    // the youngest memory operations)
+    int t = 0;
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, wofs % 3, 0, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
+    mid(F_{});
+    half(f1, f0, T_{}, H0{}, (wofs + 1) % 3, 1, T_{}, F_{}, 0, 2 * 64, T_{}, F_{}, wofs % 3,
+         3 * 64);
+    for (t = 1; t + 3 < nk; ++t) {
+      wait_frags(f0);
+      half(f0, f1, T_{}, H1{}, (wofs + t) % 3, t & 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
+      mid(T_{});
+      half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, (t + 1) & 1, T_{}, F_{}, t & 1, (t + 2) * 64,
+           T_{}, F_{}, (wofs + t) % 3, (t + 3) * 64);
+    }
+    // t = nk-3: X(nk-1) of this tile, W(0) of the next
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
+    mid(T_{});
+    half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 0, T_{}, F_{}, 1, (nk - 1) * 64, T_{}, T_{},
+         (wofs + t) % 3, 0);
+    ++t;
+    // t = nk-2: X(0), W(1) of the next tile
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 0, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
+    mid(T_{});
+    half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 1, T_{}, T_{}, 0, 0, T_{}, T_{}, (wofs + t) % 3,
+         64);
+    ++t;
+    // t = nk-1: the last half issues the next tile's X(1), W(2); its K-tile 0 landed at
+    // this boundary, and its first fragments are read after the epilogue (reading them
+    // here would keep 64 more registers live through the stores)
+    wait_frags(f0);
+    half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
+    mid(T_{});
+    half(f1, f0, F_{}, H0{}, 0, 0, T_{}, T_{}, 1, 64, T_{}, T_{}, (wofs + t) % 3, 128);
+
+    // ---- epilogue of tile id (the next tile's pieces are in flight)
+    {
+      int tm, tn;
+      tile_of(id, tm, tn);
+      const int row0 = tm * kW4M, m_valid = min(M - row0, kW4M);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int trow = 128 * wm + 16 * j + rr;
+        if (trow >= m_valid) continue;
+        bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
+        if constexpr (EPI == kW4Swiglu) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float gf = bf2f(f2bf(acc[i][j][u]));
+              const float sg = gf / (1.f + __expf(-gf));
+              o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + i][j][u]));
+            }
+            uint2 v;
+            v.x = pack_bf16x2(o[0], o[1]);
+            v.y = pack_bf16x2(o[2], o[3]);
+            *reinterpret_cast<uint2*>(orow + tn * 128 + 64 * wn + 16 * i + 4 * kq) = v;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            uint2 v;
+            v.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+            v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+            *reinterpret_cast<uint2*>(orow + tn * kW4N + 128 * wn + 16 * i + 4 * kq) = v;
+          }
+        }
+      }
+    }
+    id += G;
+    if (id >= nwg) break;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      xv_c[q] = xv_n[q];
+      ws_c[q] = ws_n[q];
+    }
+    addrs(id + G < nwg ? id + G : id, xv_n, ws_n);
+    wofs = (wofs + nk) % 3;
+    {
+      w4_lds_c* const pw = wbase(wofs) + wo + lo0;
+      w4_lds_c* const px = xbase(0) + xo + lo0;
+      W4_READ(f0[0], pw, 0);     W4_READ(f0[1], pw, 2048);  W4_READ(f0[2], pw, 4096);
+      W4_READ(f0[3], pw, 6144);  W4_READ(f0[4], pw, 8192);  W4_READ(f0[5], pw, 10240);
+      W4_READ(f0[6], pw, 12288); W4_READ(f0[7], pw, 14336);
+      W4_READ(f0[8], px, 0);     W4_READ(f0[9], px, 2048);  W4_READ(f0[10], px, 4096);
+      W4_READ(f0[11], px, 6144); W4_READ(f0[12], px, 8192); W4_READ(f0[13], px, 10240);
+      W4_READ(f0[14], px, 12288); W4_READ(f0[15], px, 14336);
+    }
+  }
+  // the last tile's "next" pieces (its own K-tiles 0-2 again) land before the workgroup
+  // ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 #undef W4_READ
 
 // out = x w^T ([M, N]) or, swiglu, act = silu(x Wg^T) * (x Wu^T) ([M, F], w = [2F, K], up
@@ -487,6 +776,25 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
     return;
   }
   const bool spread = abl & 8, early = abl & 64, mf32 = abl & 128;
+  if (spread && early && !mf32 && (abl & 256) && (abl & 512) && K % 256 == 0 &&
+      (int64_t)M * ldx * 2 < (int64_t)1 << 31) {   // X offsets are 32-bit buffer offsets
+    // persistent: one workgroup per CU (160 KB of LDS each), at most one per tile
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n >= 8 ? n / 8 * 8 : 8;
+    }();
+    const int g = grid < ncu ? grid : ncu;
+    constexpr int lds3 = 5 * kW4Img * 2;
+    if (swiglu)
+      gemm_w4p_kernel<kW4Swiglu><<<g, 256, lds3, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                      tiles_m, tiles_n, gmr);
+    else
+      gemm_w4p_kernel<kW4Store><<<g, 256, lds3, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
+                                                     tiles_m, tiles_n, gmr);
+    return;
+  }
   if (spread && early && !mf32 && (abl & 256)) {   // W image in three LDS slots
     constexpr int lds3 = 5 * kW4Img * 2;           // 160 KB
     if (swiglu)

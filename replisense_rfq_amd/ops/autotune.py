@@ -430,11 +430,12 @@ def plan_splits(times: list[float], margin: float = 0.95, launch_us: float = 4.0
 LT_CANDIDATES = int(os.environ.get("RFQ_GEMM_LT_CANDIDATES", "6"))   # heuristic algorithms timed per (M bucket, N, K)
 # RFQ_GEMM_DENSE=0 keeps every large-M projection on hipBLASLt
 DENSE_ON = os.environ.get("RFQ_GEMM_DENSE", "1") != "0"
-# 2: gemm_dense's 8-wave ping-pong; 5768 = 8 | 128 | 512 | 1024 | 4096: gemm_w4 (one wave
-# per SIMD), DMA spread over the MFMA groups, 4 row tiles per L2 group, fragment reads
-# early in each half, the weight image in three LDS slots (1672 without the third slot;
-# profiles/r4_gemm_w4.md)
-DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,5768").split(","))
+# 2: gemm_dense's 8-wave ping-pong; 13960 = 8 | 128 | 512 | 1024 | 4096 | 8192: gemm_w4
+# (one wave per SIMD), DMA spread over the MFMA groups, 4 row tiles per L2 group, fragment
+# reads early in each half, the weight image in three LDS slots, persistent over output
+# tiles with the K-tile pipeline crossing tile boundaries (K % 256; otherwise the same
+# kernel without persistence, 5768; 1672 without the third slot; profiles/r4_gemm_w4.md)
+DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,13960").split(","))
 DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 

@@ -922,17 +922,19 @@ def test_skinny_gemm_short_k_tail(gpu, M, cfg, N, K):
 
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128, 8 | 128 | 512 | 1024, 8 | 128 | 512 | 1024 | 2048,
-                                 8 | 128 | 512 | 1024 | 4096])
+                                 8 | 128 | 512 | 1024 | 4096, 8 | 128 | 512 | 1024 | 4096 | 8192])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (100, 512, 128), (256, 768, 1024),
                                    (300, 1280, 8192), (513, 4096, 576), (2048, 1024, 4096),
-                                   (777, 2048, 512), (256, 512, 256)])
+                                   (777, 2048, 512), (256, 512, 256), (4000, 4608, 512)])
 def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     """The 256x256 8-wave MFMA GEMM (gemm_dense.hip) and the one-wave-per-SIMD kernel
     (cfg 8, gemm_w4.hip: K % 128 == 0) against the fp32 oracle, asymmetric operands, row
     tails (M % 256 != 0), one-tile and many-tile K loops (K 128 / 256: only the w4
     kernel's 4-step tail; 512: one steady iteration); swiglu vs the unfused GEMM ->
-    bf16 -> silu_mul rounding."""
+    bf16 -> silu_mul rounding.  4000 x 4608: 288 output tiles (256 of them with a
+    partial row tile), so the persistent form (cfg bit 13) runs two tiles on 32
+    workgroups with the K-tile pipeline crossing the tile boundary."""
     if cfg & 8 and K % 128:
         pytest.skip("the w4 kernel needs K % 128 == 0")
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
@@ -947,7 +949,8 @@ def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128 | 512 | 1024 | 2048, 8 | 128 | 512 | 1024 | 4096])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128 | 512 | 1024 | 2048, 8 | 128 | 512 | 1024 | 4096,
+                                 8 | 128 | 512 | 1024 | 4096 | 8192])
 def test_gemm_dense_identity_asymmetric(gpu, cfg):
     """A = I with an asymmetric B catches a transposed C write (§3)."""
     K = 256

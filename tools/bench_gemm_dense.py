@@ -28,6 +28,11 @@ SHAPES = {                     # name: (N, K, swiglu)
     "70b_tp8_o": (8192, 1024, False),
     "70b_tp8_gate_up+swiglu": (7168, 8192, True),
     "70b_tp8_down": (8192, 3584, False),
+    # K sweeps of the gate_up panel: the intercept of time vs K is the per-tile
+    # prologue / epilogue cost (a K-independent part of every output tile)
+    "gu_k1024": (28672, 1024, False),
+    "gu_k2048": (28672, 2048, False),
+    "gu_k8192": (28672, 8192, False),
 }
 
 
