@@ -487,6 +487,9 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
       __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
+  // output: num_records = M rows, so a store to a row past M is dropped
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, M * (int)ldo * 2, 0x00020000);
   const int w_voff[2] = {(lrow * (int)ldw + 8 * src_chunk(0)) * 2,
                          (lrow * (int)ldw + 8 * src_chunk(1)) * 2};
   // tile id -> (row tile, weight tile): the same XCD remap and L2 groups as the
@@ -601,8 +604,9 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   };
   // K-tile boundary: VM8 leaves the 8 youngest pieces (the W DMA two K-tiles ahead) in
   // flight; after an epilogue (its stores are younger) everything is waited for
-  auto mid = [&](auto VM8) {
-    if constexpr (decltype(VM8)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  auto mid = [&](auto VM) {
+    if constexpr (decltype(VM)::value == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (decltype(VM)::value == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wait_frags(f1);
     __builtin_amdgcn_s_barrier();
@@ -612,6 +616,8 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   using F_ = std::false_type;
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
+  using V8 = std::integral_constant<int, 8>;
+  using V40 = std::integral_constant<int, 40>;
   const int nk = K / 64;                          // >= 4, even
 
   int id = blockIdx.x;
@@ -629,7 +635,9 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   for (int q = 0; q < 8; ++q) dma_w(q, 1, 64, ws_c);
 #pragma unroll
   for (int q = 0; q < 8; ++q) dma_w(q, 2, 128, ws_c);
-  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  // X1 / W1 landed too (W2 in flight): K-tile 0's boundary below waits vmcnt(40), which
+  // is what a continued tile needs and a no-op here
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   {
@@ -648,32 +656,33 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // K-tile 0 (its boundary waits for everything: the previous epilogue's stores are
-    // the youngest memory operations)
+    // K-tile 0: K-tile 1 must have landed; younger than its pieces are W(2) and the
+    // previous tile's 32 epilogue stores (a fixed count: rows past M are clipped by the
+    // output buffer's range, not skipped), so they stay in flight
     int t = 0;
     wait_frags(f0);
     half(f0, f1, T_{}, H1{}, wofs % 3, 0, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
-    mid(F_{});
+    mid(V40{});
     half(f1, f0, T_{}, H0{}, (wofs + 1) % 3, 1, T_{}, F_{}, 0, 2 * 64, T_{}, F_{}, wofs % 3,
          3 * 64);
     for (t = 1; t + 3 < nk; ++t) {
       wait_frags(f0);
       half(f0, f1, T_{}, H1{}, (wofs + t) % 3, t & 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
-      mid(T_{});
+      mid(V8{});
       half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, (t + 1) & 1, T_{}, F_{}, t & 1, (t + 2) * 64,
            T_{}, F_{}, (wofs + t) % 3, (t + 3) * 64);
     }
     // t = nk-3: X(nk-1) of this tile, W(0) of the next
     wait_frags(f0);
     half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
-    mid(T_{});
+    mid(V8{});
     half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 0, T_{}, F_{}, 1, (nk - 1) * 64, T_{}, T_{},
          (wofs + t) % 3, 0);
     ++t;
     // t = nk-2: X(0), W(1) of the next tile
     wait_frags(f0);
     half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 0, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
-    mid(T_{});
+    mid(V8{});
     half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 1, T_{}, T_{}, 0, 0, T_{}, T_{}, (wofs + t) % 3,
          64);
     ++t;
@@ -682,19 +691,25 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     // here would keep 64 more registers live through the stores)
     wait_frags(f0);
     half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
-    mid(T_{});
+    mid(V8{});
     half(f1, f0, F_{}, H0{}, 0, 0, T_{}, T_{}, 1, 64, T_{}, T_{}, (wofs + t) % 3, 128);
 
-    // ---- epilogue of tile id (the next tile's pieces are in flight)
+    // ---- epilogue of tile id (the next tile's pieces are in flight).  Exactly 32 stores
+    // per wave: buffer stores whose rows past M fall outside the output range and are
+    // dropped; plain outputs pair two lanes' 8-byte runs into 16-byte stores (the
+    // partner is lane ^ 16: ds_swizzle xor 0x10).
     {
       int tm, tn;
       tile_of(id, tm, tn);
-      const int row0 = tm * kW4M, m_valid = min(M - row0, kW4M);
+      const int row0 = tm * kW4M;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        // a never-taken, opaque branch per row block keeps the compiler from hoisting
+        // every block's accumulator reads to the top (that spilled); the store count
+        // stays fixed, which the next tile's vmcnt(40) relies on
+        if (__builtin_amdgcn_readfirstlane(nk + j) < 0) continue;
         const int trow = 128 * wm + 16 * j + rr;
-        if (trow >= m_valid) continue;
-        bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
+        const int rowb = (row0 + trow) * (int)ldo * 2;        // byte offset of the row
         if constexpr (EPI == kW4Swiglu) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -705,18 +720,30 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
               const float sg = gf / (1.f + __expf(-gf));
               o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + i][j][u]));
             }
-            uint2 v;
-            v.x = pack_bf16x2(o[0], o[1]);
-            v.y = pack_bf16x2(o[2], o[3]);
-            *reinterpret_cast<uint2*>(orow + tn * 128 + 64 * wn + 16 * i + 4 * kq) = v;
+            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+            const u32x2_t v2 = {pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+            const int col = tn * 128 + 64 * wn + 16 * i + 4 * kq;
+            __builtin_amdgcn_raw_buffer_store_b64(v2, orsrc, rowb + col * 2, 0, 0);
           }
         } else {
+          const bool odd = kq & 1;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            uint2 v;
-            v.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-            v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-            *reinterpret_cast<uint2*>(orow + tn * kW4N + 128 * wn + 16 * i + 4 * kq) = v;
+          for (int pr = 0; pr < 4; ++pr) {
+            const uint32_t a0 = pack_bf16x2(acc[2 * pr][j][0], acc[2 * pr][j][1]);
+            const uint32_t a1 = pack_bf16x2(acc[2 * pr][j][2], acc[2 * pr][j][3]);
+            const uint32_t b0 = pack_bf16x2(acc[2 * pr + 1][j][0], acc[2 * pr + 1][j][1]);
+            const uint32_t b1 = pack_bf16x2(acc[2 * pr + 1][j][2], acc[2 * pr + 1][j][3]);
+            // even kq keeps subtile 2 pr (its 4 columns + the partner's next 4), odd kq
+            // subtile 2 pr + 1 (the partner's 4 columns + its own)
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(odd ? a0 : b0), 0x401F);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(odd ? a1 : b1), 0x401F);
+            u32x4 v;
+            v[0] = odd ? r0 : a0;
+            v[1] = odd ? r1 : a1;
+            v[2] = odd ? b0 : r0;
+            v[3] = odd ? b1 : r1;
+            const int col = tn * kW4N + 128 * wn + 16 * (2 * pr + (odd ? 1 : 0)) + 4 * (kq & 2);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, rowb + col * 2, 0, 0);
           }
         }
       }
@@ -777,7 +804,8 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
   }
   const bool spread = abl & 8, early = abl & 64, mf32 = abl & 128;
   if (spread && early && !mf32 && (abl & 256) && (abl & 512) && K % 256 == 0 &&
-      (int64_t)M * ldx * 2 < (int64_t)1 << 31) {   // X offsets are 32-bit buffer offsets
+      (int64_t)M * ldx * 2 < (int64_t)1 << 31 &&   // X / output offsets are 32-bit buffer
+      (int64_t)M * ldo * 2 < (int64_t)1 << 31) {   // offsets
     // persistent: one workgroup per CU (160 KB of LDS each), at most one per tile
     static const int ncu = [] {
       int dev = 0, n = 0;
