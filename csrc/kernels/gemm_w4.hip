@@ -607,6 +607,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   auto mid = [&](auto VM) {
     if constexpr (decltype(VM)::value == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (decltype(VM)::value == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+    else if constexpr (decltype(VM)::value == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wait_frags(f1);
     __builtin_amdgcn_s_barrier();
@@ -617,7 +618,8 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
   using V8 = std::integral_constant<int, 8>;
-  using V40 = std::integral_constant<int, 40>;
+  // W(2) + this wave's epilogue stores per tile (plain 32, SwiGLU 16; all 16 bytes)
+  using V40 = std::integral_constant<int, EPI == kW4Swiglu ? 24 : 40>;
   const int nk = K / 64;                          // >= 4, even
 
   int id = blockIdx.x;
@@ -635,8 +637,8 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   for (int q = 0; q < 8; ++q) dma_w(q, 1, 64, ws_c);
 #pragma unroll
   for (int q = 0; q < 8; ++q) dma_w(q, 2, 128, ws_c);
-  // X1 / W1 landed too (W2 in flight): K-tile 0's boundary below waits vmcnt(40), which
-  // is what a continued tile needs and a no-op here
+  // X1 / W1 landed too (W2 in flight): K-tile 0's boundary below waits vmcnt(40 / 24),
+  // which is what a continued tile needs and a no-op here
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -657,7 +659,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // K-tile 0: K-tile 1 must have landed; younger than its pieces are W(2) and the
-    // previous tile's 32 epilogue stores (a fixed count: rows past M are clipped by the
+    // previous tile's epilogue stores (32, SwiGLU 16) (a fixed count: rows past M are clipped by the
     // output buffer's range, not skipped), so they stay in flight
     int t = 0;
     wait_frags(f0);
@@ -694,10 +696,10 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     mid(V8{});
     half(f1, f0, F_{}, H0{}, 0, 0, T_{}, T_{}, 1, 64, T_{}, T_{}, (wofs + t) % 3, 128);
 
-    // ---- epilogue of tile id (the next tile's pieces are in flight).  Exactly 32 stores
-    // per wave: buffer stores whose rows past M fall outside the output range and are
-    // dropped; plain outputs pair two lanes' 8-byte runs into 16-byte stores (the
-    // partner is lane ^ 16: ds_swizzle xor 0x10).
+    // ---- epilogue of tile id (the next tile's pieces are in flight).  A fixed number of
+    // stores per wave (32, SwiGLU 16): buffer stores whose rows past M fall outside the
+    // output range and are dropped; two lanes' 8-byte runs are paired into one 16-byte
+    // store each (the partner is lane ^ 16: ds_swizzle xor 0x10).
     {
       int tm, tn;
       tile_of(id, tm, tn);
@@ -710,23 +712,34 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
         if (__builtin_amdgcn_readfirstlane(nk + j) < 0) continue;
         const int trow = 128 * wm + 16 * j + rr;
         const int rowb = (row0 + trow) * (int)ldo * 2;        // byte offset of the row
+        const bool odd = kq & 1;
         if constexpr (EPI == kW4Swiglu) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float o[4];
+          for (int pr = 0; pr < 2; ++pr) {
+            uint32_t h[2][2];                     // [subtile 2 pr + e][dword]
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const float gf = bf2f(f2bf(acc[i][j][u]));
-              const float sg = gf / (1.f + __expf(-gf));
-              o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + i][j][u]));
+            for (int e = 0; e < 2; ++e) {
+              float o[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const float gf = bf2f(f2bf(acc[2 * pr + e][j][u]));
+                const float sg = gf / (1.f + __expf(-gf));
+                o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + 2 * pr + e][j][u]));
+              }
+              h[e][0] = pack_bf16x2(o[0], o[1]);
+              h[e][1] = pack_bf16x2(o[2], o[3]);
             }
-            typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-            const u32x2_t v2 = {pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-            const int col = tn * 128 + 64 * wn + 16 * i + 4 * kq;
-            __builtin_amdgcn_raw_buffer_store_b64(v2, orsrc, rowb + col * 2, 0, 0);
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(odd ? h[0][0] : h[1][0]), 0x401F);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(odd ? h[0][1] : h[1][1]), 0x401F);
+            u32x4 v;
+            v[0] = odd ? r0 : h[0][0];
+            v[1] = odd ? r1 : h[0][1];
+            v[2] = odd ? h[1][0] : r0;
+            v[3] = odd ? h[1][1] : r1;
+            const int col = tn * 128 + 64 * wn + 16 * (2 * pr + (odd ? 1 : 0)) + 4 * (kq & 2);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, rowb + col * 2, 0, 0);
           }
         } else {
-          const bool odd = kq & 1;
 #pragma unroll
           for (int pr = 0; pr < 4; ++pr) {
             const uint32_t a0 = pack_bf16x2(acc[2 * pr][j][0], acc[2 * pr][j][1]);
