@@ -546,6 +546,21 @@ def _dense_cfg(M: int, N: int, K: int, swiglu: bool = False) -> int:
     return sel[-1] if len(sel) > 1 else -1        # past the tuned range: the largest bucket
 
 
+def _hybrid_rows(M: int, N: int, K: int) -> tuple[int, int]:
+    """(rows on the hand-written kernel, its cfg) for the plan's hybrid split of this M
+    bucket (ops.autotune.plan_hybrid), or (0, -1)."""
+    p = _SPLIT_PLAN.get((N, K))
+    if p is None or len(p) < 6:
+        return 0, -1
+    q, hyb = p[0], p[5]
+    j = -(-M // q)
+    h = hyb[j] if j < len(hyb) else 0
+    if not h:
+        return 0, -1
+    m1 = h[0] * q
+    return (m1, h[1]) if 0 < m1 < M else (0, -1)
+
+
 def swiglu_large(x, w):
     """act[M, F] = silu(x Wg^T) * (x Wu^T) for large M in one hand-written MFMA GEMM with
     the SwiGLU epilogue (gemm_dense.hip) when the start-up plan measured it faster than
@@ -610,6 +625,12 @@ def linear(x, w, out=None, plan: int | None = None):
             dc = _dense_cfg(M, N, K)
             if dc >= 0 and out.stride(1) == 1 and out.stride(0) % 4 == 0:
                 _native.ops().gemm_dense(x, w, out, False, dc)
+                return out
+            m1, hc = _hybrid_rows(M, N, K)
+            if m1 > 0 and out.stride(1) == 1 and out.stride(0) % 4 == 0:
+                # whole rounds of the hand-written kernel's tiles, the rest on the library
+                _native.ops().gemm_dense(x[:m1], w, out[:m1], False, hc)
+                _lt_or_torch(x[m1:], w, out[m1:])
                 return out
             rows = split_chunks(M, N, K) or [M]
             a = 0

@@ -439,6 +439,31 @@ DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,1396
 DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 
+def plan_hybrid(t_lib: list, t_dense: list, tiles_n: int, quantum: int = 256,
+                launch_us: float = 4.0, margin: float = DENSE_MARGIN) -> list:
+    """Row split of a large-M GEMM between the hand-written persistent kernel and the
+    library.  The hand-written kernel runs whole rounds of 256 x 256 tiles on the 256 CUs
+    only when its row-tile count times ``tiles_n`` is a multiple of 256; its last, partly
+    filled round is what the library's stream-K split avoids.  So for bucket j (j
+    quanta of rows) try: the first m1 rows (a multiple of one full round) on the
+    hand-written kernel, the rest on the library.  ``t_lib[j]`` / ``t_dense[j]``: µs of
+    j quanta on each (index 0 unused; inf where not measured).  Returns ``hyb[j]`` = m1
+    quanta, or 0 where one kernel alone is at least as fast (margin)."""
+    import math
+
+    J = len(t_lib) - 1
+    round_tiles = 256 // math.gcd(256, tiles_n)          # row tiles per full round
+    step = max(1, round_tiles * 256 // quantum)          # in quanta
+    hyb = [0] * (J + 1)
+    for j in range(1, J + 1):
+        best = min(t_lib[j], t_dense[j])
+        for m1 in range(step, j, step):
+            t = t_dense[m1] + t_lib[j - m1] + launch_us
+            if t < margin * best:
+                best, hyb[j] = t, m1
+    return hyb
+
+
 def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], quantum: int = 256,
                reps: int = 3) -> tuple[dict, list]:
     """For each projection and every multiple of ``quantum`` rows up to ``max_m[name]``:
@@ -480,6 +505,9 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
         # GEMM + silu_mul vs the same kernel with the SwiGLU epilogue
         dense = [-1] * (J + 1)
         swi = [-1] * (J + 1)
+        t_dense = [float("inf")] * (J + 1)         # best hand-written time per bucket
+        c_dense = [-1] * (J + 1)                   # and its cfg
+        t_lib_j = [float("inf")] * (J + 1)
         n_dense = n_swi = 0
         if DENSE_ON and gemm_dense_ok(quantum, N, K):
             act = torch.empty(J * quantum, N // 2, device=w.device, dtype=w.dtype) \
@@ -489,11 +517,14 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                 t_lib = times[j] if table[j] is None else \
                     sum(times[c] for c in table[j]) + 4.0 * (len(table[j]) - 1)
                 best_c, t_best = -1, t_lib * DENSE_MARGIN
+                t_lib_j[j] = t_lib
                 for c in DENSE_CFGS:
                     if c & 8 and K % 128:            # gemm_w4 needs K % 128 == 0
                         continue
                     t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, out[:m], False, c),
                               [w], reps, graph=False)
+                    if t < t_dense[j]:
+                        t_dense[j], c_dense[j] = t, c
                     if t < t_best:
                         best_c, t_best = c, t
                 dense[j] = best_c
@@ -517,12 +548,21 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                 report.append(("dense:" + name, m, N, K, round(t_lib, 1),
                                f"dense{best_c}" if best_c >= 0 else "lib", round(t_best, 1)))
             del act
-        plan[(N, K)] = (quantum, table, algos, dense, swi)
+        # rows split between a whole number of the hand-written kernel's rounds and the
+        # library (plain GEMMs; buckets where one kernel alone was not beaten stay so)
+        hyb = [0] * (J + 1)
+        if DENSE_ON and any(c >= 0 for c in c_dense) and os.environ.get("RFQ_GEMM_HYBRID", "1") != "0":
+            hyb = plan_hybrid(t_lib_j, t_dense, N // 256, quantum)
+            hyb = [(m1, c_dense[m1]) if m1 > 0 and c_dense[m1] >= 0 and dense[j] < 0 else 0
+                   for j, m1 in enumerate(hyb)]
+        n_hyb = sum(1 for h in hyb if h)
+        plan[(N, K)] = (quantum, table, algos, dense, swi, hyb)
         report.append(("lt:" + name, J * quantum, N, K, J, f"{n_lt}/{J} buckets", 0.0))
         w4 = sum(1 for c in dense if c >= 0 and c & 8)
         w4s = sum(1 for c in swi if c >= 0 and c & 8)
         report.append(("dense:" + name, J * quantum, N, K, J,
-                       f"{n_dense}/{J} buckets (w4 {w4}), swiglu {n_swi}/{J} (w4 {w4s})", 0.0))
+                       f"{n_dense}/{J} buckets (w4 {w4}), hybrid {n_hyb}, swiglu {n_swi}/{J} "
+                       f"(w4 {w4s})", 0.0))
         for j, parts in enumerate(table):
             if parts is not None:
                 t_split = sum(times[c] for c in parts)

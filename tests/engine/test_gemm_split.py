@@ -3,6 +3,8 @@ on synthetic timing curves, chunk rows always cover M exactly, and the split
 linear path equals one GEMM (CPU oracle)."""
 import itertools
 
+import pytest
+
 import torch
 
 from replisense_rfq_amd import ops
@@ -101,3 +103,49 @@ def test_merge_plan_keys_match_runner_splits():
         assert ops.merge_plan(1, 4096, 4096, 16, False) == -1
     finally:
         ops.set_merge_plan({})
+
+
+def test_plan_hybrid_whole_rounds():
+    """Hybrid rows: the hand-written kernel takes whole rounds of 256 x 256 tiles (for
+    16 weight tiles that is every 16 row tiles = 4,096 rows), the library the rest, only
+    where that beats both kernels alone."""
+    from replisense_rfq_amd.ops.autotune import plan_hybrid
+
+    J = 32                                    # buckets of 256 rows up to 8,192
+    # hand-written: 10 µs per 16-row-tile round (quantised), library: linear 0.7 µs / tile
+    t_dense = [float("inf")] + [10.0 * -(-j // 16) for j in range(1, J + 1)]
+    t_lib = [float("inf")] + [0.7 * j for j in range(1, J + 1)]
+    hyb = plan_hybrid(t_lib, t_dense, tiles_n=16, quantum=256, launch_us=0.0, margin=1.0)
+    assert all(h in (0, 16) for h in hyb)               # only whole rounds (16 quanta)
+    # 17 quanta: dense alone 20 (two rounds), library 11.9, hybrid 10 + 0.7 = 10.7
+    assert hyb[17] == 16
+    # 16 quanta: one full round is best alone, no split
+    assert hyb[16] == 0
+    # a split never wins where the library alone is cheaper than a round
+    assert hyb[5] == 0
+
+
+@pytest.mark.gpu
+def test_linear_hybrid_rows_gpu():
+    """ops.linear with a hybrid plan entry: the first m1 rows on the persistent
+    hand-written GEMM, the rest on the library, equal to one GEMM."""
+    import math
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, K, M = 4096, 512, 4096 + 1000
+    J = -(-M // 256)
+    hyb = [0] * (J + 2)
+    hyb[J] = (16, 13960)
+    plan = {(N, K): (256, [None] * (J + 2), [-1] * (J + 2), [-1] * (J + 2), [-1] * (J + 2), hyb)}
+    ops.set_split_plan(plan)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(3)
+        x = ((torch.rand(M, K, device="cuda", generator=g) * 2 - 1)).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(torch.bfloat16)
+        assert ops._hybrid_rows(M, N, K) == (4096, 13960)
+        y = ops.linear(x, w)
+        ref = (x.float() @ w.float().t())
+        assert (y.float() - ref).abs().max().item() < 3e-2
+    finally:
+        ops.set_split_plan({})
