@@ -149,3 +149,23 @@ def test_linear_hybrid_rows_gpu():
         assert (y.float() - ref).abs().max().item() < 3e-2
     finally:
         ops.set_split_plan({})
+
+
+def test_hybrid_rows_lookup():
+    """ops._hybrid_rows reads the plan's sixth entry per M bucket; older 5-entry plans,
+    untuned shapes and splits that would cover all of M mean no hybrid."""
+    q = 256
+    hyb = [0] * 40
+    hyb[20] = (16, 13960)            # 20 buckets: 4,096 rows on the hand-written kernel
+    hyb[16] = (16, 13960)            # m1 == M: never a split
+    ops.set_split_plan({(4096, 512): (q, [None] * 40, [-1] * 40, [-1] * 40, [-1] * 40, hyb),
+                        (4096, 1024): (q, [None] * 40, [-1] * 40, [-1] * 40, [-1] * 40)})
+    try:
+        assert ops._hybrid_rows(20 * q - 100, 4096, 512) == (4096, 13960)
+        assert ops._hybrid_rows(16 * q, 4096, 512) == (0, -1)
+        assert ops._hybrid_rows(10 * q, 4096, 512) == (0, -1)
+        assert ops._hybrid_rows(20 * q, 4096, 1024) == (0, -1)     # 5-entry plan
+        assert ops._hybrid_rows(20 * q, 2048, 512) == (0, -1)      # untuned shape
+        assert ops._hybrid_rows(100 * q, 4096, 512) == (0, -1)     # past the tuned range
+    finally:
+        ops.set_split_plan({})
