@@ -37,6 +37,13 @@ void launch_gemv_splitk_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, 
 void launch_gemv_splitk_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                              int, float*, unsigned*, const int32_t*, const float*, const int32_t*,
                              bf16_t*, bf16_t*, int, int, int, hipStream_t);
+void launch_gemv_rows(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
+                      hipStream_t);
+void launch_gemv_rows_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
+                             int, int, hipStream_t);
+void launch_gemv_rows_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
+                           int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*, int,
+                           int, int, hipStream_t);
 void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
                      float*, unsigned*, const int32_t*, const float*, const int32_t*, bf16_t*,
                      bf16_t*, int, int, int, const int32_t*, int, const int32_t*,
@@ -280,6 +287,59 @@ void gemv_splitk_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const
                                positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(),
                                slot_mapping.data_ptr<int32_t>(), bpm(k_cache), bpm(v_cache),
                                (int)Hq, (int)Hkv, k_cache.size(2), cur_stream());
+}
+
+// Row-streaming GEMV (gemv_rows.hip) for M <= 4: one wave per weight row (or RW rows),
+// full K, no workspace.  cfg bits [1:0] RW = 1 << b (plain only), [3:2] CU = 2 << b.
+static void check_rows(const char* what, const Tensor& x, const Tensor& w, const Tensor& y,
+                       int64_t cfg, int64_t y_cols) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
+  CHECK_ROWMAJOR(x); CHECK_ROWMAJOR(y);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), what, ": w must be contiguous [N, K]");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 4, what, ": M must be in [1, 4]");
+  TORCH_CHECK(w.size(1) == K && K % 512 == 0, what, ": K % 512 == 0 required");
+  TORCH_CHECK(w.numel() < ((int64_t)1 << 40), what, ": weight too large");
+  TORCH_CHECK(y.size(0) == M && y.size(1) == y_cols, what, ": y shape");
+  TORCH_CHECK(x.stride(0) % 8 == 0, what, ": x rows must be 16-byte aligned");
+  TORCH_CHECK(cfg >= 0 && cfg < 16, what, ": cfg");
+}
+
+void gemv_rows(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cfg) {
+  check_rows("gemv_rows", x, w, y, cfg, w.size(0));
+  rfq::launch_gemv_rows(bp(x), x.stride(0), bp(w), w.size(0), x.size(1), bpm(y), y.stride(0),
+                        x.size(0), (int)cfg, cur_stream());
+}
+
+void gemv_rows_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg) {
+  const int64_t F = w.size(0) / 2;
+  TORCH_CHECK(w.size(0) == 2 * F, "gemv_rows_swiglu: w [2F, K]");
+  check_rows("gemv_rows_swiglu", x, w, out, cfg, F);
+  rfq::launch_gemv_rows_swiglu(bp(x), x.stride(0), bp(w), (int)F, x.size(1), bpm(out),
+                               out.stride(0), x.size(0), (int)cfg, cur_stream());
+}
+
+void gemv_rows_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
+                    const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
+                    const Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t cfg) {
+  const int64_t N = w.size(0);
+  check_rows("gemv_rows_rope", x, w, qkv, cfg, N);
+  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "gemv_rows_rope: w must be [(Hq + 2 Hkv) * 128, K]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == 128,
+              "gemv_rows_rope: cos_sin must be fp32 [max_pos, 128]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == 128 &&
+                  k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  v_cache.sizes() == k_cache.sizes(),
+              "gemv_rows_rope: cache must be [blocks, Hkv, BS, 128]");
+  TORCH_CHECK(positions.numel() >= x.size(0) && slot_mapping.numel() >= x.size(0),
+              "gemv_rows_rope: metadata");
+  rfq::launch_gemv_rows_rope(bp(x), x.stride(0), bp(w), (int)N, x.size(1), bpm(qkv),
+                             qkv.stride(0), x.size(0), (int)cfg, positions.data_ptr<int32_t>(),
+                             cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int32_t>(),
+                             bpm(k_cache), bpm(v_cache), (int)Hq, (int)Hkv, k_cache.size(2),
+                             cur_stream());
 }
 
 // Fused QKV projection + RoPE + KV append + split-K decode attention in ONE launch
@@ -1030,6 +1090,12 @@ void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu
               "gemm_dense: 16-byte aligned operand rows");
   TORCH_CHECK(x.stride(0) * 256 < (int64_t)INT32_MAX && N * w.stride(0) < (int64_t)INT32_MAX,
               "gemm_dense: operand offsets exceed int32");
+  // gemm_w4 / gemm_w4p (cfg bit 3) address W, X and out through buffer resources with
+  // 32-bit BYTE offsets: a weight over 2 GiB (e.g. a 152064 x 8192 LM head) would wrap
+  TORCH_CHECK(!(cfg & 8) || (N * w.stride(0) * 2 < (int64_t)INT32_MAX &&
+                             M * x.stride(0) * 2 < (int64_t)INT32_MAX &&
+                             M * out.stride(0) * 2 < (int64_t)INT32_MAX),
+              "gemm_dense: cfg bit 3 (gemm_w4) needs every operand under 2 GiB");
   rfq::launch_gemm_dense(bp(x), x.stride(0), bp(w), w.stride(0), bpm(out), out.stride(0), (int)M,
                          (int)n_out, (int)K, (int)n_out, swiglu, (int)cfg, cur_stream());
 }
@@ -1075,6 +1141,11 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("skinny_gemm_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
         "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) partials, int cfg) -> ()");
   m.def("skinny_gemm_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("gemv_rows(Tensor x, Tensor w, Tensor(a!) y, int cfg) -> ()");
+  m.def("gemv_rows_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("gemv_rows_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
+        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
+        "int cfg) -> ()");
   m.def("gemv_splitk(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) part, Tensor(c!) tile_cnt, "
         "int cfg) -> ()");
   m.def("gemv_splitk_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "
@@ -1167,6 +1238,9 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("skinny_gemm_norm", &skinny_gemm_norm);
   m.impl("skinny_gemm_rope", &skinny_gemm_rope);
   m.impl("skinny_gemm_swiglu", &skinny_gemm_swiglu);
+  m.impl("gemv_rows", &gemv_rows);
+  m.impl("gemv_rows_swiglu", &gemv_rows_swiglu);
+  m.impl("gemv_rows_rope", &gemv_rows_rope);
   m.impl("gemv_splitk", &gemv_splitk);
   m.impl("gemv_splitk_norm", &gemv_splitk_norm);
   m.impl("gemv_splitk_swiglu", &gemv_splitk_swiglu);

@@ -1,0 +1,287 @@
+// Row-streaming GEMV for the batch-1 latency path: Y[M, N] = X[M, K] . W[N, K]^T,
+// M <= 4 tokens, K % 512 == 0.
+//
+// Why a third GEMV form.  The split-K GEMV (gemv_core.h) and the skinny GEMM
+// (gemm_skinny.hip) both tile W by 16-row MFMA blocks.  On the 70B TP = 8 rank shard
+// the QKV weight has only 80 such blocks (1,280 rows), so the split-K kernel has to cut
+// K across workgroups and pay a cross-workgroup hand-off per tile (write-through fp32
+// partials, drained stores, a ticket, sc1 read-back by the last arriver): a chain of
+// 3-4 dependent memory round trips after the weight stream that set the launch's time
+// (9.8 us for 21 MB, profiles/r4/tp8_rank_kernel_window.md).
+//
+// Here the unit of work is a WAVE owning whole rows over the full K:
+//   * lane l of the wave reads bytes [16 l, 16 l + 16) of every 1 KB chunk of its row:
+//     one 1 KB fully-coalesced load per wave-instruction, straight from the row-major
+//     weight (no tiled copy needed), non-temporal (each weight byte is read once per
+//     step by one CU: MI355X_MICROARCH.md 'nt-weights');
+//   * the dot product runs on v_dot2c_f32_bf16 (two bf16 products per instruction, fp32
+//     accumulation): at M <= 4 the VALU work is a few percent of the stream's cycles,
+//     and the 15/16 of an MFMA wasted on padding tokens is not needed;
+//   * the wave sums its 64 lanes with four DPP steps and two swizzles -- no LDS round
+//     trip, no cross-workgroup traffic, no tickets, no workspace.
+// Grids are rows / RW waves: 1,280-8,192 waves on the TP = 8 shard, 4,096-28,672 on 8B,
+// i.e. 5-112 waves per CU, every CU streams.
+//
+// Epilogues:
+//   kRwPlain  Y[m, row] bf16.
+//   kRwSwi    waves 2j / 2j+1 of a workgroup own gate row q and up row F + q of the
+//             stacked gate|up weight; the pair meets in LDS and Y[m, q] = SwiGLU rounded
+//             like act.hip silu_mul (gate and up rounded to bf16 first).
+//   kRwRope   waves 2j / 2j+1 own the rotate-half partners h*128 + d and h*128 + 64 + d
+//             of one head: NeoX RoPE on the fp32 sums (as gemv_core.h kGvRope), q to Y,
+//             k / v appended to the paged cache (slot -1 = padding: no write).
+#include "common.h"
+#include "gemv_core.h"
+
+namespace rfq {
+
+enum { kRwPlain = 0, kRwSwi = 1, kRwRope = 2 };
+constexpr int kRwWaves = 4;          // waves per workgroup
+constexpr int kRwMaxM = 4;
+
+// one DPP move (row_mask / bank_mask all, bound_ctrl off)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xf, 0xf, false));
+}
+
+// full 64-lane sum, result in every lane: xor 1 / xor 2 (quad_perm), 8-lane and 16-lane
+// mirrors (each lane then holds its 16-lane row's sum), then two cross-row swizzles
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// x . w over 8 bf16 pairs.  Each dword is copied to a scalar before the bit_cast:
+// hipcc (ROCm 7.2) lowers __builtin_bit_cast of a vector-element lvalue (w.y, w[i]) as a
+// read of the vector's FIRST element, so bit-casting elements in place silently computes
+// x0 . w0 four times.
+__device__ __forceinline__ float dot2(uint32_t w, uint32_t x, float acc) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, w),
+                                         __builtin_bit_cast(bf16x2, x), acc, false);
+}
+__device__ __forceinline__ float dot8(const u32x4& w, const u32x4& x, float acc) {
+  const uint32_t w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
+  const uint32_t x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
+  acc = dot2(w0, x0, acc);
+  acc = dot2(w1, x1, acc);
+  acc = dot2(w2, x2, acc);
+  acc = dot2(w3, x3, acc);
+  return acc;
+}
+
+// 16-byte buffer load (SRSRC form, cdna_hip_programming.md T8): the per-chunk offsets
+// are wave-uniform and go in soffset, so no per-lane 64-bit address arithmetic
+template <int AUX>
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX));
+}
+
+// MM: token capacity (runtime M <= MM); RW: rows per wave (plain only; paired epilogues
+// use one row per wave); CU: 1 KB chunks per row in flight per loop iteration.
+template <int MM, int RW, int CU, int EPI, bool NTL>
+__global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
+    const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int N, int K,
+    bf16_t* __restrict__ Y, int64_t ldy, int M, int up_off, RopeEpi re) {
+  static_assert(EPI == kRwPlain || RW == 1, "paired epilogues: one row per wave");
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int gw = blockIdx.x * kRwWaves + wave;
+  // rows of this wave
+  int row0;
+  bool valid;
+  if constexpr (EPI == kRwPlain) {
+    row0 = gw * RW;
+    valid = row0 < N;
+  } else if constexpr (EPI == kRwSwi) {
+    const int q = gw >> 1;                        // N = F here
+    row0 = (wave & 1) ? up_off + q : q;
+    valid = q < N;
+  } else {
+    const int q = gw >> 1;                        // pair index; N = rows / 2 pairs
+    row0 = (q >> 6) * 128 + (q & 63) + ((wave & 1) ? 64 : 0);
+    valid = q < N;
+  }
+  float acc[RW][MM];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int m = 0; m < MM; ++m) acc[r][m] = 0.f;
+  if (valid) {
+    const int nch = K >> 9;
+    // W: the wave's RW rows (wave-uniform base, RW * K * 2 bytes); X: the M token rows,
+    // records end at row M so the loads of rows m >= M return zeros (no branch)
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(W + (int64_t)__builtin_amdgcn_readfirstlane(row0) * K), (short)0, RW * K * 2,
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(M * ldx * 2), 0x00020000);
+    const int voff = lane * 16;
+    constexpr int WAUX = NTL ? 2 : 0;
+    int c = 0;
+    for (; c + CU <= nch; c += CU) {
+      u32x4 w[RW][CU], x[MM][CU];
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) w[r][u] = bload<WAUX>(wr, voff, (r * K + (c + u) * 512) * 2);
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) x[m][u] = bload<0>(xr, voff, (int)(m * ldx + (c + u) * 512) * 2);
+#pragma unroll
+      for (int u = 0; u < CU; ++u)
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int m = 0; m < MM; ++m) acc[r][m] = dot8(w[r][u], x[m][u], acc[r][m]);
+    }
+    for (; c < nch; ++c) {                        // tail chunks (K / 512 not a multiple of CU)
+      u32x4 w[RW], x[MM];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) w[r] = bload<WAUX>(wr, voff, (r * K + c * 512) * 2);
+#pragma unroll
+      for (int m = 0; m < MM; ++m) x[m] = bload<0>(xr, voff, (int)(m * ldx + c * 512) * 2);
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int m = 0; m < MM; ++m) acc[r][m] = dot8(w[r], x[m], acc[r][m]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int m = 0; m < MM; ++m) acc[r][m] = wave_sum_dpp(acc[r][m]);
+
+  if constexpr (EPI == kRwPlain) {
+    if (!valid) return;
+    // lane r * MM + m stores row0 + r of token m
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+        if (lane == r * MM + m && m < M && row0 + r < N) Y[(int64_t)m * ldy + row0 + r] = f2bf(acc[r][m]);
+  } else {
+    __shared__ float pair_s[kRwWaves / 2][MM];
+    if ((wave & 1) && lane == 0) {
+#pragma unroll
+      for (int m = 0; m < MM; ++m) pair_s[wave >> 1][m] = acc[0][m];
+    }
+    __syncthreads();
+    if ((wave & 1) || !valid || lane >= M) return;
+    // lane m < M of the even wave finishes token m
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+      if (lane == m) {
+        a = acc[0][m];
+        b = pair_s[wave >> 1][m];
+      }
+    const int m = lane;
+    const int q = gw >> 1;
+    if constexpr (EPI == kRwSwi) {
+      const float gf = bf2f(f2bf(a));                 // = the gate_up GEMM's bf16 output
+      const float sg = gf / (1.f + __expf(-gf));
+      Y[(int64_t)m * ldy + q] = f2bf(bf2f(f2bf(sg)) * bf2f(f2bf(b)));
+    } else {
+      const int h = q >> 6, d = q & 63;
+      float o1 = a, o2 = b;
+      if (h < re.Hq + re.Hkv) {
+        const float* cs = re.cos_sin + (int64_t)re.positions[m] * 128;
+        const float cc = cs[d], ss = cs[64 + d];
+        o1 = a * cc - b * ss;
+        o2 = b * cc + a * ss;
+      }
+      bf16_t* dst = nullptr;
+      if (h < re.Hq) {
+        dst = Y + (int64_t)m * ldy + h * 128;
+      } else {
+        const int slot = re.slots[m];
+        if (slot >= 0) {
+          const bool is_k = h < re.Hq + re.Hkv;
+          const int kvh = is_k ? h - re.Hq : h - re.Hq - re.Hkv;
+          dst = (is_k ? re.k_cache : re.v_cache) +
+                (((int64_t)(slot / re.BS) * re.Hkv + kvh) * re.BS + slot % re.BS) * 128;
+        }
+      }
+      if (dst != nullptr) {
+        dst[d] = f2bf(o1);
+        dst[64 + d] = f2bf(o2);
+      }
+    }
+  }
+}
+
+// cfg bits: [1:0] RW = 1 << b (plain only), [3:2] CU = 2 << b (2, 4, 8, 16).
+// Host-checked: K % 512 == 0, 1 <= M <= 4, (RW + MM) * CU <= 40 loads in flight per lane.
+template <int EPI, int MM>
+static void launch_rows_mm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                           bf16_t* Y, int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re,
+                           int waves, hipStream_t s) {
+  const dim3 grid((waves + kRwWaves - 1) / kRwWaves), block(kRwWaves * 64);
+#define RW_L(rw, cu) \
+  hipLaunchKernelGGL((gemv_rows_kernel<MM, rw, cu, EPI, true>), grid, block, 0, s, X, ldx, W, N, \
+                     K, Y, ldy, M, up_off, re)
+  const int rw = 1 << (cfg & 3), cu = 2 << ((cfg >> 2) & 3);
+  if constexpr (EPI == kRwPlain) {
+    switch (rw * 100 + cu) {
+      case 104: RW_L(1, 4); break;
+      case 108: RW_L(1, 8); break;
+      case 116: RW_L(1, 16); break;
+      case 204: RW_L(2, 4); break;
+      case 208: RW_L(2, 8); break;
+      case 402: RW_L(4, 2); break;
+      case 404: RW_L(4, 4); break;
+      default: RW_L(8, 2); break;
+    }
+  } else {
+    switch (cu) {
+      case 4: RW_L(1, 4); break;
+      case 16: RW_L(1, 16); break;
+      default: RW_L(1, 8); break;
+    }
+  }
+#undef RW_L
+}
+
+template <int EPI>
+static void launch_rows(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                        int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re, int waves,
+                        hipStream_t s) {
+  if (M <= 1)
+    launch_rows_mm<EPI, 1>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+  else if (M <= 2)
+    launch_rows_mm<EPI, 2>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+  else
+    launch_rows_mm<EPI, 4>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+}
+
+void launch_gemv_rows(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
+                      int64_t ldy, int M, int cfg, hipStream_t s) {
+  const int rw = 1 << (cfg & 3);
+  launch_rows<kRwPlain>(X, ldx, W, N, K, Y, ldy, M, cfg, 0, RopeEpi{}, (N + rw - 1) / rw, s);
+}
+
+// Y[M, F] = silu(x Wg^T) * (x Wu^T), w = [Wg; Wu] [2F, K]
+void launch_gemv_rows_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, int F, int K,
+                             bf16_t* Y, int64_t ldy, int M, int cfg, hipStream_t s) {
+  launch_rows<kRwSwi>(X, ldx, W, F, K, Y, ldy, M, cfg, F, RopeEpi{}, 2 * F, s);
+}
+
+// qkv = x w^T with RoPE + KV append (N = (Hq + 2 Hkv) * 128); only q columns of Y written
+void launch_gemv_rows_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                           bf16_t* Y, int64_t ldy, int M, int cfg, const int32_t* positions,
+                           const float* cos_sin, const int32_t* slots, bf16_t* k_cache,
+                           bf16_t* v_cache, int Hq, int Hkv, int BS, hipStream_t s) {
+  const RopeEpi re{positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, BS};
+  launch_rows<kRwRope>(X, ldx, W, N / 2, K, Y, ldy, M, cfg, 0, re, N, s);
+}
+
+}  // namespace rfq

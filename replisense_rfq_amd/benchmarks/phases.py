@@ -87,6 +87,10 @@ async def _client_loop(url: str, docs: list, clients: int, deadline: float):
 def _client_proc(url, docs, clients, deadline, start_evt, out_q):
     import asyncio
 
+    from ..utils.affinity import restore_affinity
+
+    restore_affinity()              # a load generator, not the engine: off its cores
+
     start_evt.wait()
     out_q.put(asyncio.run(_client_loop(url, docs, clients, deadline)))
 
@@ -236,6 +240,9 @@ def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt
     """One client process: a Poisson arrival stream at ``rate`` req/s for ``duration``
     s of /parse-text/ emails and (``upload_share``) /upload/ attachments, after an
     initial burst of ``burst`` requests spread over the first second."""
+    from ..utils.affinity import restore_affinity
+
+    restore_affinity()
     import asyncio
     import random
 
@@ -269,6 +276,9 @@ def _api_server_proc(cfg_dict: dict, inq, outq, parse_procs: int, port_q, stop_e
     parsing (its parser pool), chat template + tokenisation and the G9-G12 validation
     here; requests go to the engine loop over (inq, outq) through an attached
     DPRouter.  Reports its port on ``port_q``, then serves until ``stop_evt``."""
+    from ..utils.affinity import restore_affinity
+
+    restore_affinity()              # the API process must not share the engine's cores
     import uvicorn
 
     from ..api import main as api

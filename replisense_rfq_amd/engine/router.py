@@ -46,9 +46,9 @@ def _join_group(devices: str, tp_rank: int, tp: int, port: int):
     process group.  Runs before anything touches HIP."""
     if devices:
         os.environ["HIP_VISIBLE_DEVICES"] = devices
-    from ..utils.affinity import pin_to_gpu
+        from ..utils.affinity import pin_to_gpu
 
-    pin_to_gpu(tp_rank)           # NUMA-local cores of this process's device
+        pin_to_gpu(tp_rank)       # NUMA-local cores of this process's device (GPU replicas)
     if tp <= 1:
         from ..parallel.tp import SINGLE
 
@@ -176,6 +176,14 @@ def serve_loop(eng, inq, outq, idx: int = 0, exit_after=None,
                                         "span": s.span()}))
                 served += 1
         if fatal or (exit_after is not None and served >= exit_after):
+            if not shutdown_engine:
+                # an engine embedded in a bigger process (the bench's HTTP phase): end the
+                # loop, never the process; what it held was failed above
+                for _, (rid, _s) in list(pending.items()):
+                    outq.put(("done", rid, {"text": "", "finish": "engine_error", "span": {}}))
+                pending.clear()
+                eng.runner.busy_hook = None
+                return
             outq.close()                       # flush what was served, then leave
             outq.join_thread()
             os._exit(4 if fatal else 3)        # 3 = injected replica crash
@@ -209,6 +217,8 @@ class DPRouter:
         self._lock = threading.Lock()
         self._cfg_dict = dict(cfg.to_dict())
         self._cfg_dict["dp"] = 1
+        if str(self._cfg_dict.get("device", "")).startswith("cuda:"):
+            self._cfg_dict["device"] = "cuda"     # the replica sees only its own devices
         if queues is not None:
             if n_replicas != 1:
                 raise ValueError("attached queues serve exactly one replica")
@@ -227,13 +237,26 @@ class DPRouter:
         self._thread.start()
 
     def _devices(self, i: int) -> str:
-        """HIP_VISIBLE_DEVICES of replica i (``RFQ_DEVICES`` remaps physical ids)."""
+        """HIP_VISIBLE_DEVICES of replica i.  Logical device d of the replicas maps
+        through ``RFQ_DEVICES`` when set, else through the parent's own
+        HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (an operator's
+        ``HIP_VISIBLE_DEVICES=3`` keeps the engine on physical GPU 3; a
+        ROCR_VISIBLE_DEVICES mask is inherited and indexed inside).  A single replica of
+        ``cfg.device = "cuda:N"`` starts at logical device N."""
         if self.cfg.device == "cpu":
             return ""
-        phys = os.environ.get("RFQ_DEVICES")
-        ids = [int(x) for x in phys.split(",")] if phys else None
-        devs = [i * self.dpr + j for j in range(self.dpr)]
-        return ",".join(str(ids[d] if ids else d) for d in devs)
+        phys = (os.environ.get("RFQ_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
+                or os.environ.get("CUDA_VISIBLE_DEVICES"))
+        ids = [x.strip() for x in phys.split(",") if x.strip()] if phys else None
+        base = 0
+        dev = str(self.cfg.device)
+        if self.n == 1 and dev.startswith("cuda:"):
+            base = int(dev.split(":", 1)[1])
+        devs = [base + i * self.dpr + j for j in range(self.dpr)]
+        if ids is not None and max(devs) >= len(ids):
+            raise ValueError(f"replica {i} needs logical devices {devs} but only "
+                             f"{len(ids)} are visible ({phys})")
+        return ",".join(ids[d] if ids else str(d) for d in devs)
 
     def _spawn(self, i: int) -> None:
         devs = self._devices(i)

@@ -650,6 +650,13 @@ def gemm_dense_ok(M: int, N: int, K: int, swiglu: bool = False) -> bool:
     return M >= 1 and K % 64 == 0 and K >= 64 and N % 256 == 0
 
 
+def gemm_w4_ok(M: int, N: int, K: int) -> bool:
+    """gemm_w4 / gemm_w4p (gemm_dense cfg bit 3) address every operand with 32-bit byte
+    offsets through buffer resources: K % 128 == 0 and each operand under 2 GiB."""
+    lim = (1 << 31) - 1
+    return K % 128 == 0 and N * K * 2 < lim and M * max(K, N) * 2 < lim
+
+
 def gemm_dense(x, w, out=None, swiglu: bool = False, cfg: int = 0):
     """out[M, N] = x[M, K] . w[N, K]^T on the 8-wave ping-pong MFMA kernel; swiglu:
     w = gate|up [2F, K] and out[M, F] = silu(x Wg^T) * (x Wu^T) (rounded like the

@@ -16,6 +16,7 @@ import time
 import torch
 
 from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_NT, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
+               gemm_w4_ok,
                set_linear_plan, set_merge_plan, set_norm_plan, set_rope_plan, set_silu_plan,
                set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
@@ -440,7 +441,7 @@ DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 
 def plan_hybrid(t_lib: list, t_dense: list, tiles_n: int, quantum: int = 256,
-                launch_us: float = 4.0, margin: float = DENSE_MARGIN) -> list:
+                launch_us: float = 4.0, margin: float = DENSE_MARGIN, cus: int = 256) -> list:
     """Row split of a large-M GEMM between the hand-written persistent kernel and the
     library.  The hand-written kernel runs whole rounds of 256 x 256 tiles on the 256 CUs
     only when its row-tile count times ``tiles_n`` is a multiple of 256; its last, partly
@@ -448,11 +449,14 @@ def plan_hybrid(t_lib: list, t_dense: list, tiles_n: int, quantum: int = 256,
     quanta of rows) try: the first m1 rows (a multiple of one full round) on the
     hand-written kernel, the rest on the library.  ``t_lib[j]`` / ``t_dense[j]``: µs of
     j quanta on each (index 0 unused; inf where not measured).  Returns ``hyb[j]`` = m1
-    quanta, or 0 where one kernel alone is at least as fast (margin)."""
+    quanta, or 0 where one kernel alone is at least as fast (margin).  ``cus``: the
+    persistent grid's workgroups per round = the device's CU count rounded down to a
+    multiple of 8 (gemm_w4.hip launch_gemm_w4 sizes its grid the same way)."""
     import math
 
     J = len(t_lib) - 1
-    round_tiles = 256 // math.gcd(256, tiles_n)          # row tiles per full round
+    cus = max(8, cus - cus % 8)
+    round_tiles = cus // math.gcd(cus, tiles_n)          # row tiles per full round
     step = max(1, round_tiles * 256 // quantum)          # in quanta
     hyb = [0] * (J + 1)
     for j in range(1, J + 1):
@@ -519,7 +523,7 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                 best_c, t_best = -1, t_lib * DENSE_MARGIN
                 t_lib_j[j] = t_lib
                 for c in DENSE_CFGS:
-                    if c & 8 and K % 128:            # gemm_w4 needs K % 128 == 0
+                    if c & 8 and not gemm_w4_ok(m, N, K):   # K % 128, < 2 GiB operands
                         continue
                     t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, out[:m], False, c),
                               [w], reps, graph=False)
@@ -535,7 +539,7 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                     t_ref = min(t_lib, t_best) + t_silu
                     bs, ts = -1, t_ref * DENSE_MARGIN
                     for c in DENSE_CFGS:
-                        if c & 8 and K % 128:
+                        if c & 8 and not gemm_w4_ok(m, N, K):
                             continue
                         t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, act[:m], True, c),
                                   [w], reps, graph=False)
@@ -552,7 +556,8 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
         # library (plain GEMMs; buckets where one kernel alone was not beaten stay so)
         hyb = [0] * (J + 1)
         if DENSE_ON and any(c >= 0 for c in c_dense) and os.environ.get("RFQ_GEMM_HYBRID", "1") != "0":
-            hyb = plan_hybrid(t_lib_j, t_dense, N // 256, quantum)
+            cus = torch.cuda.get_device_properties(w.device).multi_processor_count
+            hyb = plan_hybrid(t_lib_j, t_dense, N // 256, quantum, cus=cus)
             hyb = [(m1, c_dense[m1]) if m1 > 0 and c_dense[m1] >= 0 and dense[j] < 0 else 0
                    for j, m1 in enumerate(hyb)]
         n_hyb = sum(1 for h in hyb if h)

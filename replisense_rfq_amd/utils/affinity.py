@@ -120,6 +120,22 @@ def plan_affinity(local_rank: int, kfd_nodes: str = KFD_NODES,
             "cpus": mine or cpus, "node_cpus": len(cpus), "gpus_on_node": n}
 
 
+ORIG_ENV = "RFQ_ORIG_AFFINITY"
+
+
+def restore_affinity() -> bool:
+    """Undo pin_to_gpu's NUMA pinning in a process that inherited it but is no part of
+    the engine (HTTP API server, client / load-generator processes).  True if reset."""
+    orig = os.environ.get(ORIG_ENV)
+    if not orig or not hasattr(os, "sched_setaffinity"):
+        return False
+    try:
+        os.sched_setaffinity(0, {int(c) for c in orig.split(",") if c})
+    except OSError:
+        return False
+    return True
+
+
 def pin_to_gpu(local_rank: int) -> dict:
     """Apply :func:`plan_affinity` to this process (call before any HIP call).
     Returns what was done, for the bench JSON."""
@@ -138,5 +154,9 @@ def pin_to_gpu(local_rank: int) -> dict:
         os.sched_setaffinity(0, cpus)
     except OSError as e:
         return {"status": f"failed: {e}"}
+    # children that are not part of the engine (API server, load generators) put the
+    # original mask back with restore_affinity(): they must not compete with the engine
+    # for its few pinned cores
+    os.environ.setdefault(ORIG_ENV, ",".join(str(c) for c in sorted(allowed)))
     return {"status": "pinned", "numa_node": plan["numa_node"], "cores": len(cpus),
             "first_core": cpus[0], "gpus_on_node": plan["gpus_on_node"]}

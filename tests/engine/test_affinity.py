@@ -60,3 +60,24 @@ def test_pin_without_topology_is_a_noop(monkeypatch):
     assert os.sched_getaffinity(0) == before
     monkeypatch.setenv("RFQ_PIN_NUMA", "0")
     assert af.pin_to_gpu(0)["status"] == "off"
+
+
+def test_restore_affinity_undoes_pinning(monkeypatch):
+    """processes that inherit the engine's NUMA pinning but are no part of the
+    engine (API server, load generators) put the original mask back."""
+    import os
+
+    from replisense_rfq_amd.utils import affinity
+
+    if not hasattr(os, "sched_setaffinity"):
+        return
+    orig = os.sched_getaffinity(0)
+    monkeypatch.setenv(affinity.ORIG_ENV, ",".join(str(c) for c in sorted(orig)))
+    try:
+        os.sched_setaffinity(0, {min(orig)})
+        assert affinity.restore_affinity()
+        assert os.sched_getaffinity(0) == orig
+    finally:
+        os.sched_setaffinity(0, orig)
+    monkeypatch.delenv(affinity.ORIG_ENV)
+    assert not affinity.restore_affinity()

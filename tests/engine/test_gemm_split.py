@@ -169,3 +169,20 @@ def test_hybrid_rows_lookup():
         assert ops._hybrid_rows(100 * q, 4096, 512) == (0, -1)     # past the tuned range
     finally:
         ops.set_split_plan({})
+
+
+def test_plan_hybrid_follows_cu_count():
+    """a whole round of persistent tiles is CU-count dependent.  On a 240-CU
+    device with 16 weight tiles a round is 15 row tiles (240 / gcd(240, 16)), so the only
+    split the plan may take is a multiple of 15 quanta."""
+    from replisense_rfq_amd.ops.autotune import plan_hybrid
+
+    J = 40
+    t_dense = [float("inf")] + [10.0 * -(-j // 15) for j in range(1, J + 1)]
+    t_lib = [float("inf")] + [0.7 * j for j in range(1, J + 1)]
+    hyb = plan_hybrid(t_lib, t_dense, tiles_n=16, quantum=256, launch_us=0.0, margin=1.0,
+                      cus=240)
+    assert all(h % 15 == 0 for h in hyb)
+    assert hyb[16] == 15
+    # a CU count that is not a multiple of 8 rounds down like the launcher (244 -> 240)
+    assert plan_hybrid(t_lib, t_dense, 16, 256, 0.0, 1.0, cus=244) == hyb

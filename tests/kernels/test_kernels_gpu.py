@@ -1109,3 +1109,81 @@ def test_qkv_attn_fused(gpu, Hq, Hkv, K, cfg, splits):
     ref.attn_prefill(exp_qkv[:, :Hq * 128].contiguous(), kc_e, vc_e, btc, torch.tensor(qs),
                      torch.tensor(qlens), torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
     _close(out1, exp, 3e-2, 0, f"fused attention vs fp32 Hq={Hq} splits={splits}")
+
+
+ROWS_CFGS_PLAIN = (0 | 4, 0 | 8, 0 | 12, 1 | 4, 1 | 8, 2 | 0, 2 | 4, 3 | 0)   # (RW, CU) pairs
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", ROWS_CFGS_PLAIN)
+@pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (1000, 3584)])
+def test_gemv_rows(gpu, M, cfg, N, K):
+    """Row-streaming GEMV (gemv_rows.hip, M <= 4, one wave per RW rows over the full K,
+    v_dot2c_f32_bf16) == fp32 torch; N not a multiple of RW (1000) and K / 512 not a
+    multiple of the in-flight chunk count (3584 = 7 x 512) cover the tails."""
+    torch.manual_seed(M * 31 + cfg + N)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    y = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows(x, w, y, cfg)
+    _close(y, x.float() @ w.float().t(), 2e-2, 1e-2, f"gemv_rows M={M} cfg={cfg} N={N} K={K}")
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("cfg", [4, 8, 12])
+def test_gemv_rows_strided_x(gpu, M, cfg):
+    """x as a row-strided view of a wider buffer (ldx > K): the X buffer resource spans
+    M rows of the stride, rows past M read zeros."""
+    torch.manual_seed(M + cfg)
+    K, N = 2048, 512
+    xb = torch.randn(M, K + 64, device=gpu, dtype=BF)
+    x = xb[:, :K]
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    y = torch.empty(M, N, device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows(x, w, y, cfg)
+    _close(y, x.float() @ w.float().t(), 2e-2, 1e-2, f"gemv_rows strided M={M}")
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [4, 8, 12])
+@pytest.mark.parametrize("F,K", [(3584, 8192), (1792, 4096)])
+def test_gemv_rows_swiglu(gpu, M, cfg, F, K):
+    """gate|up GEMV with the SwiGLU epilogue (waves 2j / 2j+1 pair through LDS) ==
+    silu_mul of the fp32 GEMM, rounded like act.hip."""
+    torch.manual_seed(M * 7 + cfg + F)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(2 * F, K, device=gpu) / math.sqrt(K)).to(BF)
+    out = torch.full((M, F), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows_swiglu(x, w, out, cfg)
+    gu = (x.float() @ w.float().t()).to(BF)
+    exp = torch.empty(M, F, dtype=BF, device=gpu)
+    ref.silu_mul(gu, exp)
+    _close(out, exp, 2e-2, 1e-2, f"gemv_rows_swiglu M={M} cfg={cfg}")
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [4, 8, 12])
+@pytest.mark.parametrize("Hq,Hkv,K", [(8, 1, 8192), (32, 8, 4096)])
+def test_gemv_rows_rope_kv(gpu, M, cfg, Hq, Hkv, K):
+    """QKV GEMV with the RoPE + paged-KV-append epilogue (waves 2j / 2j+1 = rotate-half
+    partners) == fp32 GEMM + rope_kv oracle; padding rows (slot -1) write nothing."""
+    torch.manual_seed(M * 13 + cfg + Hq)
+    N = (Hq + 2 * Hkv) * 128
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    cos_sin = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(4 * 32, device=gpu)[:M].to(torch.int32)
+    if M > 1:
+        slots[-1] = -1
+    kc = torch.zeros(4, Hkv, 32, 128, device=gpu, dtype=BF)
+    vc = torch.zeros_like(kc)
+    qkv = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows_rope(x, w, qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, cfg)
+    exp = (x.float() @ w.float().t()).cpu()
+    kc_e, vc_e = torch.zeros(kc.shape), torch.zeros(vc.shape)
+    ref.rope_kv(exp, pos.cpu(), cos_sin.cpu(), slots.cpu(), kc_e, vc_e, Hq, Hkv)
+    q = Hq * 128
+    _close(qkv[:, :q], exp[:, :q], 2e-2, 1e-2, f"rows rope q M={M} cfg={cfg}")
+    _close(kc, kc_e, 2e-2, 1e-2, f"rows rope k cache M={M} cfg={cfg}")
+    _close(vc, vc_e, 2e-2, 1e-2, f"rows rope v cache M={M} cfg={cfg}")

@@ -11,6 +11,7 @@
 #   lat8b        latency-path kernel window of the 8B single stream
 #   tput         kernel window of a short throughput bench
 #   gemv         tools/bench_decode_gemv.py  (8B and TP=8 shard shapes)
+#   rows         tools/bench_gemv_rows.py    (row-streaming GEMV vs the split-K / skinny GEMVs)
 #   gemm         tools/bench_gemm_dense.py   (hand-written large-M GEMM vs hipBLASLt)
 #   attn         tools/bench_attn.py         (decode attention)
 #   prefill      tools/bench_prefill.py
@@ -91,6 +92,9 @@ for task in "$@"; do
       timeout -k 10 600 python -u tools/bench_gemm_dense.py ${GEMM_ARGS:---ms 2048,4096,7168} \
         > gpurun_out/gemm.log 2>&1
       tail -20 gpurun_out/gemm.log ;;
+    rows)
+      timeout -k 10 400 python -u tools/bench_gemv_rows.py ${ROWS_ARGS:-} \
+        > gpurun_out/gemv_rows.jsonl 2> gpurun_out/gemv_rows.err ;;
     attn)
       timeout -k 10 300 python -u tools/bench_attn.py ${ATTN_ARGS:-} > gpurun_out/attn.log 2>&1 ;;
     prefill)
