@@ -22,6 +22,7 @@ with ``status`` set, and a model phase frees its engine before the next starts.
 """
 from __future__ import annotations
 
+import collections
 import gc
 import logging
 import os
@@ -192,7 +193,7 @@ def http_upload_phase(engine, n_docs: int = 512, clients: int = 64, client_procs
 async def _open_loop(url: str, sched: list, t0: float, deadline: float):
     """Fire every scheduled request at its arrival time, never waiting for earlier
     responses (open loop).  ``sched``: [(offset_s, kind, payload)].  Returns
-    [(offset_s, done_offset_s, latency_s, ok)]."""
+    [(offset_s, done_offset_s, latency_s, ok, failure kind or "")]."""
     import asyncio
 
     import aiohttp
@@ -201,7 +202,7 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
 
     async def one(sess, off, kind, payload):
         t_send = time.perf_counter()
-        status, body = 0, {}
+        status, body, why = 0, {}, ""
         try:
             if kind == "text":
                 async with sess.post(url + "/parse-text/", json=payload) as r:
@@ -212,12 +213,26 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
                 form.add_field("file", blob, filename=name)
                 async with sess.post(url + "/upload/", data=form) as r:
                     status, body = r.status, await r.json()
-        except (aiohttp.ClientError, asyncio.TimeoutError, ValueError):
-            pass
+        except asyncio.TimeoutError:
+            why = "client_timeout"
+        except aiohttp.ClientConnectionError:
+            why = "connection_error"
+        except aiohttp.ClientError as e:
+            why = f"client_error:{type(e).__name__}"
+        except ValueError:
+            why = f"bad_body_http_{status}"
         t_done = time.perf_counter()
         data = body.get("data", {}) if status == 200 else {}
         ok = bool(data.get("success")) and "validation warnings" not in data.get("message", "")
-        out.append((off, t_done - t0, t_done - t_send, ok))
+        if not ok and not why:
+            if status != 200:
+                why = f"http_{status}"
+            elif not data.get("success"):
+                # the G11 error dict (HTTP 200): generation failed inside the service
+                why = "error_dict:" + str(data.get("error", ""))[:40]
+            else:
+                why = "validation_fallback"
+        out.append((off, t_done - t0, t_done - t_send, ok, why))
 
     conn = aiohttp.TCPConnector(limit=0)
     tasks = []
@@ -270,6 +285,39 @@ def _open_loop_proc(url, rate, duration, seed, upload_share, deadline, start_evt
     out_q.put(asyncio.run(_open_loop(url, sched, t0, deadline)))
 
 
+def _idle_client_proc(url: str, n: int, seed: int, out_q) -> None:
+    """Sequential idle /parse-text/ requests (one at a time, the engine otherwise idle):
+    the BASELINE metric's p50 /parse-text/ latency measured through the HTTP surface.
+    Returns [(client latency s, X-Process-Time s, ok)] on ``out_q``."""
+    from ..utils.affinity import restore_affinity
+
+    restore_affinity()
+    import json as _json
+    import urllib.request
+
+    from ..utils import synth
+
+    out = []
+    for i in range(n):
+        body = _json.dumps({"text": synth.make_rfq(seed + i).text}).encode()
+        req = urllib.request.Request(url + "/parse-text/", data=body,
+                                     headers={"Content-Type": "application/json"})
+        t0 = time.perf_counter()
+        try:
+            with urllib.request.urlopen(req, timeout=60) as r:
+                payload = _json.loads(r.read())
+                xpt = float(r.headers.get("X-Process-Time", "nan"))
+                status = r.status
+        except Exception:  # noqa: BLE001 -- counted as a failed request
+            out.append((time.perf_counter() - t0, float("nan"), False))
+            continue
+        dt = time.perf_counter() - t0
+        data = payload.get("data", {}) if status == 200 else {}
+        ok = bool(data.get("success")) and "validation warnings" not in data.get("message", "")
+        out.append((dt, xpt, ok))
+    out_q.put(out)
+
+
 def _api_server_proc(cfg_dict: dict, inq, outq, parse_procs: int, port_q, stop_evt) -> None:
     """The service's API process with the engine in another process (the service's
     RFQ_ENGINE_PROCESS=1 layout): uvicorn + the FastAPI app, HTTP parsing, attachment
@@ -310,7 +358,8 @@ def _api_server_proc(cfg_dict: dict, inq, outq, parse_procs: int, port_q, stop_e
 def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: float = 40.0,
                          upload_share: float = 0.25, client_procs: int = 8,
                          parse_procs: int = 4, budget_s: float = 120.0, seed: int = 0,
-                         burst_depth: int = 0, api_process: bool = True) -> dict:
+                         burst_depth: int = 0, api_process: bool = True,
+                         idle_requests: int = 20) -> dict:
     """does the HTTP surface sustain the engine's throughput?
 
     uvicorn + the FastAPI app (api/main.py, the reference's app/main.py:205-344
@@ -330,7 +379,13 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
     runs in its own spawned process (``_api_server_proc``) and reaches this process's
     engine loop (engine/router.py ``serve_loop``) over two queues, so HTTP, parsing,
     tokenisation and validation never take the engine thread's GIL.  False: uvicorn in
-    a thread of this process on AsyncEngine (the in-process default)."""
+    a thread of this process on AsyncEngine (the in-process default).
+
+    Then, once the engine has drained, ``idle_requests`` single /parse-text/ requests
+    are sent one at a time from a client process: ``idle`` reports
+    the client-side p50 and the p50 of the service's own ``X-Process-Time`` header
+    (the reference's only latency instrumentation, app/main.py:92-113) -- the BASELINE
+    metric's "p50 /parse-text/ latency" measured through /parse-text/."""
     import multiprocessing as mp
 
     from ..api import main as api
@@ -422,11 +477,35 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
                    valid=round(ok / max(1, len(done_in)), 3),
                    http_latency_s=pcts([r[2] for r in sent_in]),
                    failed=sum(not r[3] for r in recs),
+                   failed_by=dict(collections.Counter(r[4] for r in recs if not r[3])),
                    burst_depth=burst_depth,
                    engine_depth={"mean": round(statistics.mean(win_depth), 1),
                                  "min": min(win_depth), "max": max(win_depth)}
                    if win_depth else None)
         res["status"] = "ok"
+        if idle_requests > 0:
+            # drain: what is left belongs to requests the clients gave up on
+            t_dr = time.time() + 30.0
+            while time.time() < t_dr and (engine.core.num_running + engine.core.num_waiting):
+                time.sleep(0.1)
+            idle_q = ctx.Queue()
+            ip = ctx.Process(target=_idle_client_proc,
+                             args=(url, idle_requests, 20_000_000 + seed, idle_q), daemon=True)
+            ip.start()
+            try:
+                recs_i = idle_q.get(timeout=max(30.0, 10.0 * idle_requests))
+            finally:
+                ip.join(timeout=10)
+                if ip.is_alive():
+                    ip.kill()
+            good = [r for r in recs_i if r[2]]
+            res["idle"] = {
+                "requests": len(recs_i), "valid": len(good),
+                "client_p50_s": round(statistics.median(r[0] for r in good), 4) if good else None,
+                "x_process_time_p50_s": (round(statistics.median(r[1] for r in good), 4)
+                                         if good else None),
+                "client_s": pcts([r[0] for r in good]) if good else None,
+                "engine_depth_at_start": engine.core.num_running + engine.core.num_waiting}
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line
         res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"
     finally:

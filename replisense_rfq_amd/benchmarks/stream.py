@@ -381,12 +381,22 @@ class DocStream:
 
 
 def token_shape(seqs) -> dict:
-    """Per-document token shape of a window's completions."""
+    """Per-document token shape of a window's completions.  ``sampled_share`` = sampled /
+    completion tokens (the reference's recorded completions: 0.524 on this grammar and
+    tokenizer, tests/engine/test_decode_shape.py); ``completion_tokens_p50`` /
+    ``sampled_tokens_p50`` compare with the recorded rows' 341.5 / 160."""
+    import statistics
+
     n = max(1, len(seqs))
+    gen = sum(s.num_generated for s in seqs)
+    samp = sum(s.num_sampled for s in seqs)
     return dict(
         prompt_tokens=sum(s.prompt_len for s in seqs) / n,
-        completion_tokens=sum(s.num_generated for s in seqs) / n,
-        sampled_tokens=sum(s.num_sampled for s in seqs) / n,
+        completion_tokens=gen / n,
+        sampled_tokens=samp / n,
+        sampled_share=samp / max(1, gen),
+        completion_tokens_p50=statistics.median([s.num_generated for s in seqs]) if seqs else 0,
+        sampled_tokens_p50=statistics.median([s.num_sampled for s in seqs]) if seqs else 0,
         prefix_hit_tokens=sum(s.prefix_hit_tokens for s in seqs) / n)
 
 

@@ -93,6 +93,8 @@ class PyGrammarFSM:
         prof, cnt, minv = st[5], st[2], st[4]
         combo = 1 if prof == PROFILE_SYNTHETIC else 0
         lim = g.max_items[ci] if prof == PROFILE_SYNTHETIC else 0
+        if lim and g.honors_min[ci] and 0 < minv < lim:
+            lim = minv          # SYNTHETIC + item hint: exactly the document's item count
         at_max = lim > 0 and cnt >= lim
         if at_max:
             combo |= 2

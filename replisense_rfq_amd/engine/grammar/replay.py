@@ -41,8 +41,13 @@ def _allowed(mask_rows: np.ndarray, row: int, token: int) -> bool:
 
 
 def grammar_tokens(executor, tok, text: str, mask_rows: np.ndarray, *, min_items: int = 0,
-                   profile: int = 0, budget: int = 1 << 30, max_steps: int = 20000) -> list[int]:
+                   profile: int = 0, budget: int = 1 << 30, max_steps: int = 20000,
+                   sampled: list | None = None) -> list[int]:
     """Token ids (sampled + forced) that make `executor` emit `text`.
+
+    ``sampled``: if a list is given it receives one bool per returned id -- True where
+    the decoder samples the token (one engine step), False where the grammar forces it
+    (jump-forward) -- so ``sum(sampled)`` is the serial step count of that completion.
 
     `executor`: an object with ``initial(min_items, profile, budget)``,
     ``advance(state, token, budget)`` and ``mask(state)`` (the native automaton or
@@ -60,6 +65,7 @@ def grammar_tokens(executor, tok, text: str, mask_rows: np.ndarray, *, min_items
 
     st, forced = executor.initial(min_items, profile, budget)
     out = list(forced)
+    flags = [False] * len(out)
     pos = spell(forced, 0)
     if pos < 0:
         raise GrammarError("the grammar's opening literal does not match the text")
@@ -82,6 +88,8 @@ def grammar_tokens(executor, tok, text: str, mask_rows: np.ndarray, *, min_items
     while True:
         if executor.mask(st) < 0:
             if pos == len(target):
+                if sampled is not None:
+                    sampled[:] = flags
                 return out
             cands = []                      # finished early: backtrack
         advanced = False
@@ -100,6 +108,7 @@ def grammar_tokens(executor, tok, text: str, mask_rows: np.ndarray, *, min_items
                 continue
             stack.append((st, pos, len(out), cands))
             out = out + [t] + list(f)
+            flags = flags + [True] + [False] * len(f)
             st, pos = nst, npos
             cands = candidates(st, pos)
             advanced = True
@@ -111,3 +120,4 @@ def grammar_tokens(executor, tok, text: str, mask_rows: np.ndarray, *, min_items
                                f"{target[max(0, pos - 40):pos + 40]!r}")
         st, pos, n, cands = stack.pop()
         out = out[:n]
+        flags = flags[:n]

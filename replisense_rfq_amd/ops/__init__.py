@@ -23,6 +23,7 @@ __all__ = [
     "rope_plan", "qkv_rope", "moe_route", "attn_decode_shared", "SHARED_PREFIX_MIN_ROWS",
     "gemm_dense", "gemm_dense_ok", "swiglu_large", "tile_weight", "untile_weight",
     "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT", "SPLITK_PERSIST",
+    "ROWS_BIT", "ROWS_MAX_M", "ROWS_CFGS", "ROWS_CFGS_PAIRED", "rows_ok",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -164,6 +165,21 @@ SPLITK_CFGS = (0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14)
 SPLITK_TILED = 16        # split-K GEMV cfg bit: W in the decode-tiled layout (tile_weight)
 SPLITK_NT = 32           # split-K GEMV cfg bit: non-temporal weight loads
 SPLITK_PERSIST = 64      # split-K GEMV cfg bit: persistent grid (tiled layout only)
+
+# plan cfg bit: the row-streaming GEMV (csrc/kernels/gemv_rows.hip; low 4 bits = its cfg:
+# [1:0] rows per wave = 1 << b, [3:2] 1 KB chunks in flight = 2 << b).  One wave per
+# weight row over the full K, no cross-workgroup hand-off; M <= ROWS_MAX_M, K % 512 == 0,
+# row-major weights.  Measured on MI355X at M = 1 (profiles/r5_gemv_rows.md): 1.2-1.5x
+# the split-K GEMV on the 70B TP=8 shard and 8B shapes.
+ROWS_BIT = 256
+ROWS_MAX_M = 4
+ROWS_CFGS = (4, 8, 12, 5, 9, 2, 6, 3)      # (RW, CU) = (1,4) (1,8) (1,16) (2,4) (2,8) (4,2) (4,4) (8,2)
+ROWS_CFGS_PAIRED = (4, 8, 12)             # SwiGLU / RoPE epilogues: one row per wave
+
+
+def rows_ok(M: int, K: int, w: torch.Tensor) -> bool:
+    """Shapes the row-streaming GEMV takes (host mirror of torch_ops.cpp check_rows)."""
+    return 1 <= M <= ROWS_MAX_M and K % 512 == 0 and w.is_contiguous() and not tiled_only(w)
 
 
 def tile_weight(w: torch.Tensor) -> torch.Tensor:
@@ -378,7 +394,9 @@ def linear_swiglu(x, w):
             if cfg < 0 or (tiled_only(w) and not (cfg & SPLITK_BIT and cfg & SPLITK_TILED)):
                 return None
             out = torch.empty((M, F), dtype=x.dtype, device=x.device)
-            if cfg & SPLITK_BIT:
+            if cfg & ROWS_BIT:
+                _native.ops().gemv_rows_swiglu(x, w, out, cfg & 15)
+            elif cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
                 _native.ops().gemv_splitk_swiglu(x, _wsel(w, cfg), out, part, tiles, cfg & 127)
             else:
@@ -417,7 +435,10 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
             cfg = -1
         if cfg >= 0:
             qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-            if cfg & SPLITK_BIT:
+            if cfg & ROWS_BIT:
+                _native.ops().gemv_rows_rope(x, w, qkv, positions, cos_sin, slot_mapping,
+                                             k_cache, v_cache, Hq, Hkv, cfg & 15)
+            elif cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
                 _native.ops().gemv_splitk_rope(x, _wsel(w, cfg), qkv, positions, cos_sin,
                                                slot_mapping, k_cache, v_cache, Hq, Hkv, part,
@@ -613,6 +634,9 @@ def linear(x, w, out=None, plan: int | None = None):
         if cfg >= 0:
             if out is None:
                 out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            if cfg & ROWS_BIT:
+                _native.ops().gemv_rows(x, w, out, cfg & 15)
+                return out
             if cfg & SPLITK_BIT:
                 part, tiles = splitk_ws(x.device)
                 _native.ops().gemv_splitk(x, _wsel(w, cfg), out, part, tiles, cfg & 127)

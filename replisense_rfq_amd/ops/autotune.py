@@ -15,8 +15,8 @@ import time
 
 import torch
 
-from . import (SPLITK_BIT, SPLITK_CFGS, SPLITK_NT, SPLITK_TILED, _native, _wsel, gemm_dense_ok,
-               gemm_w4_ok,
+from . import (ROWS_BIT, ROWS_CFGS, ROWS_CFGS_PAIRED, SPLITK_BIT, SPLITK_CFGS, SPLITK_NT,
+               SPLITK_TILED, _native, _wsel, gemm_dense_ok, gemm_w4_ok, rows_ok,
                set_linear_plan, set_merge_plan, set_norm_plan, set_rope_plan, set_silu_plan,
                set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
@@ -154,6 +154,12 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
                               ws, reps)
                     if t < t_best:
                         best, t_best = c | SPLITK_BIT, t
+            if rows_ok(M, K, ws[0]):
+                # row-streaming GEMV (one wave per row, full K): M <= 4
+                for c in ROWS_CFGS:
+                    t = _time(lambda w, c=c: ops.gemv_rows(x, w, out, c), ws, reps)
+                    if t < t_best:
+                        best, t_best = c | ROWS_BIT, t
             plan[(M, N, K)] = best
             report.append((name, M, N, K, round(t_lib, 1), best, round(min(t_best, t_lib), 1)))
     return plan, report
@@ -344,6 +350,11 @@ def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: fl
                       ws, reps)
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
+        if rows_ok(M, K, ws[0]):
+            for c in ROWS_CFGS_PAIRED:
+                t = _time(lambda w, c=c: ops.gemv_rows_swiglu(x, w, act, c), ws, reps)
+                if t < t_best:
+                    best, t_best = c | ROWS_BIT, t
         if best >= 0:
             plan[(M, F, K)] = best
         report.append(("gate_up+swiglu", M, N2, K, round(t_ref, 1), best,
@@ -394,6 +405,12 @@ def tune_rope(ws: list[torch.Tensor], ms: list[int], cos_sin: torch.Tensor, hq: 
                       ws, reps)
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
+        if rows_ok(M, K, ws[0]):
+            for c in ROWS_CFGS_PAIRED:
+                t = _time(lambda w, c=c: ops.gemv_rows_rope(x, w, qkv, pos, cos_sin, slots, kc, vc,
+                                                            hq, hkv, c), ws, reps)
+                if t < t_best:
+                    best, t_best = c | ROWS_BIT, t
         if best >= 0:
             plan[(M, N, K)] = best
         report.append(("qkv+rope", M, N, K, round(t_ref, 1), best, round(min(t_best, t_ref), 1)))
@@ -639,6 +656,7 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
             log.info("gemm split %-14s M=%-5d N=%-6d K=%-6d lib %.1fus -> %s %.1fus", *r)
     for r in report:
         sel = "lib" if r[5] < 0 else (
+            f"rows{r[5] & 15}" if r[5] & ROWS_BIT else
             (f"splitk{r[5] & 15}" + ("t" if r[5] & SPLITK_TILED else "")
              + ("n" if r[5] & SPLITK_NT else ""))
             if r[5] & SPLITK_BIT else f"skinny{r[5]}")

@@ -6,7 +6,8 @@ mentions (mixed letters+digits such as ``62GB-56T-16-8S``, ``ACX-4015-03``,
 benchmark passes it to the grammar as ``min_items`` so a constrained decode emits
 one ``line_items`` object per requested part -- what a trained extraction model
 does and what the reference's recorded completions show (cache.db rows 11-14: 4,
-4, 3 and 23 items).  The service path applies it only with ``RFQ_DECODE_HINTS=1``
+4, 3 and 23 items).  Under the SYNTHETIC profile the item count is then exact
+(min_items = max), capped at the profile's item limit.  The service path applies it only with ``RFQ_DECODE_HINTS=1``
 (load tests on random weights).  Emails and phone numbers are excluded; the count
 is clamped to the SYNTHETIC profile's item limit.
 """
@@ -32,6 +33,13 @@ def decode_hints_for(document: str, enabled: bool) -> dict:
     from ..engine.grammar import PROFILE_SYNTHETIC
 
     return {"min_items": estimate_line_items(document), "profile": PROFILE_SYNTHETIC}
+
+
+def synthetic_item_limit() -> int:
+    """The SYNTHETIC profile's line-item cap (engine/grammar/compiler.py Limits)."""
+    from ..engine.grammar import Limits
+
+    return Limits().max_items
 
 
 def estimate_line_items(text: str, limit: int = 8) -> int:

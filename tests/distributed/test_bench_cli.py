@@ -189,7 +189,7 @@ def test_bench_extra_phases_cpu():
                 "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
                 "--latency-runs", "1", "--phases", "http_open,http,mixtral,70b",
                 "--http-open-rate", "3", "--http-open-warm", "2", "--http-open-measure", "4",
-                "--http-docs", "6",
+                "--http-idle-requests", "3", "--http-docs", "6",
                 "--http-clients", "3", "--mixtral-model", "tiny-mixtral",
                 "--mixtral-in-flight", "4", "--mixtral-warm", "2", "--mixtral-docs", "4",
                 "--big-model", "tiny-llama70", "--big-latency-runs", "1"], timeout=800)
@@ -201,6 +201,16 @@ def test_bench_extra_phases_cpu():
     assert o["layout"] == "api process + engine process" and o["responses"] >= o["docs"]
     assert o["docs_per_s"] > 0 and o["valid"] == 1.0 and o["http_latency_s"]["p50"] > 0
     assert o["http_vs_engine"] > 0
+    assert o["failed_by"] == {}, o
+    # the metric's p50 /parse-text/ comes from HTTP responses
+    idle = o["idle"]
+    assert idle["requests"] == 3 and idle["valid"] == 3, idle
+    assert idle["client_p50_s"] > 0 and idle["x_process_time_p50_s"] > 0
+    assert idle["client_p50_s"] >= idle["x_process_time_p50_s"] * 0.9
+    assert out["p50_parse_text_latency_s"] == idle["client_p50_s"]
+    assert out["p50_parse_text_source"].startswith("HTTP POST /parse-text/")
+    assert out["p50_x_process_time_s"] == idle["x_process_time_p50_s"]
+    assert out["p50_engine_latency_s"] > 0
     h = ph["http_upload"]
     assert h["status"] == "ok" and h["docs"] == 6 and h["valid"] == 1.0, h
     assert h["docs_per_s"] > 0 and h["http_latency_s"]["n"] == 6
