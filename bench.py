@@ -83,14 +83,14 @@ def parse():
     ap.add_argument("--phases", default="auto",
                     help="extra phases after the timed window: comma list of http, mixtral, "
                          "70b; 'auto' = all on the 1-GPU run of the 8B bench, 'none' = off")
-    ap.add_argument("--phase-budget", type=float, default=400.0,
+    ap.add_argument("--phase-budget", type=float, default=330.0,
                     help="seconds for all extra phases together (each is bounded; a watchdog "
                          "prints the JSON line if they overrun)")
     ap.add_argument("--http-open-rate", type=float, default=0.0,
                     help="open-loop HTTP phase: offered requests/s (0 = 90 %% of the "
                          "timed window's docs/s per replica)")
-    ap.add_argument("--http-open-warm", type=float, default=30.0)
-    ap.add_argument("--http-open-measure", type=float, default=40.0)
+    ap.add_argument("--http-open-warm", type=float, default=25.0)
+    ap.add_argument("--http-open-measure", type=float, default=35.0)
     ap.add_argument("--http-open-burst", type=float, default=0.75,
                     help="open-loop HTTP phase: initial burst as a fraction of the "
                          "in-flight depth (starts the queue near its steady state)")
@@ -99,12 +99,17 @@ def parse():
                          "a time after the window (the metric's p50 /parse-text/ latency)")
     ap.add_argument("--http-docs", type=int, default=512)
     ap.add_argument("--http-clients", type=int, default=64)
+    ap.add_argument("--depth-in-flight", type=int, default=160,
+                    help="latency-bounded depth phase: documents in flight (loaded p50 ~2 s)")
+    ap.add_argument("--depth-docs", type=int, default=640)
     ap.add_argument("--mixtral-model", default="mixtral-8x7b")
     ap.add_argument("--mixtral-in-flight", type=int, default=768)
     ap.add_argument("--mixtral-warm", type=int, default=768)
     ap.add_argument("--mixtral-docs", type=int, default=1536)
     ap.add_argument("--big-model", default="llama3-70b")
-    ap.add_argument("--big-latency-runs", type=int, default=5)
+    ap.add_argument("--big-latency-runs", type=int, default=14,
+                    help="70B phase: single requests over the reference's 14 recorded prompts "
+                         "(a fixed set; fewer if the phase budget runs out)")
     ap.add_argument("--tp-latency-runs", type=int, default=7)
     ap.add_argument("--tp-docs", type=int, default=256,
                     help="TP phase: documents timed in a continuous stream (0 = skip)")
@@ -133,8 +138,8 @@ def _phase_list(args, world: int) -> list:
     if v in ("", "none", "0"):
         return []
     if v == "auto":
-        return ["http_open", "http", "mixtral", "70b"] if (world == 1 and args.tp == 1
-                                                           and args.model == "llama3-8b") else []
+        return (["http_open", "http", "depth", "mixtral", "70b"]
+                if (world == 1 and args.tp == 1 and args.model == "llama3-8b") else [])
     return [p for p in v.split(",") if p]
 
 
@@ -568,6 +573,13 @@ def main():
             out["phases"]["http_upload"] = ph.http_upload_phase(
                 engine, n_docs=args.http_docs, clients=args.http_clients,
                 budget_s=min(120.0, left()), seed=args.seed)
+        if "depth" in phases:
+            mark("phase:depth")
+            d = ph.depth_phase(engine, in_flight=args.depth_in_flight,
+                               warm_docs=args.depth_in_flight, docs=args.depth_docs,
+                               budget_s=min(60.0, left()), seed=args.seed)
+            d["headline_in_flight"] = args.max_num_seqs
+            out["phases"]["latency_bounded_depth"] = d
         import gc
 
         if hb is not None:
@@ -587,7 +599,7 @@ def main():
             mark("phase:70b")
             out["phases"]["llama3_70b"] = ph.model_phase(
                 args.big_model, seed=args.seed, latency_runs=args.big_latency_runs,
-                budget_s=left(), in_flight=8)
+                budget_s=left(), in_flight=8, reference_set=True)
         guard.cancel()
         out["phases"]["phase_s"] = round(time.perf_counter() - t_ph, 1)
         out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)

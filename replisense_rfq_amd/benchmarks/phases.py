@@ -30,7 +30,8 @@ import statistics
 import threading
 import time
 
-from .stream import (DocStream, latency, loaded_latency, pcts, single_stream, validate)
+from .stream import (DocStream, latency, latency_reference, loaded_latency, pcts, single_stream,
+                     validate)
 
 BASELINE_P50_S = 0.883            # Groq llama3-70b p50 server time per request
 
@@ -541,9 +542,54 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
 
 
 # --------------------------------------------------------------- model phases
+def depth_phase(engine, in_flight: int, warm_docs: int, docs: int, budget_s: float = 60.0,
+                seed: int = 0) -> dict:
+    """throughput at a latency-bounded depth.  The headline runs at
+    the deepest in-flight count whose loaded p99 stays inside the 30 s request deadline;
+    here the SAME engine serves the same document stream at ``in_flight`` documents
+    (sized so the loaded p50 stays near 2 s) and reports docs/s and the loaded latency
+    of the ``docs`` documents completed after ``warm_docs`` of warm-up."""
+    import torch
+
+    t_start = time.perf_counter()
+    deadline = t_start + budget_s
+    res = {"in_flight": in_flight, "status": "running"}
+    stream = None
+    try:
+        stream = DocStream(engine, 0, seed + 3, in_flight)
+        on_gpu = engine.device.type == "cuda"
+        if stream.run_until(warm_docs, deadline):
+            stream.clear_window()
+            if on_gpu:
+                torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            done = stream.run_until(warm_docs + docs, deadline)
+            if on_gpu:
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t1
+            n = len(stream.finished)
+            ll = loaded_latency(stream.finished)
+            res.update(docs=n, docs_per_s=round(n / dt, 3), seconds=round(dt, 1),
+                       loaded_latency_s=ll["e2e_s"], loaded_ttft_s=ll["ttft_s"],
+                       valid=round(stream.window_valid(), 3),
+                       status="ok" if done else "timeout")
+        else:
+            res["status"] = "timeout"
+    except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+        res["status"] = f"error: {type(e).__name__}: {str(e)[:200]}"
+    finally:
+        if stream is not None:
+            stream.close()
+        if engine.has_work():
+            engine.abort_all("abort")
+    res["phase_s"] = round(time.perf_counter() - t_start, 1)
+    return res
+
+
 def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 0,
                 docs: int = 0, latency_runs: int = 0, formats: tuple | None = None,
-                budget_s: float = 120.0, parse_procs: int = 4, **cfg_over) -> dict:
+                budget_s: float = 120.0, parse_procs: int = 4, reference_set: bool = False,
+                **cfg_over) -> dict:
     """Build ``model`` on this GPU, then (a) ``latency_runs`` idle single requests and
     (b) a closed-loop stream of ``docs`` documents at ``in_flight`` after
     ``warm_docs`` of warm-up; free everything before returning."""
@@ -563,7 +609,20 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
         cfg = EngineConfig.from_env(model=model, seed=seed, max_num_seqs=nseq, **cfg_over)
         eng = LLMEngine(cfg)
         res["init_s"] = round(time.perf_counter() - t_start, 1)
-        if latency_runs:
+        if latency_runs and reference_set:
+            # a FIXED latency set -- the reference's 14 recorded prompts
+            lat, detail, rows = latency_reference(eng, latency_runs,
+                                                  deadline=deadline - 10.0 if docs else deadline)
+            if lat:
+                res["latency_set"] = "reference prompts (cache.db rows 1-14), bench hints"
+                res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
+                res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
+                res["single_stream"] = single_stream(detail)
+                res["runs"] = len(lat)
+                res["sampled_steps_p50"] = statistics.median(r[1] for r in rows)
+                res["per_row"] = [{"row": a, "sampled": b, "tokens": c, "prompt": d,
+                                   "s": round(t, 3)} for (a, b, c, d), t in zip(rows, lat)]
+        elif latency_runs:
             lat, detail = latency(eng, 0, latency_runs)
             res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
             res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)

@@ -464,6 +464,48 @@ def latency(engine, dp_rank: int, runs: int):
     return out, detail
 
 
+def reference_requests() -> list[dict]:
+    """The reference's 14 recorded requests to llama3-70b-8192 (cache.db rows 1-14):
+    system + user message exactly as the reference sent them, the document inside the
+    user message (for the decoding hint), and Groq's usage telemetry."""
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "reference_prompts.json")) as f:
+        return json.load(f)["rows"]
+
+
+def latency_reference(engine, runs: int = 14, deadline: float | None = None):
+    """Single-request latency over a FIXED set: the reference's own recorded prompts
+    (the same prefill Groq saw), decoded with the bench's hints (SYNTHETIC profile, item
+    count from the document) so random-init weights produce the reference's decode shape.
+    Deterministic per (weights seed, prompt), so two runs differ only by timing noise.
+    Returns (latencies, detail) like ``latency``, plus the per-row (row, sampled steps,
+    completion tokens) list."""
+    from ..engine.grammar import PROFILE_SYNTHETIC
+    from ..service.extract import parse_and_validate_response
+    from ..service.hints import estimate_line_items
+
+    out, detail, rows = [], [], []
+    tok = engine.tokenizer
+    for r in reference_requests()[:runs]:
+        if deadline is not None and time.perf_counter() > deadline:
+            break
+        msgs = [{"role": "system", "content": r["system"]}, {"role": "user", "content": r["user"]}]
+        t0 = time.perf_counter()
+        ids = tok.chat_ids(msgs)
+        params = engine.default_params(min_items=estimate_line_items(r["document"]),
+                                       profile=PROFILE_SYNTHETIC)
+        s, = engine.generate([ids], params)
+        res = parse_and_validate_response(engine.decode_text(s), "direct_text_input")
+        out.append(time.perf_counter() - t0)
+        ok = bool(res.get("success")) and "validation warnings" not in res.get("message", "")
+        detail.append((s.num_generated, s.num_sampled, s.span().get("ttft_ms") or 0.0, out[-1],
+                       ok))
+        rows.append((r["row"], s.num_sampled, s.num_generated, len(ids)))
+    return out, detail, rows
+
+
 def single_stream(detail):
     """Single-request decode rates (Groq 350 tok/s per stream): output
     tokens/s after the first token, and the sampled (non-jump-forward) step rate."""

@@ -187,12 +187,13 @@ def test_bench_extra_phases_cpu():
     phase, all in the same JSON line (tiny models of the same architectures here)."""
     out = _run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0",
                 "--model", "tiny-llama", "--docs-per-step", "2", "--max-num-seqs", "4",
-                "--latency-runs", "1", "--phases", "http_open,http,mixtral,70b",
+                "--latency-runs", "1", "--phases", "http_open,http,depth,mixtral,70b",
+                "--depth-in-flight", "2", "--depth-docs", "2",
                 "--http-open-rate", "3", "--http-open-warm", "2", "--http-open-measure", "4",
                 "--http-idle-requests", "3", "--http-docs", "6",
                 "--http-clients", "3", "--mixtral-model", "tiny-mixtral",
                 "--mixtral-in-flight", "4", "--mixtral-warm", "2", "--mixtral-docs", "4",
-                "--big-model", "tiny-llama70", "--big-latency-runs", "1"], timeout=800)
+                "--big-model", "tiny-llama70", "--big-latency-runs", "2"], timeout=800)
     ph = out["phases"]
     o = ph["http_open_loop"]
     assert o["status"] == "ok", o
@@ -211,6 +212,9 @@ def test_bench_extra_phases_cpu():
     assert out["p50_parse_text_source"].startswith("HTTP POST /parse-text/")
     assert out["p50_x_process_time_s"] == idle["x_process_time_p50_s"]
     assert out["p50_engine_latency_s"] > 0
+    dp = ph["latency_bounded_depth"]
+    assert dp["status"] == "ok" and dp["in_flight"] == 2 and dp["docs"] >= 2, dp
+    assert dp["docs_per_s"] > 0 and dp["loaded_latency_s"]["p50"] > 0 and dp["valid"] == 1.0
     h = ph["http_upload"]
     assert h["status"] == "ok" and h["docs"] == 6 and h["valid"] == 1.0, h
     assert h["docs_per_s"] > 0 and h["http_latency_s"]["n"] == 6
@@ -219,7 +223,10 @@ def test_bench_extra_phases_cpu():
     assert m["docs"] >= 4 and m["formats"] == ["pdf", "xlsx"] and m["per_doc"]["valid"] == 1.0
     assert m["loaded_latency_s"]["p50"] > 0
     b = ph["llama3_70b"]
-    assert b["status"] == "ok" and b["runs"] == 1 and b["p50_parse_text_latency_s"] > 0, b
+    assert b["status"] == "ok" and b["runs"] == 2 and b["p50_parse_text_latency_s"] > 0, b
+    # the fixed latency set is the reference's recorded prompts
+    assert b["latency_set"].startswith("reference prompts")
+    assert [r["row"] for r in b["per_row"]] == [1, 2] and all(r["sampled"] > 0 for r in b["per_row"])
     assert out["value"] > 0 and out["steps"] == 1
 
 
@@ -229,7 +236,7 @@ def test_bench_phases_auto_only_on_one_gpu_8b():
 
     class A:
         phases, tp, model = "auto", 1, "llama3-8b"
-    assert bench._phase_list(A, 1) == ["http_open", "http", "mixtral", "70b"]
+    assert bench._phase_list(A, 1) == ["http_open", "http", "depth", "mixtral", "70b"]
     assert bench._phase_list(A, 8) == [] and bench._phase_list(A, 2) == []
     A.model = "tiny-llama"
     assert bench._phase_list(A, 1) == []
