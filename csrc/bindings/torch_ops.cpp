@@ -40,10 +40,10 @@ void launch_gemv_splitk_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf
 void launch_gemv_rows(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
                       hipStream_t);
 void launch_gemv_rows_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t,
-                             int, int, hipStream_t);
+                             int, int, float, hipStream_t);
 void launch_gemv_rows_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                            int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*, int,
-                           int, int, hipStream_t);
+                           int, int, float, hipStream_t);
 void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
                      float*, unsigned*, const int32_t*, const float*, const int32_t*, bf16_t*,
                      bf16_t*, int, int, int, const int32_t*, int, const int32_t*,
@@ -302,28 +302,35 @@ static void check_rows(const char* what, const Tensor& x, const Tensor& w, const
   TORCH_CHECK(w.numel() < ((int64_t)1 << 40), what, ": weight too large");
   TORCH_CHECK(y.size(0) == M && y.size(1) == y_cols, what, ": y shape");
   TORCH_CHECK(x.stride(0) % 8 == 0, what, ": x rows must be 16-byte aligned");
-  TORCH_CHECK(cfg >= 0 && cfg < 16, what, ": cfg");
+  TORCH_CHECK(cfg >= 0 && cfg < 64, what, ": cfg");
 }
 
+// cfg bit 5: y is the residual stream, y <- bf16(x . w^T) + y (residual add)
 void gemv_rows(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cfg) {
   check_rows("gemv_rows", x, w, y, cfg, w.size(0));
+  TORCH_CHECK(!(cfg & 16), "gemv_rows: cfg bit 4 (normalised x) is for the SwiGLU / RoPE forms");
   rfq::launch_gemv_rows(bp(x), x.stride(0), bp(w), w.size(0), x.size(1), bpm(y), y.stride(0),
                         x.size(0), (int)cfg, cur_stream());
 }
 
-void gemv_rows_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg) {
+// cfg bit 4: x is the un-normalised residual, w carries the RMSNorm weight folded in
+// (rows scaled by rsqrt(mean(x^2) + eps) in the kernel)
+void gemv_rows_swiglu(const Tensor& x, const Tensor& w, const Tensor& out, int64_t cfg,
+                      double eps) {
   const int64_t F = w.size(0) / 2;
   TORCH_CHECK(w.size(0) == 2 * F, "gemv_rows_swiglu: w [2F, K]");
   check_rows("gemv_rows_swiglu", x, w, out, cfg, F);
+  TORCH_CHECK(!(cfg & 32), "gemv_rows_swiglu: cfg bit 5 (residual add) is for the plain form");
   rfq::launch_gemv_rows_swiglu(bp(x), x.stride(0), bp(w), (int)F, x.size(1), bpm(out),
-                               out.stride(0), x.size(0), (int)cfg, cur_stream());
+                               out.stride(0), x.size(0), (int)cfg, (float)eps, cur_stream());
 }
 
 void gemv_rows_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
                     const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
-                    const Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t cfg) {
+                    const Tensor& v_cache, int64_t Hq, int64_t Hkv, int64_t cfg, double eps) {
   const int64_t N = w.size(0);
   check_rows("gemv_rows_rope", x, w, qkv, cfg, N);
+  TORCH_CHECK(!(cfg & 32), "gemv_rows_rope: cfg bit 5 (residual add) is for the plain form");
   CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
   TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "gemv_rows_rope: w must be [(Hq + 2 Hkv) * 128, K]");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
@@ -339,7 +346,7 @@ void gemv_rows_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const T
                              qkv.stride(0), x.size(0), (int)cfg, positions.data_ptr<int32_t>(),
                              cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int32_t>(),
                              bpm(k_cache), bpm(v_cache), (int)Hq, (int)Hkv, k_cache.size(2),
-                             cur_stream());
+                             (float)eps, cur_stream());
 }
 
 // Fused QKV projection + RoPE + KV append + split-K decode attention in ONE launch
@@ -1142,10 +1149,10 @@ TORCH_LIBRARY(rfq_amd, m) {
         "float eps, Tensor(c!) out, Tensor(d!) counter, Tensor(e!) partials, int cfg) -> ()");
   m.def("skinny_gemm_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
   m.def("gemv_rows(Tensor x, Tensor w, Tensor(a!) y, int cfg) -> ()");
-  m.def("gemv_rows_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg) -> ()");
+  m.def("gemv_rows_swiglu(Tensor x, Tensor w, Tensor(a!) out, int cfg, float eps=0.0) -> ()");
   m.def("gemv_rows_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
-        "int cfg) -> ()");
+        "int cfg, float eps=0.0) -> ()");
   m.def("gemv_splitk(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) part, Tensor(c!) tile_cnt, "
         "int cfg) -> ()");
   m.def("gemv_splitk_norm(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) residual, Tensor norm_w, "

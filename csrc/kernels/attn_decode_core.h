@@ -504,66 +504,69 @@ __device__ __forceinline__ void attn_decode_body(
   if (prev != (unsigned)num_splits - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
   if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // The merge uses the whole wave per group of 4 columns: lane l serves column
+  // 4 r + (l >> 4) and split j = l & 15 of the (max, sum) pairs, and dims
+  // [8 j, 8 j + 8) of every split's partial row.  Every split's partial loads of the
+  // group are issued at once (32 x 16 B per lane), so a group costs ONE dependent round
+  // trip, not one per split pair (the r2 form: 8 chained rounds for 16 splits).
+  const int mj = lane & 15, mq = lane >> 4;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    if (!act[t] || !cvalid[t]) continue;
-    const int64_t pbase = ((int64_t)qrow[t] * Hq + h[t]) * num_splits;
-    // every split's (max, sum) in flight at once (num_splits <= 16), then the partial
-    // rows 2 splits at a time: the merge is a few memory round trips, not 16 chained
-    float ms[16], ls[16];
+    if (!act[t]) continue;
 #pragma unroll
-    for (int sp = 0; sp < 16; ++sp) {
-      ms[sp] = -INFINITY;
-      ls[sp] = 0.f;
-      if (sp < num_splits) {
-        const unsigned long long x = __hip_atomic_load((const gu64*)(part_ml + (pbase + sp) * 2),
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ms[sp] = __uint_as_float((unsigned)x);
-        ls[sp] = __uint_as_float((unsigned)(x >> 32));
-      }
-    }
-    float gm = -INFINITY;
+    for (int r = 0; r < 4; ++r) {
+      const int cc = 4 * r + mq;                          // column this lane merges
+      const int v_cc = __shfl((int)cvalid[t], cc, 64);
+      const int q_cc = __shfl(qrow[t], cc, 64), h_cc = __shfl(h[t], cc, 64);
+      if (!__builtin_amdgcn_ballot_w64(v_cc != 0)) continue;       // wave-uniform: group empty
+      const int64_t pbase = ((int64_t)q_cc * Hq + h_cc) * num_splits;
+      const bool live = v_cc != 0;
+      // (max, sum) of split mj, and every split's dims [8 mj, 8 mj + 8)
+      unsigned long long mlx = 0xff800000ull;             // (-inf, 0)
+      if (live && mj < num_splits)
+        mlx = __hip_atomic_load((const gu64*)(part_ml + (pbase + mj) * 2), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+      f32x4 pv[16][2];
 #pragma unroll
-    for (int sp = 0; sp < 16; ++sp) gm = fmaxf(gm, ms[sp]);
-    f32x4 num[8];
+      for (int sp = 0; sp < 16; ++sp) {
+        if (live && sp < num_splits) {
+          const gu64* d = (const gu64*)(part_o + (pbase + sp) * kD + 8 * mj);
 #pragma unroll
-    for (int m = 0; m < 8; ++m) num[m] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float den = 0.f;
-    if (gm != -INFINITY) {
-#pragma unroll
-      for (int s0 = 0; s0 < 16; s0 += 2) {
-        if (s0 >= num_splits) break;
-        f32x4 pv[2][8];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float* po = part_o + (pbase + min(s0 + u, num_splits - 1)) * kD;
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const gu64* d = (const gu64*)(po + 16 * m + 4 * g);
-            const unsigned long long x0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long x1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pv[u][m] = (f32x4){__uint_as_float((unsigned)x0), __uint_as_float((unsigned)(x0 >> 32)),
-                               __uint_as_float((unsigned)x1), __uint_as_float((unsigned)(x1 >> 32))};
+          for (int u = 0; u < 2; ++u) {
+            const unsigned long long x0 =
+                __hip_atomic_load(d + 2 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x1 =
+                __hip_atomic_load(d + 2 * u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pv[sp][u] = (f32x4){__uint_as_float((unsigned)x0), __uint_as_float((unsigned)(x0 >> 32)),
+                                __uint_as_float((unsigned)x1), __uint_as_float((unsigned)(x1 >> 32))};
           }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int sp = s0 + u;
-          const float wgt = (sp < num_splits && ms[sp] != -INFINITY) ? fast_exp2(ms[sp] - gm) : 0.f;
-          den += wgt * ls[sp];
-#pragma unroll
-          for (int m = 0; m < 8; ++m) num[m] += wgt * pv[u][m];
+        } else {
+          pv[sp][0] = pv[sp][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
       }
-    }
-    const float inv = den > 0.f ? 1.f / den : 0.f;
-    bf16_t* orow = out + (int64_t)qrow[t] * out_stride + (int64_t)h[t] * kD;
+      const float m_j = __uint_as_float((unsigned)mlx), l_j = __uint_as_float((unsigned)(mlx >> 32));
+      float gm = m_j;                                     // max over the 16 lanes of the column
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      uint2 wv;
-      wv.x = pack_bf16x2(num[m][0] * inv, num[m][1] * inv);
-      wv.y = pack_bf16x2(num[m][2] * inv, num[m][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * m + 4 * g) = wv;
+      for (int o2 = 1; o2 < 16; o2 <<= 1) gm = fmaxf(gm, __shfl_xor(gm, o2, 64));
+      const float w_j = (gm == -INFINITY || m_j == -INFINITY) ? 0.f : fast_exp2(m_j - gm);
+      float den = w_j * l_j;
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) den += __shfl_xor(den, o2, 64);
+      f32x4 num[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int sp = 0; sp < 16; ++sp) {
+        const float wsp = __shfl(w_j, (lane & 48) | sp, 64);   // split sp's weight
+#pragma unroll
+        for (int u = 0; u < 2; ++u) num[u] += wsp * pv[sp][u];
+      }
+      if (!live) continue;
+      const float inv = den > 0.f ? 1.f / den : 0.f;
+      uint4 ov;
+      ov.x = pack_bf16x2(num[0][0] * inv, num[0][1] * inv);
+      ov.y = pack_bf16x2(num[0][2] * inv, num[0][3] * inv);
+      ov.z = pack_bf16x2(num[1][0] * inv, num[1][1] * inv);
+      ov.w = pack_bf16x2(num[1][2] * inv, num[1][3] * inv);
+      *reinterpret_cast<uint4*>(out + (int64_t)q_cc * out_stride + (int64_t)h_cc * kD + 8 * mj) = ov;
     }
   }
 }

@@ -30,12 +30,24 @@
 //   kRwRope   waves 2j / 2j+1 own the rotate-half partners h*128 + d and h*128 + 64 + d
 //             of one head: NeoX RoPE on the fp32 sums (as gemv_core.h kGvRope), q to Y,
 //             k / v appended to the paged cache (slot -1 = padding: no write).
+//
+// Folded-norm forms (FL, the TP = 1 latency path, models/llama.py _forward_fold):
+//   kRwNormX  (SwiGLU / RoPE) X is the UN-normalised residual stream and W carries the
+//             RMSNorm weight folded into its columns (W' = W diag(g), DecoderLM
+//             fold_norms): rmsnorm(x) g . W^T = rsqrt(mean(x^2) + eps) (x . W'^T).  Every
+//             wave reads the whole X row anyway, so it also accumulates sum(x^2) with the
+//             same dot2 (x . x) and scales its sums once: no norm launch, no cross-
+//             workgroup reduction.
+//   kRwResAdd (plain) Y is the residual stream: Y <- bf16(bf16(x . W^T) + Y), the
+//             residual add of the o / down projections (what fused_add_rms_norm did
+//             before the norm itself moved into the next projection).
 #include "common.h"
 #include "gemv_core.h"
 
 namespace rfq {
 
 enum { kRwPlain = 0, kRwSwi = 1, kRwRope = 2 };
+enum { kRwNormX = 1, kRwResAdd = 2 };
 constexpr int kRwWaves = 4;          // waves per workgroup
 constexpr int kRwMaxM = 4;
 
@@ -86,11 +98,14 @@ __device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, int voff, int s
 
 // MM: token capacity (runtime M <= MM); RW: rows per wave (plain only; paired epilogues
 // use one row per wave); CU: 1 KB chunks per row in flight per loop iteration.
-template <int MM, int RW, int CU, int EPI, bool NTL>
+template <int MM, int RW, int CU, int EPI, bool NTL, int FL = 0>
 __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int N, int K,
-    bf16_t* __restrict__ Y, int64_t ldy, int M, int up_off, RopeEpi re) {
+    bf16_t* __restrict__ Y, int64_t ldy, int M, int up_off, RopeEpi re, float eps) {
   static_assert(EPI == kRwPlain || RW == 1, "paired epilogues: one row per wave");
+  static_assert(!(FL & kRwNormX) || EPI != kRwPlain, "normalised X: SwiGLU / RoPE forms");
+  static_assert(!(FL & kRwResAdd) || EPI == kRwPlain, "residual add: plain form");
+  constexpr bool NX = FL & kRwNormX;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int gw = blockIdx.x * kRwWaves + wave;
@@ -109,11 +124,13 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     row0 = (q >> 6) * 128 + (q & 63) + ((wave & 1) ? 64 : 0);
     valid = q < N;
   }
-  float acc[RW][MM];
+  float acc[RW][MM], ssq[MM];
 #pragma unroll
   for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[r][m] = 0.f;
+#pragma unroll
+  for (int m = 0; m < MM; ++m) ssq[m] = 0.f;
   if (valid) {
     const int nch = K >> 9;
     // W: the wave's RW rows (wave-uniform base, RW * K * 2 bytes); X: the M token rows,
@@ -142,6 +159,12 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
         for (int r = 0; r < RW; ++r)
 #pragma unroll
           for (int m = 0; m < MM; ++m) acc[r][m] = dot8(w[r][u], x[m][u], acc[r][m]);
+      if constexpr (NX) {
+#pragma unroll
+        for (int u = 0; u < CU; ++u)
+#pragma unroll
+          for (int m = 0; m < MM; ++m) ssq[m] = dot8(x[m][u], x[m][u], ssq[m]);
+      }
     }
     for (; c < nch; ++c) {                        // tail chunks (K / 512 not a multiple of CU)
       u32x4 w[RW], x[MM];
@@ -153,12 +176,24 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
       for (int r = 0; r < RW; ++r)
 #pragma unroll
         for (int m = 0; m < MM; ++m) acc[r][m] = dot8(w[r], x[m], acc[r][m]);
+      if constexpr (NX) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) ssq[m] = dot8(x[m], x[m], ssq[m]);
+      }
     }
   }
 #pragma unroll
   for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int m = 0; m < MM; ++m) acc[r][m] = wave_sum_dpp(acc[r][m]);
+  if constexpr (NX) {
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      const float rs = rsqrtf(wave_sum_dpp(ssq[m]) / (float)K + eps);
+#pragma unroll
+      for (int r = 0; r < RW; ++r) acc[r][m] *= rs;
+    }
+  }
 
   if constexpr (EPI == kRwPlain) {
     if (!valid) return;
@@ -167,7 +202,13 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int m = 0; m < MM; ++m)
-        if (lane == r * MM + m && m < M && row0 + r < N) Y[(int64_t)m * ldy + row0 + r] = f2bf(acc[r][m]);
+        if (lane == r * MM + m && m < M && row0 + r < N) {
+          bf16_t* yp = Y + (int64_t)m * ldy + row0 + r;
+          if constexpr (FL & kRwResAdd)
+            *yp = f2bf(bf2f(f2bf(acc[r][m])) + bf2f(*yp));   // residual <- bf16(y + residual)
+          else
+            *yp = f2bf(acc[r][m]);
+        }
   } else {
     __shared__ float pair_s[kRwWaves / 2][MM];
     if ((wave & 1) && lane == 0) {
@@ -221,14 +262,14 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
 
 // cfg bits: [1:0] RW = 1 << b (plain only), [3:2] CU = 2 << b (2, 4, 8, 16).
 // Host-checked: K % 512 == 0, 1 <= M <= 4, (RW + MM) * CU <= 40 loads in flight per lane.
-template <int EPI, int MM>
-static void launch_rows_mm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+template <int EPI, int MM, int FL>
+static void launch_rows_fl(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
                            bf16_t* Y, int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re,
-                           int waves, hipStream_t s) {
+                           int waves, float eps, hipStream_t s) {
   const dim3 grid((waves + kRwWaves - 1) / kRwWaves), block(kRwWaves * 64);
 #define RW_L(rw, cu) \
-  hipLaunchKernelGGL((gemv_rows_kernel<MM, rw, cu, EPI, true>), grid, block, 0, s, X, ldx, W, N, \
-                     K, Y, ldy, M, up_off, re)
+  hipLaunchKernelGGL((gemv_rows_kernel<MM, rw, cu, EPI, true, FL>), grid, block, 0, s, X, ldx, W, \
+                     N, K, Y, ldy, M, up_off, re, eps)
   const int rw = 1 << (cfg & 3), cu = 2 << ((cfg >> 2) & 3);
   if constexpr (EPI == kRwPlain) {
     switch (rw * 100 + cu) {
@@ -251,37 +292,55 @@ static void launch_rows_mm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N,
 #undef RW_L
 }
 
+// cfg bit 4: kRwNormX (SwiGLU / RoPE), bit 5: kRwResAdd (plain)
+template <int EPI, int MM>
+static void launch_rows_mm(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
+                           bf16_t* Y, int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re,
+                           int waves, float eps, hipStream_t s) {
+  if constexpr (EPI == kRwPlain) {
+    if (cfg & 32)
+      launch_rows_fl<EPI, MM, kRwResAdd>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
+    else
+      launch_rows_fl<EPI, MM, 0>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
+  } else {
+    if (cfg & 16)
+      launch_rows_fl<EPI, MM, kRwNormX>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
+    else
+      launch_rows_fl<EPI, MM, 0>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
+  }
+}
+
 template <int EPI>
 static void launch_rows(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
                         int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re, int waves,
-                        hipStream_t s) {
+                        float eps, hipStream_t s) {
   if (M <= 1)
-    launch_rows_mm<EPI, 1>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+    launch_rows_mm<EPI, 1>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
   else if (M <= 2)
-    launch_rows_mm<EPI, 2>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+    launch_rows_mm<EPI, 2>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
   else
-    launch_rows_mm<EPI, 4>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, s);
+    launch_rows_mm<EPI, 4>(X, ldx, W, N, K, Y, ldy, M, cfg, up_off, re, waves, eps, s);
 }
 
 void launch_gemv_rows(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K, bf16_t* Y,
                       int64_t ldy, int M, int cfg, hipStream_t s) {
   const int rw = 1 << (cfg & 3);
-  launch_rows<kRwPlain>(X, ldx, W, N, K, Y, ldy, M, cfg, 0, RopeEpi{}, (N + rw - 1) / rw, s);
+  launch_rows<kRwPlain>(X, ldx, W, N, K, Y, ldy, M, cfg, 0, RopeEpi{}, (N + rw - 1) / rw, 0.f, s);
 }
 
 // Y[M, F] = silu(x Wg^T) * (x Wu^T), w = [Wg; Wu] [2F, K]
 void launch_gemv_rows_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W, int F, int K,
-                             bf16_t* Y, int64_t ldy, int M, int cfg, hipStream_t s) {
-  launch_rows<kRwSwi>(X, ldx, W, F, K, Y, ldy, M, cfg, F, RopeEpi{}, 2 * F, s);
+                             bf16_t* Y, int64_t ldy, int M, int cfg, float eps, hipStream_t s) {
+  launch_rows<kRwSwi>(X, ldx, W, F, K, Y, ldy, M, cfg, F, RopeEpi{}, 2 * F, eps, s);
 }
 
 // qkv = x w^T with RoPE + KV append (N = (Hq + 2 Hkv) * 128); only q columns of Y written
 void launch_gemv_rows_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
                            bf16_t* Y, int64_t ldy, int M, int cfg, const int32_t* positions,
                            const float* cos_sin, const int32_t* slots, bf16_t* k_cache,
-                           bf16_t* v_cache, int Hq, int Hkv, int BS, hipStream_t s) {
+                           bf16_t* v_cache, int Hq, int Hkv, int BS, float eps, hipStream_t s) {
   const RopeEpi re{positions, cos_sin, slots, k_cache, v_cache, Hq, Hkv, BS};
-  launch_rows<kRwRope>(X, ldx, W, N / 2, K, Y, ldy, M, cfg, 0, re, N, s);
+  launch_rows<kRwRope>(X, ldx, W, N / 2, K, Y, ldy, M, cfg, 0, re, N, eps, s);
 }
 
 }  // namespace rfq

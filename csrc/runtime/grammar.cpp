@@ -20,7 +20,10 @@ State Grammar::enter_cnt(int32_t pc, const State& from, int32_t cnt) const {
 int Grammar::combo(int32_t ci, const State& st) const {
   const bool synth = st.prof == PROFILE_SYNTHETIC;
   int c = synth ? 1 : 0;
-  const int32_t lim = synth ? max_items[ci] : 0;
+  int32_t lim = synth ? max_items[ci] : 0;
+  // SYNTHETIC + item hint: exactly the document's item count (a trained extractor emits
+  // one object per part; a random-init model would otherwise flip a coin at every ',')
+  if (lim > 0 && honors_min[ci] && st.minv > 0 && st.minv < lim) lim = st.minv;
   if (lim > 0 && st.cnt >= lim) c |= 2;
   else if (honors_min[ci] && st.cnt < st.minv) c |= 4;
   return c;

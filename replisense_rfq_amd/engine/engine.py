@@ -92,6 +92,10 @@ class LLMEngine:
                                        moe_ep=self.cfg.moe_parallel == "ep")
         self.model = model or DecoderLM(self.model_cfg, self.device, tp, seed=self.cfg.seed,
                                         weights=weights, moe_ep=self.cfg.moe_parallel == "ep")
+        # the norm weights go into qkv / gate|up before anything copies those weights
+        # (tiled copies below) or times them (start-up plans): models/llama.py fold_norms
+        if self.device.type == "cuda":
+            self.model.fold_norms()
         # before the KV pool is sized from the free memory: the tiled copies take theirs
         self.tiled_bytes = self.model.tile_decode_weights() if self.cfg.tune_gemm else 0
         self.init_weights_s = time.perf_counter() - t0

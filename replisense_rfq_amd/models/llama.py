@@ -36,12 +36,14 @@ from .config import ModelConfig
 from .moe import MoEBuffers, moe_mlp
 from .weights import init_weights
 
-# RFQ_SINGLE_PASS_DECODE=1: split-K decode attention merges its partials in-kernel (the
-# last split wave of each work item, Guideline-16 sc1 hand-off) instead of a second
-# reduce launch.  Off by default: measured 19.1 us per layer vs 8.5 + 4.8 us for the
-# two launches at batch 1 (profiles/r2_decode_attention_single_pass.md) -- one wave
-# merging 16 splits x 16 columns is slower than the 32-workgroup reduce kernel.
-SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "0") == "1"
+# RFQ_SINGLE_PASS_DECODE: split-K decode attention merges its partials in-kernel (the
+# last split wave of each work item, Guideline-16 sc1 hand-off; the whole wave merges
+# 4 columns at a time with every split's loads in flight) instead of a second reduce
+# launch.  "auto" (default): on where a kv head has at most 4 query columns (8B,
+# Mixtral: 8.3 / 9.2 / 11.0 µs vs 8.9 / 9.8 / 11.8 with the reduce launch at ctx
+# 512 / 1024 / 2048), off with 8 columns per kv head (70B at TP=8 and TP=1: two merge
+# rounds, the reduce launch is 0.6-0.9 µs faster) -- profiles/r5_tp8_rank_emulation.md.
+SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "auto").lower()
 # RFQ_DECODE_WG_MERGE=1: with >= 4 splits, four splits share a workgroup and merge
 # through LDS (attn_decode.hip NWV = 4) and the workgroups' partials merge in-kernel:
 # one launch per layer.  Off by default: measured 1-2 us per layer SLOWER than one wave
@@ -111,6 +113,50 @@ class DecoderLM:
         self.sp_min_tokens = int(os.environ.get("RFQ_SP_MIN_TOKENS", "0"))
         self.tiled_inplace = False      # some projection stored only in the decode-tiled layout
         self.tiled_plan: dict = {}      # projection -> copy | inplace | off
+        self.norms_folded = False       # fold_norms: attn / mlp RMSNorm weights in qkv / gate|up
+        self.single_pass = (SINGLE_PASS_DECODE in ("1", "on", "true")
+                            or (SINGLE_PASS_DECODE == "auto" and self.hq // self.hkv <= 4))
+
+    # ------------------------------------------------------------ folded norms
+    def fold_norms(self) -> bool:
+        """Fold each layer's attention / MLP RMSNorm weight into the columns of the
+        projection that consumes the normalised activations:
+
+            rmsnorm(x) diag(g) W^T = rsqrt(mean(x^2) + eps) * (x W'^T),   W' = W diag(g)
+
+        qkv <- qkv * attn_norm, gate|up <- gate|up * mlp_norm (in place, rounded to bf16
+        once), and both norm weights become ones, so every path of the forward stays exact
+        algebra.  What it buys is the TP = 1 small-step path (_forward_fold): the qkv and
+        gate|up row-streaming GEMVs read the UN-normalised residual and apply the norm's
+        scale themselves (each wave reads the whole row anyway), and the o / down GEMVs add
+        into the residual in their epilogue -- no norm launch and no cross-workgroup
+        reduction left in a decode layer (2 launches fewer per layer).  Dense models at
+        TP = 1 only (RFQ_NORM_FOLD=0 turns it off); the final norm before the LM head
+        stays.  Returns whether the weights were folded."""
+        if (self.norms_folded or self.cfg.is_moe or self.tp.enabled
+                or os.environ.get("RFQ_NORM_FOLD", "1") == "0"):
+            return self.norms_folded
+        with torch.no_grad():
+            for lw in self.w["layers"]:
+                lw["qkv"].mul_(lw["attn_norm"][None, :])
+                lw["gate_up"].mul_(lw["mlp_norm"][None, :])
+                lw["attn_norm_folded"], lw["mlp_norm_folded"] = lw["attn_norm"], lw["mlp_norm"]
+                lw["attn_norm"] = torch.ones_like(lw["attn_norm"])
+                lw["mlp_norm"] = torch.ones_like(lw["mlp_norm"])
+        self.norms_folded = True
+        return True
+
+    def _fold_step(self, m: "ForwardMeta", T: int) -> bool:
+        """Run this step through _forward_fold: folded weights, a small step whose
+        projections all fit the row-streaming GEMV, no cascade attention."""
+        if not self.norms_folded or T < 1:
+            return False
+        lw = self.w["layers"][0]
+        d = self.cfg.hidden
+        return (ops.fold_ok(T, d, lw["qkv"]) and ops.fold_ok(T, self.hq * self.cfg.head_dim, lw["o"])
+                and ops.fold_ok(T, self.ffn_local, lw["down"])
+                and not ops.tiled_only(lw["qkv"]) and not ops.tiled_only(lw["gate_up"])
+                and not ops.tiled_only(lw["o"]) and not ops.tiled_only(lw["down"]))
 
     # ------------------------------------------------------- decode weight layout
     TILED_PROJ = ("qkv", "o", "gate_up", "down")
@@ -199,6 +245,8 @@ class DecoderLM:
 
         if self.tp.enabled and 0 < self.sp_min_tokens <= T:
             return self._forward_sp(m)
+        if self._fold_step(m, T):
+            return self._forward_fold(m)
         h = ops.embed(m.input_ids[:T], w["embed"])
         residual = h
         x = ops.rms_norm(h, w["layers"][0]["attn_norm"], eps)
@@ -260,6 +308,35 @@ class DecoderLM:
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
 
+    def _forward_fold(self, m: ForwardMeta) -> torch.Tensor:
+        """Small-step forward over folded norm weights (fold_norms; TP = 1): the residual
+        stream itself is every layer's input, so a layer is
+
+            qkv + RoPE + KV append (norm scale in-kernel) -> attention -> o (+= residual)
+            -> gate|up + SwiGLU (norm scale in-kernel) -> down (+= residual)
+
+        four row-streaming GEMVs and the attention launches, with no RMSNorm launch and no
+        cross-workgroup reduction (csrc/kernels/gemv_rows.hip kRwNormX / kRwResAdd)."""
+        cfg, w = self.cfg, self.w
+        T = m.num_tokens
+        eps = cfg.rms_eps
+        qd = self.hq * cfg.head_dim
+        residual = ops.embed(m.input_ids[:T], w["embed"])
+        attn = torch.empty((T, qd), dtype=self.dtype, device=self.device)
+        dec_parts, shared = self._attn_scratch(m, residual)
+        for li in range(cfg.n_layers):
+            lw = w["layers"][li]
+            qkv = ops.rows_rope_normx(residual, lw["qkv"], m.positions, self.cos_sin,
+                                      m.slot_mapping, self.kv_k[li], self.kv_v[li], self.hq,
+                                      self.hkv, eps)
+            self._attend(li, residual, attn, m, dec_parts, shared, qkv=qkv)
+            ops.rows_residual_add(attn, lw["o"], residual)
+            act = ops.rows_swiglu_normx(residual, lw["gate_up"], eps)
+            ops.rows_residual_add(act, lw["down"], residual)
+        x = ops.rms_norm(residual, w["final_norm"], eps)
+        xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
+        return ops.linear(xs, w["lm_head"])
+
     def _forward_sp(self, m: ForwardMeta) -> torch.Tensor:
         """Sequence-parallel forward (TP group of W ranks, T tokens padded to Tp = W*n).
 
@@ -312,7 +389,7 @@ class DecoderLM:
         head) waves (engine/runner.py _decode_splits), extend rows at most 4x that.
         Used by the 4-wave workgroup form (its few partials merge in-kernel) and, with
         RFQ_SINGLE_PASS_DECODE, by the one-wave form."""
-        if self.device.type != "cuda" or not (SINGLE_PASS_DECODE or waves > 1):
+        if self.device.type != "cuda" or not (self.single_pass or waves > 1):
             return None
         if self._tickets is None:
             self._tickets = torch.zeros(4096 * self.hkv, dtype=torch.int32, device=self.device)
@@ -336,7 +413,7 @@ class DecoderLM:
         return dec_parts, shared
 
     def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared,
-                merge: bool = False) -> None:
+                merge: bool = False, qkv=None) -> None:
         """QKV GEMM + RoPE + paged-KV append, then decode / prefill attention into
         ``attn`` (rows [0, T) of x and attn; rows past T are SP padding).  ``merge``:
         the decode attention leaves its split partials in ``dec_parts`` for the o
@@ -345,7 +422,7 @@ class DecoderLM:
         hq, hkv = self.hq, self.hkv
         lw = self.w["layers"][li]
         kc, vc = self.kv_k[li], self.kv_v[li]
-        fcfg = self._fused_cfg(m, x, lw["qkv"], shared)
+        fcfg = self._fused_cfg(m, x, lw["qkv"], shared) if qkv is None else -1
         if fcfg >= 0:
             # one launch: QKV GEMV + RoPE + KV append + decode attention (decode_fused.hip)
             ns = m.decode_splits if dec_parts is not None else 1
@@ -358,8 +435,9 @@ class DecoderLM:
             if ns > 1:
                 ops.attn_decode_merge(po, pm, attn[:D], hq, ns)
             return
-        qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
-                           hq, hkv)
+        if qkv is None:
+            qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc,
+                               vc, hq, hkv)
         if shared is not None:
             ops.attn_decode_shared(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start,
                                    m.dec_q_len, m.dec_kv_len, m.dec_work_seq, m.dec_work_ct,
@@ -387,7 +465,7 @@ class DecoderLM:
         start-up plan entry that measured the fold faster."""
         T, D = m.num_tokens, m.num_decode
         if (not x.is_cuda or D == 0 or T != D or T > 16 or dec_parts is None
-                or shared is not None or SINGLE_PASS_DECODE):
+                or shared is not None or self.single_pass):
             return -1
         ns = m.decode_splits
         if DECODE_WG_MERGE and ns >= 4 and ns % 4 == 0:

@@ -24,6 +24,7 @@ __all__ = [
     "gemm_dense", "gemm_dense_ok", "swiglu_large", "tile_weight", "untile_weight",
     "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT", "SPLITK_PERSIST",
     "ROWS_BIT", "ROWS_MAX_M", "ROWS_CFGS", "ROWS_CFGS_PAIRED", "rows_ok",
+    "set_rows_best", "rows_rope_normx", "rows_swiglu_normx", "rows_residual_add", "fold_ok",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -403,6 +404,80 @@ def linear_swiglu(x, w):
                 _native.ops().skinny_gemm_swiglu(x, w, out, cfg)
             return out
     return None
+
+
+# ---------------------------------------------------------------- folded-norm latency path
+# Best row-streaming cfg per (kind, M, N, K) measured by the start-up plans, whether or
+# not it won its plan: the folded-norm path (models/llama.py _forward_fold) has no
+# other kernel for its epilogues.  kind: "plain" | "swiglu" | "rope".
+_ROWS_BEST: dict[tuple, int] = {}
+ROWS_DEFAULT = {"plain": 9, "swiglu": 8, "rope": 8}
+FOLD_MAX_M = int(os.environ.get("RFQ_FOLD_MAX_M", "4"))
+
+
+def set_rows_best(best: dict) -> None:
+    _ROWS_BEST.update(best)
+
+
+def _rows_cfg(kind: str, M: int, N: int, K: int) -> int:
+    for m in _TUNED_MS or [M]:
+        if m >= M:
+            c = _ROWS_BEST.get((kind, m, N, K))
+            if c is not None:
+                return c
+            break
+    return ROWS_DEFAULT[kind]
+
+
+def rows_rope_normx(res, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, eps):
+    """qkv = rmsnorm(res) @ w'^T with the norm weight folded into w' (DecoderLM.fold_norms),
+    RoPE on q / k, k / v appended to the paged cache; only q columns are written (GPU).
+    One row-streaming launch reading the UN-normalised residual (gemv_rows.hip kRwNormX)."""
+    M, K = res.shape
+    N = w.shape[0]
+    qkv = torch.empty((M, N), dtype=res.dtype, device=res.device)
+    if _gpu(res):
+        _native.ops().gemv_rows_rope(res, w, qkv, positions, cos_sin, slot_mapping, k_cache,
+                                     v_cache, Hq, Hkv, _rows_cfg("rope", M, N, K) | 16, eps)
+        return qkv
+    xn = torch.empty_like(res)
+    ref.rms_norm(res, torch.ones(K, dtype=res.dtype), eps, xn)
+    qkv.copy_(xn @ w.t())
+    ref.rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv)
+    return qkv
+
+
+def rows_swiglu_normx(res, w, eps):
+    """act = SwiGLU(rmsnorm(res) @ w'^T) with the norm weight folded into w' (gate|up)."""
+    M, K = res.shape
+    F = w.shape[0] // 2
+    out = torch.empty((M, F), dtype=res.dtype, device=res.device)
+    if _gpu(res):
+        _native.ops().gemv_rows_swiglu(res, w, out, _rows_cfg("swiglu", M, F, K) | 16, eps)
+        return out
+    xn = torch.empty_like(res)
+    ref.rms_norm(res, torch.ones(K, dtype=res.dtype), eps, xn)
+    ref.silu_mul(xn @ w.t(), out)
+    return out
+
+
+def rows_residual_add(x, w, residual):
+    """residual <- bf16(bf16(x @ w^T) + residual) (o / down + the residual add)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if _gpu(x):
+        _native.ops().gemv_rows(x, w, residual, _rows_cfg("plain", M, N, K) | 32)
+        return residual
+    residual.copy_(((x @ w.t()).float() + residual.float()).to(residual.dtype))
+    return residual
+
+
+def fold_ok(M: int, K: int, w: torch.Tensor) -> bool:
+    """The folded-norm path can run a projection of this step on the row-streaming
+    kernel (GPU: rows_ok; CPU: always, through the oracles)."""
+    if not w.is_cuda:
+        return 1 <= M <= FOLD_MAX_M
+    return 1 <= M <= min(FOLD_MAX_M, ROWS_MAX_M) and K % 512 == 0
 
 
 # (M, N, K) -> skinny cfg (NT = 2) whose epilogue applies RoPE to q/k and appends k/v
@@ -966,3 +1041,12 @@ def moe_combine_splitk(yf, splits, inv_pos, weights, topk, out):
 
 def moe_combine(y, inv_pos, weights, topk, out):
     _native.ops().moe_combine(y, inv_pos, weights, topk, out)
+
+
+def reset_plans() -> None:
+    """Forget every start-up plan (tests that build bare models after an engine: the
+    plans are keyed by shape and may name a decode-tiled copy the new weights lack)."""
+    for d in (_LINEAR_PLAN, _SILU_PLAN, _NORM_PLAN, _MERGE_PLAN, _SWI_PLAN, _ROWS_BEST,
+              _ROPE_PLAN, _SPLIT_PLAN):
+        d.clear()
+    _TUNED_MS.clear()

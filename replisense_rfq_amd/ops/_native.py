@@ -15,7 +15,8 @@ from pathlib import Path
 
 import torch
 
-_LIB = Path(__file__).resolve().parent.parent / "_C.so"
+# RFQ_C_SO: an alternative build of the same library (A/B tools only, never the default)
+_LIB = Path(os.environ.get("RFQ_C_SO") or Path(__file__).resolve().parent.parent / "_C.so")
 _lock = threading.Lock()
 _loaded = False
 _error: Exception | None = None

@@ -16,7 +16,7 @@ import time
 import torch
 
 from . import (ROWS_BIT, ROWS_CFGS, ROWS_CFGS_PAIRED, SPLITK_BIT, SPLITK_CFGS, SPLITK_NT,
-               SPLITK_TILED, _native, _wsel, gemm_dense_ok, gemm_w4_ok, rows_ok,
+               SPLITK_TILED, _native, _wsel, gemm_dense_ok, gemm_w4_ok, rows_ok, set_rows_best,
                set_linear_plan, set_merge_plan, set_norm_plan, set_rope_plan, set_silu_plan,
                set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
@@ -156,10 +156,14 @@ def tune_linear(groups: dict[str, list[torch.Tensor]], ms_by_group: dict[str, li
                         best, t_best = c | SPLITK_BIT, t
             if rows_ok(M, K, ws[0]):
                 # row-streaming GEMV (one wave per row, full K): M <= 4
+                rb, t_rb = -1, float("inf")
                 for c in ROWS_CFGS:
                     t = _time(lambda w, c=c: ops.gemv_rows(x, w, out, c), ws, reps)
+                    if t < t_rb:
+                        rb, t_rb = c, t
                     if t < t_best:
                         best, t_best = c | ROWS_BIT, t
+                set_rows_best({("plain", M, N, K): rb})
             plan[(M, N, K)] = best
             report.append((name, M, N, K, round(t_lib, 1), best, round(min(t_best, t_lib), 1)))
     return plan, report
@@ -351,10 +355,14 @@ def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: fl
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
         if rows_ok(M, K, ws[0]):
+            rb, t_rb = -1, float("inf")
             for c in ROWS_CFGS_PAIRED:
                 t = _time(lambda w, c=c: ops.gemv_rows_swiglu(x, w, act, c), ws, reps)
+                if t < t_rb:
+                    rb, t_rb = c, t
                 if t < t_best:
                     best, t_best = c | ROWS_BIT, t
+            set_rows_best({("swiglu", M, F, K): rb})
         if best >= 0:
             plan[(M, F, K)] = best
         report.append(("gate_up+swiglu", M, N2, K, round(t_ref, 1), best,
@@ -406,11 +414,15 @@ def tune_rope(ws: list[torch.Tensor], ms: list[int], cos_sin: torch.Tensor, hq: 
             if t < t_best:
                 best, t_best = c | SPLITK_BIT, t
         if rows_ok(M, K, ws[0]):
+            rb, t_rb = -1, float("inf")
             for c in ROWS_CFGS_PAIRED:
                 t = _time(lambda w, c=c: ops.gemv_rows_rope(x, w, qkv, pos, cos_sin, slots, kc, vc,
                                                             hq, hkv, c), ws, reps)
+                if t < t_rb:
+                    rb, t_rb = c, t
                 if t < t_best:
                     best, t_best = c | ROWS_BIT, t
+            set_rows_best({("rope", M, N, K): rb})
         if best >= 0:
             plan[(M, N, K)] = best
         report.append(("qkv+rope", M, N, K, round(t_ref, 1), best, round(min(t_best, t_ref), 1)))

@@ -35,6 +35,9 @@ def _meta(T, device, nblocks):
 
 @pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
 def test_model_forward_matches_cpu_oracle(gpu, name):
+    from replisense_rfq_amd import ops
+
+    ops.reset_plans()            # bare models: no plan of an earlier engine applies
     torch.manual_seed(0)
     cfg = get_config(name)
     m_gpu = DecoderLM(cfg, gpu, seed=3)

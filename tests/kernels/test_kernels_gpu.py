@@ -1187,3 +1187,54 @@ def test_gemv_rows_rope_kv(gpu, M, cfg, Hq, Hkv, K):
     _close(qkv[:, :q], exp[:, :q], 2e-2, 1e-2, f"rows rope q M={M} cfg={cfg}")
     _close(kc, kc_e, 2e-2, 1e-2, f"rows rope k cache M={M} cfg={cfg}")
     _close(vc, vc_e, 2e-2, 1e-2, f"rows rope v cache M={M} cfg={cfg}")
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("cfg", [4, 8])
+def test_gemv_rows_folded_norm(gpu, M, cfg):
+    """Folded-norm forms of the row-streaming GEMV (models/llama.py _forward_fold):
+    SwiGLU / RoPE over the UN-normalised residual x with the RMSNorm weight folded into
+    w's columns (cfg bit 4) == the fp32 oracle of rmsnorm(x) g . w^T; the plain form's
+    residual add (cfg bit 5) == bf16(bf16(x w^T) + residual)."""
+    torch.manual_seed(M * 3 + cfg)
+    K, F, eps = 4096, 1792, 1e-5
+    x = (3 * torch.randn(M, K, device=gpu)).to(BF)
+    g = (1 + 0.1 * torch.randn(K, device=gpu)).to(BF)
+    w = (torch.randn(2 * F, K, device=gpu) / math.sqrt(K)).to(BF)
+    wf = (w.float() * g.float()[None, :]).to(BF)                 # DecoderLM.fold_norms
+    xn = torch.empty_like(x)
+    ref.rms_norm(x, g, eps, xn)
+    # SwiGLU
+    act = torch.full((M, F), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows_swiglu(x, wf, act, cfg | 16, eps)
+    gu = (xn.float() @ w.float().t()).to(BF)
+    exp = torch.empty(M, F, dtype=BF, device=gpu)
+    ref.silu_mul(gu, exp)
+    _close(act, exp, 3e-2, 2e-2, f"folded swiglu M={M}")
+    # RoPE + KV append
+    Hq, Hkv = 8, 2
+    N = (Hq + 2 * Hkv) * 128
+    wq = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
+    wqf = (wq.float() * g.float()[None, :]).to(BF)
+    cos_sin = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(64, device=gpu)[:M].to(torch.int32)
+    kc = torch.zeros(2, Hkv, 32, 128, device=gpu, dtype=BF)
+    vc = torch.zeros_like(kc)
+    qkv = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+    torch.ops.rfq_amd.gemv_rows_rope(x, wqf, qkv, pos, cos_sin, slots, kc, vc, Hq, Hkv, cfg | 16,
+                                     eps)
+    e = (xn.float() @ wq.float().t()).cpu()
+    kc_e, vc_e = torch.zeros(kc.shape), torch.zeros(vc.shape)
+    ref.rope_kv(e, pos.cpu(), cos_sin.cpu(), slots.cpu(), kc_e, vc_e, Hq, Hkv)
+    _close(qkv[:, :Hq * 128], e[:, :Hq * 128], 3e-2, 2e-2, f"folded rope q M={M}")
+    _close(kc, kc_e, 3e-2, 2e-2, f"folded rope k M={M}")
+    _close(vc, vc_e, 3e-2, 2e-2, f"folded rope v M={M}")
+    # residual add
+    wo = (torch.randn(K, 1024, device=gpu) / math.sqrt(1024)).to(BF)
+    a = torch.randn(M, 1024, device=gpu, dtype=BF)
+    res = torch.randn(M, K, device=gpu, dtype=BF)
+    r2 = res.clone()
+    torch.ops.rfq_amd.gemv_rows(a, wo, r2, (cfg | 1) | 32)
+    y = (a.float() @ wo.float().t()).to(BF)
+    _close(r2, (y.float() + res.float()).to(BF), 2e-2, 1e-2, f"residual add M={M}")

@@ -118,7 +118,7 @@ def run_cascade(B, C, P, Hq=32, Hkv=8, q=1, tiles=2, iters=20):
     return min(res[0], res[2]), min(res[1], res[3]), diff
 
 
-def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1):
+def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1, single=False):
     """Batch-1 decode attention as the latency path runs it: L layers with their own
     KV caches, the L (split kernel [+ reduce]) launches captured in one hipGraph;
     returns µs per layer."""
@@ -138,7 +138,8 @@ def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1):
     out = torch.empty_like(qt)
     po = torch.empty(Hq * splits * 128, device=dev)
     pm = torch.empty(Hq * splits * 2, device=dev)
-    tickets = torch.zeros(items * Hkv, dtype=torch.int32, device=dev) if waves > 1 else None
+    tickets = (torch.zeros(items * Hkv, dtype=torch.int32, device=dev)
+               if (waves > 1 or single) else None)
 
     def body():
         for k, v in zip(ks, vs):
@@ -177,6 +178,19 @@ def main():
                     row[f"s{sp}_us"] = round(run_latency(C, Hq, 8, sp), 2)
                 for sp in (8, 16):                 # one column tile per work item
                     row[f"s{sp}_t1_us"] = round(run_latency(C, Hq, 8, sp, tiles=1), 2)
+                print(json.dumps(row), flush=True)
+        return
+    if os.environ.get("LAT_SP"):
+        # one wave per split: the reduce launch vs the in-kernel merge by the last split wave
+        # (tickets; whole-wave merge, every split's loads in flight at once)
+        for Hq, Hkv, L in ((8, 1, 80), (32, 8, 32)):
+            for C in (512, 1024, 2048):
+                row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
+                for sp in (8, 16):
+                    for t in (1, 2):
+                        row[f"s{sp}_t{t}_reduce_us"] = round(run_latency(C, Hq, Hkv, sp, t, L=L), 2)
+                        row[f"s{sp}_t{t}_single_us"] = round(
+                            run_latency(C, Hq, Hkv, sp, t, L=L, single=True), 2)
                 print(json.dumps(row), flush=True)
         return
     if os.environ.get("LAT_TP8"):

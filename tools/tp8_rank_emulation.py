@@ -41,6 +41,9 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import logging
+
+    logging.basicConfig(level=logging.INFO, stream=sys.stderr)   # start-up plan lines
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-70b")
     ap.add_argument("--world", type=int, default=8)
