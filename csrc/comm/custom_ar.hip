@@ -48,13 +48,13 @@ __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
   s16x8* own = reinterpret_cast<s16x8*>(peers.base[rank] + kCarDataOffset);
   const s16x8* src = reinterpret_cast<const s16x8*>(in);
   for (int64_t i = c0 + tid; i < c1; i += kCarThreads) own[i] = src[i];
-  car_drain_barrier();                               // every wave drained its stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: staged slice visible
+  __syncthreads();
   const uint32_t c = cnt_s;
   // 2-3. publish, then wait for every peer's slice b
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->start[b][rank], c);
+    car_store(&peer->start[b][rank], c);
     if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -72,8 +72,7 @@ __global__ __launch_bounds__(kCarThreads) void car_oneshot_kernel(
   // 5. everyone is done reading slice b before anyone reuses it
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->end[b][rank], c);
+    car_store(&peer->end[b][rank], c);
     if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -118,12 +117,12 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
     for (int64_t i = o0 + tid; i < o1; i += kCarThreads)
       if (base + i < n8) own[base + i] = src[base + i];
   }
-  car_drain_barrier();                               // every wave drained its stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
   const uint32_t c = cnt_s;
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->start[b][rank], c);
+    car_store(&peer->start[b][rank], c);
     if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -141,11 +140,11 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
       own[base + i] = pack8(acc);
     }
   }
-  car_drain_barrier();                               // every wave drained its stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->mid[b][rank], c);
+    car_store(&peer->mid[b][rank], c);
     if (!car_wait(self, &self->mid[b][tid], c, kCarMid, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -160,8 +159,7 @@ __global__ __launch_bounds__(kCarThreads) void car_twoshot_kernel(
   __syncthreads();
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->end[b][rank], c);
+    car_store(&peer->end[b][rank], c);
     if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -213,12 +211,12 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
       wv[k] = wr[c];
     }
   }
-  car_drain_barrier();                               // every wave drained its stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: staged row visible
+  __syncthreads();
   const uint32_t c = cnt_s;
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->start[b][rank], c);
+    car_store(&peer->start[b][rank], c);
     if (!car_wait(self, &self->start[b][tid], c, kCarStart, b, tid)) fail_s = 1;
   }
   __syncthreads();
@@ -253,8 +251,7 @@ __global__ __launch_bounds__(256) void car_oneshot_add_norm_kernel(
   // 3. every peer is done reading row b of this rank before anyone restages it
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->end[b][rank], c);
+    car_store(&peer->end[b][rank], c);
     if (!car_wait(self, &self->end[b][tid], c, kCarEnd, b, tid)) fail_s = 1;
   }
   ss = block_sum(ss, scratch);        // its barriers also order the end handshake
@@ -329,11 +326,12 @@ __global__ __launch_bounds__(256) void car_push_add_norm_kernel(
       if (ch < nchunk) dst[ch] = xv[k];
     }
   }
-  car_drain_barrier();                               // every wave drained its stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: pushed rows landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (tid < world) {
     CarSignal* peer = reinterpret_cast<CarSignal*>(peers.base[tid]);
-    car_release();
-    car_signal(&peer->push[par][b][rank], c);
+    car_store(&peer->push[par][b][rank], c);
     // 2. wait for row b of peer `tid` in the own staging
     if (!car_wait(self, &self->push[par][b][tid], c, kCarPush, b, tid)) fail_s = 1;
   }

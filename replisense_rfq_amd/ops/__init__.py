@@ -412,7 +412,10 @@ def linear_swiglu(x, w):
 # other kernel for its epilogues.  kind: "plain" | "swiglu" | "rope".
 _ROWS_BEST: dict[tuple, int] = {}
 ROWS_DEFAULT = {"plain": 9, "swiglu": 8, "rope": 8}
-FOLD_MAX_M = int(os.environ.get("RFQ_FOLD_MAX_M", "4"))
+# folded path up to 2 tokens: at M = 3-4 the dot2 GEMV re-reads X per token and the
+# gate|up + SwiGLU launch loses ~12 µs to the split-K MFMA GEMV (8B), more than the two
+# norm launches the fold saves (profiles/r5_gemv_rows.md)
+FOLD_MAX_M = int(os.environ.get("RFQ_FOLD_MAX_M", "2"))
 
 
 def set_rows_best(best: dict) -> None:

@@ -50,7 +50,7 @@ def _pair(device):
 def test_fold_norms_cpu_matches_plain_forward():
     torch.manual_seed(0)
     a, b = _pair("cpu")
-    for T in (1, 3):
+    for T in (1, 2):
         la = a.forward(_meta(T, "cpu")).float()
         assert b._fold_step(_meta(T, "cpu"), T)
         lb = b.forward(_meta(T, "cpu")).float()
@@ -83,7 +83,9 @@ def test_fold_norms_gpu_matches_plain_forward(gpu):
     a, b = _pair(gpu)
     for T in (1, 2, 3, 4):
         la = a.forward(_meta(T, gpu)).float()
-        assert b._fold_step(_meta(T, gpu), T)
+        # steps of up to FOLD_MAX_M tokens take the folded path, larger ones the plain
+        # forward on the folded weights (unit norm weights): the same logits either way
+        assert b._fold_step(_meta(T, gpu), T) == (T <= ops.FOLD_MAX_M)
         lb = b.forward(_meta(T, gpu)).float()
         rel = (la - lb).norm() / la.norm()
         assert rel < 3e-2, (T, rel)
