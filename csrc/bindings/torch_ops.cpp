@@ -302,13 +302,14 @@ static void check_rows(const char* what, const Tensor& x, const Tensor& w, const
   TORCH_CHECK(w.numel() < ((int64_t)1 << 40), what, ": weight too large");
   TORCH_CHECK(y.size(0) == M && y.size(1) == y_cols, what, ": y shape");
   TORCH_CHECK(x.stride(0) % 8 == 0, what, ": x rows must be 16-byte aligned");
-  TORCH_CHECK(cfg >= 0 && cfg < 64, what, ": cfg");
+  TORCH_CHECK(cfg >= 0 && cfg < 128, what, ": cfg");
 }
 
 // cfg bit 5: y is the residual stream, y <- bf16(x . w^T) + y (residual add)
 void gemv_rows(const Tensor& x, const Tensor& w, const Tensor& y, int64_t cfg) {
   check_rows("gemv_rows", x, w, y, cfg, w.size(0));
-  TORCH_CHECK(!(cfg & 16), "gemv_rows: cfg bit 4 (normalised x) is for the SwiGLU / RoPE forms");
+  TORCH_CHECK(!(cfg & 80), "gemv_rows: cfg bits 4 / 6 (normalised x, pair per wave) are for "
+              "the SwiGLU / RoPE forms");
   rfq::launch_gemv_rows(bp(x), x.stride(0), bp(w), w.size(0), x.size(1), bpm(y), y.stride(0),
                         x.size(0), (int)cfg, cur_stream());
 }

@@ -98,11 +98,17 @@ __device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, int voff, int s
 
 // MM: token capacity (runtime M <= MM); RW: rows per wave (plain only; paired epilogues
 // use one row per wave); CU: 1 KB chunks per row in flight per loop iteration.
-template <int MM, int RW, int CU, int EPI, bool NTL, int FL = 0>
+// PW (paired epilogues): ONE wave owns both rows of a pair (gate q and up q, or the two
+// rotate-half partners), RW = 2 with the second row rstride rows after the first: X is
+// loaded once for both rows (at M = 3-4 the X re-reads, not the weights, bound the
+// one-row-per-wave form) and the pair meets in registers, no LDS.
+template <int MM, int RW, int CU, int EPI, bool NTL, int FL = 0, bool PW = false>
 __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     const bf16_t* __restrict__ X, int64_t ldx, const bf16_t* __restrict__ W, int N, int K,
     bf16_t* __restrict__ Y, int64_t ldy, int M, int up_off, RopeEpi re, float eps) {
-  static_assert(EPI == kRwPlain || RW == 1, "paired epilogues: one row per wave");
+  static_assert(EPI == kRwPlain || RW == (PW ? 2 : 1), "paired epilogues: one row per wave, "
+                "or both rows of the pair (PW)");
+  static_assert(!PW || EPI != kRwPlain, "PW: paired epilogues only");
   static_assert(!(FL & kRwNormX) || EPI != kRwPlain, "normalised X: SwiGLU / RoPE forms");
   static_assert(!(FL & kRwResAdd) || EPI == kRwPlain, "residual add: plain form");
   constexpr bool NX = FL & kRwNormX;
@@ -110,11 +116,16 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
   const int wave = threadIdx.x >> 6;
   const int gw = blockIdx.x * kRwWaves + wave;
   // rows of this wave
-  int row0;
+  int row0, rstride = 1;
   bool valid;
   if constexpr (EPI == kRwPlain) {
     row0 = gw * RW;
     valid = row0 < N;
+  } else if constexpr (PW) {
+    const int q = gw;                              // one pair per wave
+    row0 = EPI == kRwSwi ? q : (q >> 6) * 128 + (q & 63);
+    rstride = EPI == kRwSwi ? up_off : 64;
+    valid = q < N;
   } else if constexpr (EPI == kRwSwi) {
     const int q = gw >> 1;                        // N = F here
     row0 = (wave & 1) ? up_off + q : q;
@@ -136,8 +147,8 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     // W: the wave's RW rows (wave-uniform base, RW * K * 2 bytes); X: the M token rows,
     // records end at row M so the loads of rows m >= M return zeros (no branch)
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(W + (int64_t)__builtin_amdgcn_readfirstlane(row0) * K), (short)0, RW * K * 2,
-        0x00020000);
+        (void*)(W + (int64_t)__builtin_amdgcn_readfirstlane(row0) * K), (short)0,
+        ((RW - 1) * rstride + 1) * K * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(M * ldx * 2), 0x00020000);
     const int voff = lane * 16;
@@ -148,7 +159,8 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
-        for (int u = 0; u < CU; ++u) w[r][u] = bload<WAUX>(wr, voff, (r * K + (c + u) * 512) * 2);
+        for (int u = 0; u < CU; ++u)
+          w[r][u] = bload<WAUX>(wr, voff, (r * rstride * K + (c + u) * 512) * 2);
 #pragma unroll
       for (int m = 0; m < MM; ++m)
 #pragma unroll
@@ -169,7 +181,7 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
     for (; c < nch; ++c) {                        // tail chunks (K / 512 not a multiple of CU)
       u32x4 w[RW], x[MM];
 #pragma unroll
-      for (int r = 0; r < RW; ++r) w[r] = bload<WAUX>(wr, voff, (r * K + c * 512) * 2);
+      for (int r = 0; r < RW; ++r) w[r] = bload<WAUX>(wr, voff, (r * rstride * K + c * 512) * 2);
 #pragma unroll
       for (int m = 0; m < MM; ++m) x[m] = bload<0>(xr, voff, (int)(m * ldx + c * 512) * 2);
 #pragma unroll
@@ -210,23 +222,35 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
             *yp = f2bf(acc[r][m]);
         }
   } else {
-    __shared__ float pair_s[kRwWaves / 2][MM];
-    if ((wave & 1) && lane == 0) {
-#pragma unroll
-      for (int m = 0; m < MM; ++m) pair_s[wave >> 1][m] = acc[0][m];
-    }
-    __syncthreads();
-    if ((wave & 1) || !valid || lane >= M) return;
-    // lane m < M of the even wave finishes token m
     float a = 0.f, b = 0.f;
+    int q;
+    if constexpr (PW) {
+      if (!valid || lane >= M) return;
 #pragma unroll
-    for (int m = 0; m < MM; ++m)
-      if (lane == m) {
-        a = acc[0][m];
-        b = pair_s[wave >> 1][m];
+      for (int m = 0; m < MM; ++m)
+        if (lane == m) {
+          a = acc[0][m];
+          b = acc[RW - 1][m];
+        }
+      q = gw;
+    } else {
+      __shared__ float pair_s[kRwWaves / 2][MM];
+      if ((wave & 1) && lane == 0) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) pair_s[wave >> 1][m] = acc[0][m];
       }
+      __syncthreads();
+      if ((wave & 1) || !valid || lane >= M) return;
+      // lane m < M of the even wave finishes token m
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+        if (lane == m) {
+          a = acc[0][m];
+          b = pair_s[wave >> 1][m];
+        }
+      q = gw >> 1;
+    }
     const int m = lane;
-    const int q = gw >> 1;
     if constexpr (EPI == kRwSwi) {
       const float gf = bf2f(f2bf(a));                 // = the gate_up GEMM's bf16 output
       const float sg = gf / (1.f + __expf(-gf));
@@ -260,12 +284,28 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
   }
 }
 
-// cfg bits: [1:0] RW = 1 << b (plain only), [3:2] CU = 2 << b (2, 4, 8, 16).
+// cfg bits: [1:0] RW = 1 << b (plain only), [3:2] CU = 2 << b (2, 4, 8, 16), bit 6: PW
+// (paired epilogues: both rows of a pair in one wave).
 // Host-checked: K % 512 == 0, 1 <= M <= 4, (RW + MM) * CU <= 40 loads in flight per lane.
 template <int EPI, int MM, int FL>
 static void launch_rows_fl(const bf16_t* X, int64_t ldx, const bf16_t* W, int N, int K,
                            bf16_t* Y, int64_t ldy, int M, int cfg, int up_off, const RopeEpi& re,
                            int waves, float eps, hipStream_t s) {
+  if constexpr (EPI != kRwPlain) {
+    if (cfg & 64) {                       // PW: one wave per pair -> half the waves
+      const dim3 grid((waves / 2 + kRwWaves - 1) / kRwWaves), block(kRwWaves * 64);
+      switch (2 << ((cfg >> 2) & 3)) {
+#define RW_PW(cu)                                                                              \
+  hipLaunchKernelGGL((gemv_rows_kernel<MM, 2, cu, EPI, true, FL, true>), grid, block, 0, s, X, \
+                     ldx, W, N, K, Y, ldy, M, up_off, re, eps)
+        case 4: RW_PW(4); break;
+        case 16: RW_PW(16); break;
+        default: RW_PW(8); break;
+#undef RW_PW
+      }
+      return;
+    }
+  }
   const dim3 grid((waves + kRwWaves - 1) / kRwWaves), block(kRwWaves * 64);
 #define RW_L(rw, cu) \
   hipLaunchKernelGGL((gemv_rows_kernel<MM, rw, cu, EPI, true, FL>), grid, block, 0, s, X, ldx, W, \

@@ -175,7 +175,9 @@ SPLITK_PERSIST = 64      # split-K GEMV cfg bit: persistent grid (tiled layout o
 ROWS_BIT = 256
 ROWS_MAX_M = 4
 ROWS_CFGS = (4, 8, 12, 5, 9, 2, 6, 3)      # (RW, CU) = (1,4) (1,8) (1,16) (2,4) (2,8) (4,2) (4,4) (8,2)
-ROWS_CFGS_PAIRED = (4, 8, 12)             # SwiGLU / RoPE epilogues: one row per wave
+# SwiGLU / RoPE epilogues: one row per wave (4, 8, 12), or both rows of the pair in one
+# wave (| 64: X read once per pair, the better form at M = 3-4)
+ROWS_CFGS_PAIRED = (4, 8, 12, 68, 72, 76)
 
 
 def rows_ok(M: int, K: int, w: torch.Tensor) -> bool:

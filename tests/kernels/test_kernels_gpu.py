@@ -1145,7 +1145,7 @@ def test_gemv_rows_strided_x(gpu, M, cfg):
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
-@pytest.mark.parametrize("cfg", [4, 8, 12])
+@pytest.mark.parametrize("cfg", [4, 8, 12, 68, 72, 76])
 @pytest.mark.parametrize("F,K", [(3584, 8192), (1792, 4096)])
 def test_gemv_rows_swiglu(gpu, M, cfg, F, K):
     """gate|up GEMV with the SwiGLU epilogue (waves 2j / 2j+1 pair through LDS) ==
@@ -1162,7 +1162,7 @@ def test_gemv_rows_swiglu(gpu, M, cfg, F, K):
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
-@pytest.mark.parametrize("cfg", [4, 8, 12])
+@pytest.mark.parametrize("cfg", [4, 8, 12, 68, 72, 76])
 @pytest.mark.parametrize("Hq,Hkv,K", [(8, 1, 8192), (32, 8, 4096)])
 def test_gemv_rows_rope_kv(gpu, M, cfg, Hq, Hkv, K):
     """QKV GEMV with the RoPE + paged-KV-append epilogue (waves 2j / 2j+1 = rotate-half
@@ -1190,7 +1190,7 @@ def test_gemv_rows_rope_kv(gpu, M, cfg, Hq, Hkv, K):
 
 
 @pytest.mark.parametrize("M", [1, 2, 4])
-@pytest.mark.parametrize("cfg", [4, 8])
+@pytest.mark.parametrize("cfg", [4, 8, 72])
 def test_gemv_rows_folded_norm(gpu, M, cfg):
     """Folded-norm forms of the row-streaming GEMV (models/llama.py _forward_fold):
     SwiGLU / RoPE over the UN-normalised residual x with the RMSNorm weight folded into
@@ -1235,6 +1235,6 @@ def test_gemv_rows_folded_norm(gpu, M, cfg):
     a = torch.randn(M, 1024, device=gpu, dtype=BF)
     res = torch.randn(M, K, device=gpu, dtype=BF)
     r2 = res.clone()
-    torch.ops.rfq_amd.gemv_rows(a, wo, r2, (cfg | 1) | 32)
+    torch.ops.rfq_amd.gemv_rows(a, wo, r2, ((cfg & 15) | 1) | 32)
     y = (a.float() @ wo.float().t()).to(BF)
     _close(r2, (y.float() + res.float()).to(BF), 2e-2, 1e-2, f"residual add M={M}")

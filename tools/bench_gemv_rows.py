@@ -24,7 +24,7 @@ SHAPES = {
     "8b": {"hidden": 4096, "hq": 32, "hkv": 8, "ffn": 14336},
 }
 ROWS_PLAIN = (4, 8, 12, 5, 9, 2, 6, 3)
-ROWS_PAIRED = (4, 8, 12)
+ROWS_PAIRED = (4, 8, 12, 68, 72, 76)
 SPLIT_TN = ops.SPLITK_TILED | ops.SPLITK_NT
 
 
