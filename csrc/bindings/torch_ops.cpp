@@ -44,29 +44,15 @@ void launch_gemv_rows_swiglu(const bf16_t*, int64_t, const bf16_t*, int, int, bf
 void launch_gemv_rows_rope(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int,
                            int, const int32_t*, const float*, const int32_t*, bf16_t*, bf16_t*, int,
                            int, int, float, hipStream_t);
-void launch_qkv_attn(const bf16_t*, int64_t, const bf16_t*, int, int, bf16_t*, int64_t, int, int,
-                     float*, unsigned*, const int32_t*, const float*, const int32_t*, bf16_t*,
-                     bf16_t*, int, int, int, const int32_t*, int, const int32_t*,
-                     const int32_t*, const int32_t*, const int32_t*, const int32_t*, int, int,
-                     int, bf16_t*, int64_t, float*, float*, float, int, unsigned*, unsigned*,
-                     unsigned*, hipStream_t);
 void launch_attn_decode_reduce(const float*, const float*, bf16_t*, int64_t, int, int, int,
                                hipStream_t);
-bool gemv_merge_fits(int, int, int, int);
-bool gemv_push_fits(int, int, int, int, int);
-void launch_gemv_push_norm(const bf16_t*, int64_t, const bf16_t*, int, int, int, int, float*,
-                           unsigned*, bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, float,
-                           unsigned*, char* const*, int, int, hipStream_t);
-void launch_gemv_splitk_merge(const float*, const float*, int, const bf16_t*, int, int, bf16_t*,
-                              int64_t, int, int, float*, unsigned*, bf16_t*, int64_t,
-                              const bf16_t*, bf16_t*, int64_t, float, unsigned*, hipStream_t);
 void launch_embed(const int32_t*, const bf16_t*, bf16_t*, int, int, int, int, hipStream_t);
 void launch_rope_kv(bf16_t*, int64_t, const int32_t*, const float*, const int32_t*, bf16_t*,
                     bf16_t*, int, int, int, int, hipStream_t);
 void launch_attn_decode(const bf16_t*, int64_t, const bf16_t*, const bf16_t*, const int32_t*, int,
                         const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                         const int32_t*, int, int, bf16_t*, int64_t, float*, float*, int, int,
-                        float, int, int, int32_t*, int, hipStream_t, bool);
+                        float, int, int, int32_t*, hipStream_t, bool);
 void launch_attn_decode_shared(const bf16_t*, int64_t, const bf16_t*, const bf16_t*,
                                const int32_t*, int, const int32_t*, const int32_t*,
                                const int32_t*, int, const int32_t*, const int32_t*, int, int,
@@ -350,77 +336,6 @@ void gemv_rows_rope(const Tensor& x, const Tensor& w, const Tensor& qkv, const T
                              (float)eps, cur_stream());
 }
 
-// Fused QKV projection + RoPE + KV append + split-K decode attention in ONE launch
-// (decode_fused.hip): qkv = x . w^T (q columns written), this step's K / V appended to
-// the paged cache, and the decode attention over [work_seq, work_ct] rows leaves its
-// split partials in part_o / part_ml (num_splits > 1; merge with attn_decode_merge) or
-// writes `out` directly (num_splits == 1).  done: this layer's zeroed counter slot
-// (Hkv uint32); zero_slot: the previous layer's slot (zeroed by the launch); err: a
-// uint32 the kernel increments on a wait timeout.  cfg: split-K GEMV cfg (8 waves).
-void qkv_attn(const Tensor& x, const Tensor& w, const Tensor& qkv, const Tensor& positions,
-              const Tensor& cos_sin, const Tensor& slot_mapping, const Tensor& k_cache,
-              const Tensor& v_cache, int64_t Hq, int64_t Hkv, const Tensor& part,
-              const Tensor& tile_cnt, int64_t cfg, const Tensor& block_tables,
-              const Tensor& seq_q_start, const Tensor& seq_q_len, const Tensor& seq_kv_len,
-              const Tensor& work_seq, const Tensor& work_ct, int64_t list_tpi, int64_t run_tiles,
-              const Tensor& out, const Tensor& part_o, const Tensor& part_ml, double scale,
-              int64_t num_splits, const Tensor& done, const std::optional<Tensor>& zero_slot,
-              const Tensor& err) {
-  const int64_t N = w.size(0);
-  check_splitk("qkv_attn", x, w, qkv, part, tile_cnt, cfg, N, N / 32);
-  CHECK_BF16(k_cache); CHECK_BF16(v_cache); CHECK_I32(positions); CHECK_I32(slot_mapping);
-  TORCH_CHECK(N == (Hq + 2 * Hkv) * 128, "qkv_attn: w must be [(Hq + 2 Hkv) * 128, K]");
-  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
-                  cos_sin.size(1) == 128, "qkv_attn: cos_sin must be fp32 [max_pos, 128]");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(2) == 32 &&
-                  k_cache.size(3) == 128 && k_cache.is_contiguous() && v_cache.is_contiguous() &&
-                  v_cache.sizes() == k_cache.sizes(),
-              "qkv_attn: cache must be [blocks, Hkv, 32, 128]");
-  TORCH_CHECK(positions.numel() >= x.size(0) && slot_mapping.numel() >= x.size(0),
-              "qkv_attn: metadata");
-  TORCH_CHECK(Hq % Hkv == 0 && Hq / Hkv <= 16, "qkv_attn: GQA group must be <= 16");
-  CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
-  CHECK_I32(seq_q_start); CHECK_I32(seq_q_len); CHECK_I32(seq_kv_len);
-  CHECK_I32(work_seq); CHECK_I32(work_ct);
-  CHECK_BF16(out); CHECK_ROWMAJOR(out);
-  const int rows = out.size(0);
-  TORCH_CHECK(rows <= x.size(0), "qkv_attn: attention rows must be rows of x");
-  TORCH_CHECK(work_seq.numel() == work_ct.numel(), "qkv_attn: work list mismatch");
-  TORCH_CHECK(block_tables.size(0) >= seq_q_len.numel() && seq_kv_len.numel() >= seq_q_len.numel()
-                  && seq_q_start.numel() >= seq_q_len.numel(),
-              "qkv_attn: per-sequence arrays mismatch");
-  TORCH_CHECK(list_tpi == 1 || list_tpi == 2, "qkv_attn: list_tpi in {1, 2}");
-  TORCH_CHECK(run_tiles >= 1 && run_tiles <= list_tpi, "qkv_attn: run_tiles in [1, list_tpi]");
-  TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "qkv_attn: num_splits in [1, 32]");
-  if (num_splits > 1) {
-    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat &&
-                    part_o.numel() >= (int64_t)rows * Hq * num_splits * 128 &&
-                    part_ml.numel() >= (int64_t)rows * Hq * num_splits * 2,
-                "qkv_attn: fp32 partial buffers too small");
-  }
-  CHECK_DEV(done); CHECK_I32(done); CHECK_DEV(err); CHECK_I32(err);
-  TORCH_CHECK(done.numel() >= 32 * Hkv, "qkv_attn: done slot holds Hkv counters, 32 words apart");
-  unsigned* zs = nullptr;
-  if (zero_slot.has_value()) {
-    CHECK_DEV(*zero_slot); CHECK_I32(*zero_slot);
-    TORCH_CHECK(zero_slot->numel() >= 32 * Hkv, "qkv_attn: zero_slot holds Hkv counters");
-    TORCH_CHECK(zero_slot->data_ptr() != done.data_ptr(), "qkv_attn: zero_slot is the done slot");
-    zs = reinterpret_cast<unsigned*>(zero_slot->data_ptr());
-  }
-  rfq::launch_qkv_attn(
-      bp(x), x.stride(0), bp(w), (int)N, x.size(1), bpm(qkv), qkv.stride(0), x.size(0), (int)cfg,
-      part.data_ptr<float>(), reinterpret_cast<unsigned*>(tile_cnt.data_ptr()),
-      positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int32_t>(),
-      bpm(k_cache), bpm(v_cache), (int)Hq, (int)Hkv, 32, block_tables.data_ptr<int32_t>(),
-      block_tables.stride(0), seq_q_start.data_ptr<int32_t>(), seq_q_len.data_ptr<int32_t>(),
-      seq_kv_len.data_ptr<int32_t>(), work_seq.data_ptr<int32_t>(), work_ct.data_ptr<int32_t>(),
-      work_seq.numel(), (int)list_tpi, (int)run_tiles, bpm(out), out.stride(0),
-      num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
-      num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, (float)scale, (int)num_splits,
-      reinterpret_cast<unsigned*>(done.data_ptr()), zs,
-      reinterpret_cast<unsigned*>(err.data_ptr()), cur_stream());
-}
-
 // Merge split-K decode-attention partials into bf16 rows (attn_decode_reduce).
 void attn_decode_merge(const Tensor& part_o, const Tensor& part_ml, const Tensor& out, int64_t Hq,
                        int64_t num_splits) {
@@ -434,63 +349,6 @@ void attn_decode_merge(const Tensor& part_o, const Tensor& part_ml, const Tensor
   TORCH_CHECK(out.size(1) >= Hq * 128, "attn_decode_merge: out [rows, >= Hq * 128]");
   rfq::launch_attn_decode_reduce(part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bpm(out),
                                  out.stride(0), rows, (int)Hq, (int)num_splits, cur_stream());
-}
-
-// y = attn . w^T where attn [M, Hq * 128] is the decode attention still in its split
-// partials (part_o [M][Hq][S][128], part_ml [M][Hq][S][2] fp32): the split merge runs as
-// the split-K GEMV's prologue (gemv_core.h AM).  With residual / norm_w / out / counter
-// given, the residual-add RMSNorm epilogue of gemv_splitk_norm follows.
-void gemv_splitk_merge(const Tensor& part_o, const Tensor& part_ml, int64_t S, const Tensor& w,
-                       const Tensor& y, const Tensor& part, const Tensor& tile_cnt, int64_t cfg,
-                       const std::optional<Tensor>& residual, const std::optional<Tensor>& norm_w,
-                       double eps, const std::optional<Tensor>& out,
-                       const std::optional<Tensor>& counter) {
-  CHECK_DEV(y); CHECK_BF16(w); CHECK_BF16(y); CHECK_ROWMAJOR(y); CHECK_I32(tile_cnt);
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemv_splitk_merge: w must be contiguous [N, K]");
-  const int64_t M = y.size(0), N = w.size(0), K = w.size(1), KS = 2 << (cfg & 3);
-  TORCH_CHECK(rfq::gemv_merge_fits((int)M, (int)K, (int)cfg, (int)S),
-              "gemv_splitk_merge: M <= 16, 2 <= S <= 16, K % 128 == 0, K / 128 >= KS, "
-              "M * slice heads * 128 <= 16384, no persistent cfg");
-  TORCH_CHECK(N % 16 == 0 && y.size(1) == N && y.stride(0) % 8 == 0, "gemv_splitk_merge: y [M, N]");
-  TORCH_CHECK(part_o.is_cuda() && part_ml.is_cuda() && part_o.scalar_type() == at::kFloat &&
-                  part_ml.scalar_type() == at::kFloat && part_o.is_contiguous() &&
-                  part_ml.is_contiguous() && part_o.numel() >= M * (K / 128) * S * 128 &&
-                  part_ml.numel() >= M * (K / 128) * S * 2,
-              "gemv_splitk_merge: fp32 partials [M][Hq][S][128] / [M][Hq][S][2]");
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
-              "gemv_splitk_merge: fp32 partials workspace of KS*M*N floats");
-  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, "gemv_splitk_merge: tile counters");
-  const bool norm = residual.has_value();
-  TORCH_CHECK(norm == norm_w.has_value() && norm == out.has_value() && norm == counter.has_value(),
-              "gemv_splitk_merge: residual, norm_w, out and counter go together");
-  rfq::bf16_t* res = nullptr;
-  rfq::bf16_t* o = nullptr;
-  const rfq::bf16_t* nw = nullptr;
-  unsigned* cnt = nullptr;
-  int64_t rs = 0, os = 0;
-  if (norm) {
-    CHECK_BF16(*residual); CHECK_BF16(*norm_w); CHECK_BF16(*out); CHECK_I32(*counter);
-    CHECK_ROWMAJOR(*residual); CHECK_ROWMAJOR(*out);
-    const int threads = (cfg & 4) ? 512 : 256;
-    TORCH_CHECK(N % 8 == 0 && N / 8 <= 4 * threads, "gemv_splitk_merge: N <= 32 * threads");
-    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N && out->size(0) == M &&
-                    out->size(1) == N && norm_w->numel() == N,
-                "gemv_splitk_merge: norm shapes");
-    TORCH_CHECK(residual->stride(0) % 8 == 0 && out->stride(0) % 8 == 0,
-                "gemv_splitk_merge: alignment");
-    TORCH_CHECK(counter->is_cuda() && counter->numel() >= 1, "gemv_splitk_merge: counter");
-    res = bpm(*residual);
-    o = bpm(*out);
-    nw = bp(*norm_w);
-    cnt = reinterpret_cast<unsigned*>(counter->data_ptr());
-    rs = residual->stride(0);
-    os = out->stride(0);
-  }
-  rfq::launch_gemv_splitk_merge(part_o.data_ptr<float>(), part_ml.data_ptr<float>(), (int)S, bp(w),
-                                (int)N, (int)K, bpm(y), y.stride(0), (int)M, (int)cfg,
-                                part.data_ptr<float>(),
-                                reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), res, rs, nw, o,
-                                os, (float)eps, cnt, cur_stream());
 }
 
 // Diagnostics: while `buf` is set (int64, >= 8 words per workgroup), every attn_prefill
@@ -625,7 +483,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                  const Tensor& seq_kv_len, const Tensor& work_seq, const Tensor& work_ct,
                  const Tensor& out, const Tensor& part_o, const Tensor& part_ml, int64_t Hq,
                  int64_t Hkv, double scale, int64_t num_splits, int64_t tiles_per_item,
-                 const std::optional<Tensor>& tickets, int64_t waves, bool reduce) {
+                 const std::optional<Tensor>& tickets, bool reduce) {
   CHECK_DEV(q); CHECK_BF16(q); CHECK_ROWMAJOR(q); CHECK_BF16(out); CHECK_ROWMAJOR(out);
   TORCH_CHECK(tiles_per_item == 1 || tiles_per_item == 2, "attn_decode: tiles_per_item in {1, 2}");
   CHECK_I32(block_tables); CHECK_ROWMAJOR(block_tables);
@@ -642,8 +500,6 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                   && seq_q_start.numel() >= seq_q_len.numel(),
               "attn_decode: per-sequence arrays mismatch");
   TORCH_CHECK(num_splits >= 1 && num_splits <= 32, "attn_decode: num_splits in [1, 32]");
-  TORCH_CHECK(waves == 1 || ((waves == 4 || waves == 8) && num_splits % waves == 0),
-              "attn_decode: waves 1, or 4 / 8 with num_splits % waves == 0");
   if (num_splits > 1) {
     TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_ml.scalar_type() == at::kFloat,
                 "partials must be fp32");
@@ -658,7 +514,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
     // zero-initialised once by the caller; the merging wave resets its entry
     CHECK_DEV(*tickets); CHECK_I32(*tickets);
     TORCH_CHECK(tickets->numel() >= work_seq.numel() * Hkv, "attn_decode: ticket buffer too small");
-    TORCH_CHECK(num_splits / waves <= 16, "attn_decode: the in-kernel merge takes at most 16 splits");
+    TORCH_CHECK(num_splits <= 16, "attn_decode: the in-kernel merge takes at most 16 splits");
     tk = tickets->data_ptr<int32_t>();
   }
   rfq::launch_attn_decode(bp(q), q.stride(0), bp(k_cache), bp(v_cache),
@@ -668,7 +524,7 @@ void attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
                           work_ct.data_ptr<int32_t>(), work_seq.numel(), rows, bpm(out),
                           out.stride(0), num_splits > 1 ? part_o.data_ptr<float>() : nullptr,
                           num_splits > 1 ? part_ml.data_ptr<float>() : nullptr, Hq, Hkv,
-                          (float)scale, num_splits, tiles_per_item, tk, (int)waves, cur_stream(), reduce);
+                          (float)scale, num_splits, tiles_per_item, tk, cur_stream(), reduce);
 }
 
 // Shared-prefix (cascade) decode attention, num_splits == 1; see attn_decode.hip.
@@ -972,45 +828,6 @@ void car_allreduce_add_norm(const Tensor& inp, const Tensor& residual, const Ten
                                      (int)d, (float)eps, cur_stream());
 }
 
-// TP row-parallel GEMV + custom all-reduce (push form) + residual-add RMSNorm in one
-// launch (csrc/comm/gemv_push.hip): residual <- bf16(allreduce(x . w^T) + residual),
-// out <- rmsnorm(residual) * norm_w, bit-identical to gemv_splitk + car_allreduce_add_norm
-// (algo 2).  counter: the norm ticket (ops.norm_counter), left at zero.
-void gemv_push_norm(const Tensor& x, const Tensor& w, const Tensor& part, const Tensor& tile_cnt,
-                    int64_t cfg, const Tensor& residual, const Tensor& norm_w, double eps,
-                    const Tensor& out, const Tensor& counter, c10::IntArrayRef bases,
-                    int64_t rank, int64_t capacity_bytes) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_ROWMAJOR(x); CHECK_I32(tile_cnt);
-  CHECK_BF16(residual); CHECK_BF16(norm_w); CHECK_BF16(out); CHECK_I32(counter);
-  CHECK_ROWMAJOR(residual); CHECK_ROWMAJOR(out);
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "gemv_push_norm: w must be contiguous [N, K]");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), KS = 2 << (cfg & 3);
-  const int world = (int)bases.size();
-  TORCH_CHECK(rfq::gemv_push_fits(world, (int)M, (int)N, (int)K, (int)cfg) && w.size(1) == K,
-              "gemv_push_norm: 1 <= M <= 4, N % 16 == 0, N <= 8192, K % 128 == 0, K / 128 >= KS, "
-              "no persistent cfg, world <= 8");
-  TORCH_CHECK(rank >= 0 && rank < world, "gemv_push_norm: rank");
-  TORCH_CHECK(rfq::car_push_fits(world, (int)M, (int)N, capacity_bytes),
-              "gemv_push_norm: push slots exceed the custom all-reduce buffer");
-  TORCH_CHECK(x.stride(0) % 8 == 0, "gemv_push_norm: alignment");
-  TORCH_CHECK(residual.size(0) == M && residual.size(1) == N && out.size(0) == M &&
-                  out.size(1) == N && norm_w.numel() == N && residual.stride(0) % 8 == 0 &&
-                  out.stride(0) % 8 == 0,
-              "gemv_push_norm: residual / out [M, N], norm_w [N]");
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= KS * M * N,
-              "gemv_push_norm: fp32 partials workspace of KS*M*N floats");
-  TORCH_CHECK(tile_cnt.is_cuda() && tile_cnt.numel() >= N / 16, "gemv_push_norm: tile counters");
-  TORCH_CHECK(counter.is_cuda() && counter.numel() >= 1, "gemv_push_norm: counter");
-  char* b[8];
-  for (int i = 0; i < world; ++i) b[i] = reinterpret_cast<char*>(bases[i]);
-  rfq::launch_gemv_push_norm(bp(x), x.stride(0), bp(w), (int)N, (int)K, (int)M, (int)cfg,
-                             part.data_ptr<float>(),
-                             reinterpret_cast<unsigned*>(tile_cnt.data_ptr()), bpm(residual),
-                             residual.stride(0), bp(norm_w), bpm(out), out.stride(0), (float)eps,
-                             reinterpret_cast<unsigned*>(counter.data_ptr()), b, (int)rank, world,
-                             cur_stream());
-}
-
 void moe_align(const Tensor& topk_ids, int64_t E, int64_t block_m, const Tensor& sorted_ids,
                const Tensor& inv_pos, const Tensor& expert_of_block,
                const Tensor& expert_offsets, const Tensor& num_blocks) {
@@ -1164,22 +981,10 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("gemv_splitk_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
         "Tensor(d!) part, Tensor(e!) tile_cnt, int cfg) -> ()");
-  m.def("qkv_attn(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
-        "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, "
-        "Tensor(d!) part, Tensor(e!) tile_cnt, int cfg, Tensor block_tables, Tensor seq_q_start, "
-        "Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, int list_tpi, "
-        "int run_tiles, Tensor(f!) out, Tensor(g!) part_o, Tensor(h!) part_ml, float scale, "
-        "int num_splits, Tensor(i!) done, Tensor(j!)? zero_slot, Tensor(k!) err) -> ()");
   m.def("attn_decode_merge(Tensor part_o, Tensor part_ml, Tensor(a!) out, int Hq, "
         "int num_splits) -> ()");
-  m.def("gemv_splitk_merge(Tensor part_o, Tensor part_ml, int S, Tensor w, Tensor(a!) y, "
-        "Tensor(b!) part, Tensor(c!) tile_cnt, int cfg, Tensor(d!)? residual, Tensor? norm_w, "
-        "float eps, Tensor(e!)? out, Tensor(f!)? counter) -> ()");
   m.def("skinny_gemm_rope(Tensor x, Tensor w, Tensor(a!) qkv, Tensor positions, Tensor cos_sin, "
         "Tensor slot_mapping, Tensor(b!) k_cache, Tensor(c!) v_cache, int Hq, int Hkv, int cfg) -> ()");
-  m.def("gemv_push_norm(Tensor x, Tensor w, Tensor(a!) part, Tensor(b!) tile_cnt, int cfg, "
-        "Tensor(c!) residual, Tensor norm_w, float eps, Tensor(d!) out, Tensor(e!) counter, "
-        "int[] bases, int rank, int capacity_bytes) -> ()");
   m.def("car_allreduce(Tensor inp, Tensor(a!) out, int[] bases, int rank, int capacity_bytes, "
         "int algo=0) -> ()");
   m.def("car_allreduce_add_norm(Tensor inp, Tensor(a!) residual, Tensor w, float eps, "
@@ -1201,7 +1006,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, Tensor work_ct, "
         "Tensor(a!) out, Tensor(b!) part_o, Tensor(c!) part_ml, int Hq, int Hkv, float scale, "
-        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None, int waves=1, "
+        "int num_splits, int tiles_per_item=1, Tensor(d!)? tickets=None, "
         "bool reduce=True) -> ()");
   m.def("attn_decode_shared(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, "
         "Tensor seq_q_start, Tensor seq_q_len, Tensor seq_kv_len, Tensor work_seq, "
@@ -1253,10 +1058,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("gemv_splitk_norm", &gemv_splitk_norm);
   m.impl("gemv_splitk_swiglu", &gemv_splitk_swiglu);
   m.impl("gemv_splitk_rope", &gemv_splitk_rope);
-  m.impl("qkv_attn", &qkv_attn);
   m.impl("attn_decode_merge", &attn_decode_merge);
-  m.impl("gemv_splitk_merge", &gemv_splitk_merge);
-  m.impl("gemv_push_norm", &gemv_push_norm);
   m.impl("car_allreduce", &car_allreduce);
   m.impl("car_allreduce_add_norm", &car_allreduce_add_norm);
   m.impl("moe_skinny", &moe_skinny);

@@ -1,7 +1,6 @@
-// Custom all-reduce core shared by the all-reduce kernels (custom_ar.hip) and the
-// row-parallel GEMV that pushes its output straight into the peers' staging
-// (gemv_core.h kGvPush): the signal region layout, the bounded flag protocol and the
-// push form's fixed slots and per-row sum + residual-add RMSNorm.
+// Custom all-reduce core of the all-reduce kernels (custom_ar.hip): the signal region
+// layout, the bounded flag protocol and the push form's fixed slots and per-row sum +
+// residual-add RMSNorm.
 #pragma once
 #include <hip/hip_runtime.h>
 

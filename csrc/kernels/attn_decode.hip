@@ -79,8 +79,8 @@ __global__ __launch_bounds__(1024) void attn_prefix_meta_kernel(
   if (tid == 0) { meta[0] = P * kPage; meta[1] = s_cnt; }
 }
 
-template <int NT, int MODE = 0, int NWV = 1, bool NTK = false>
-__global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
+template <int NT, int MODE = 0, bool NTK = false>
+__global__ __launch_bounds__(64, 2) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
     int bt_stride, const int32_t* __restrict__ seq_q_start, const int32_t* __restrict__ seq_q_len,
@@ -88,12 +88,11 @@ __global__ __launch_bounds__(64 * NWV, 2) void attn_decode_kernel(
     const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
     int num_splits, PrefixArgs px = PrefixArgs{}, int32_t* __restrict__ tickets = nullptr) {
-  __shared__ __attribute__((aligned(16))) bf16_t v_lds_all[NWV * kPage * kD];
-  attn_decode_body<NT, MODE, NWV, NTK, false>(
+  __shared__ __attribute__((aligned(16))) bf16_t v_lds[kPage * kD];
+  attn_decode_body<NT, MODE, NTK>(
       q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len, seq_kv_len,
       work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2, num_splits, px,
-      tickets, blockIdx.x, blockIdx.y, blockIdx.z, NWV > 1 ? (int)(threadIdx.x >> 6) : 0,
-      v_lds_all, FuseWait{});
+      tickets, blockIdx.x, blockIdx.y, blockIdx.z, v_lds);
 }
 
 // Merge split-K partials: one workgroup of 128 lanes (one per dh) per (row, head).
@@ -129,8 +128,8 @@ __global__ __launch_bounds__(128) void attn_decode_reduce_kernel(
   out[(int64_t)b * out_stride + (int64_t)h * kD + d] = f2bf(den > 0.f ? num / den : 0.f);
 }
 
-// Merge split-K partials of `rows` q rows (the fused QKV + attention launch leaves them
-// for this kernel, decode_fused.hip).
+// Merge split-K partials of `rows` q rows (also exposed as ops.attn_decode_merge for a
+// decode attention launched with reduce = false).
 void launch_attn_decode_reduce(const float* part_o, const float* part_ml, bf16_t* out,
                                int64_t out_stride, int rows, int Hq, int num_splits,
                                hipStream_t s) {
@@ -140,60 +139,17 @@ void launch_attn_decode_reduce(const float* part_o, const float* part_ml, bf16_t
 }
 
 // rows = number of q rows covered (for the split-K reduce), W = work items;
-// reduce = false leaves split partials for the consumer to merge (gemv_splitk_merge)
+// reduce = false leaves split partials for the consumer to merge (attn_decode_merge)
 void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache,
                         const bf16_t* v_cache, const int32_t* block_tables, int bt_stride,
                         const int32_t* seq_q_start, const int32_t* seq_q_len,
                         const int32_t* seq_kv_len, const int32_t* work_seq,
                         const int32_t* work_ct, int W, int rows, bf16_t* out, int64_t out_stride,
                         float* part_o, float* part_ml, int Hq, int Hkv, float scale,
-                        int num_splits, int tiles_per_item, int32_t* tickets, int waves,
-                        hipStream_t s, bool reduce) {
+                        int num_splits, int tiles_per_item, int32_t* tickets, hipStream_t s,
+                        bool reduce) {
   if (W == 0 || rows == 0) return;
   const float scale_log2 = scale * 1.4426950408889634f;
-  if (waves == 8 && num_splits % 8 == 0) {
-    // 8 splits per workgroup (one per wave, 2 waves per SIMD) merged in LDS: with 8
-    // splits per (work item, kv head) the whole attention is ONE launch with no
-    // cross-workgroup merge (outer == 1 writes bf16 rows directly)
-    const int outer = num_splits / 8;
-    const dim3 grid8(outer, Hkv, W);
-    int32_t* tk8 = outer > 1 ? tickets : nullptr;
-    if (tiles_per_item == 2)
-      attn_decode_kernel<2, 0, 8><<<grid8, 512, 0, s>>>(
-          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
-          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
-          outer, PrefixArgs{}, tk8);
-    else
-      attn_decode_kernel<1, 0, 8><<<grid8, 512, 0, s>>>(
-          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
-          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
-          outer, PrefixArgs{}, tk8);
-    if (outer > 1 && tk8 == nullptr && reduce)
-      attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
-                                                          outer);
-    return;
-  }
-  if (waves == 4 && num_splits % 4 == 0) {
-    // 4 splits per workgroup merged in LDS; the workgroups' partials merged in-kernel
-    // by the last to finish (tickets) or, without tickets, by the reduce launch
-    const int outer = num_splits / 4;
-    const dim3 grid4(outer, Hkv, W);
-    int32_t* tk4 = outer > 1 ? tickets : nullptr;
-    if (tiles_per_item == 2)
-      attn_decode_kernel<2, 0, 4><<<grid4, 256, 0, s>>>(
-          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
-          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
-          outer, PrefixArgs{}, tk4);
-    else
-      attn_decode_kernel<1, 0, 4><<<grid4, 256, 0, s>>>(
-          q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,
-          seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,
-          outer, PrefixArgs{}, tk4);
-    if (outer > 1 && tk4 == nullptr && reduce)
-      attn_decode_reduce_kernel<<<rows * Hq, 128, 0, s>>>(part_o, part_ml, out, out_stride, Hq,
-                                                          outer);
-    return;
-  }
   dim3 grid(num_splits, Hkv, W);
   int32_t* tk = num_splits > 1 ? tickets : nullptr;
   // RFQ_ATTN_NT=1: non-temporal loads for the per-sequence KV pages (NTK above)
@@ -202,7 +158,7 @@ void launch_attn_decode(const bf16_t* q, int64_t q_stride, const bf16_t* k_cache
     return v != nullptr && v[0] == '1';
   }();
 #define RFQ_AD_LAUNCH(T, N)                                                                     \
-  attn_decode_kernel<T, 0, 1, N><<<grid, 64, 0, s>>>(                                            \
+  attn_decode_kernel<T, 0, N><<<grid, 64, 0, s>>>(                                            \
       q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_q_start, seq_q_len,            \
       seq_kv_len, work_seq, work_ct, out, out_stride, part_o, part_ml, Hq, Hkv, scale_log2,      \
       num_splits, PrefixArgs{}, tk)

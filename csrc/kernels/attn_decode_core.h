@@ -1,5 +1,4 @@
-// Decode attention core (paged, GQA, split-K) shared by attn_decode.hip (its own launch)
-// and decode_fused.hip (inside the fused QKV + attention launch of the latency path).
+// Decode attention core (paged, GQA, split-K) of attn_decode.hip.
 // The design notes are at the top of attn_decode.hip.
 #pragma once
 #include "common.h"
@@ -24,27 +23,7 @@ struct PrefixArgs {
   float* pre_ml;           // [rows][Hq][2] running max (log2 domain), softmax sum
 };
 
-// LDS hand-off inside one wave's V tile buffer.  One wave per workgroup: the block
-// barrier (as before).  Several waves with independent split loops (different page
-// counts): a barrier would mismatch, and the tile buffer is the wave's own, so draining
-// this wave's LDS operations (in-order per wave) and fencing the compiler suffices.
-template <int NWV>
-__device__ __forceinline__ void wave_lds_sync() {
-  if constexpr (NWV == 1) {
-    __syncthreads();
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // (64, 2): two waves per SIMD — NT=2 fits in 244 VGPRs without AGPR spill-over.
-// NWV > 1 (small decode batches): a workgroup of NWV waves, one KV split per wave,
-// merged through LDS before the workgroup's single partial (or, with one workgroup per
-// item, the bf16 output) leaves the CU.  16 splits of one (work item, kv head) then
-// cost 4 workgroups + a 4-way in-kernel merge instead of 16 waves whose partials a
-// second launch (attn_decode_reduce) or a 16-way single-wave merge combines: the
-// decode step of a batch-1 request runs one attention launch per layer.
 // NTK: K / V pages past the first kNtFromPage of a sequence are loaded non-temporal.
 // Those pages belong to one sequence and are read once per step per layer; the leading
 // pages hold the prompt prefix every request shares (prefix cache), which the other
@@ -57,55 +36,7 @@ __device__ __forceinline__ s16x8 ld16(const bf16_t* p) {
   else return *reinterpret_cast<const s16x8*>(p);
 }
 
-// Fused mode (decode_fused.hip): the decode attention waves run in the same launch as
-// the QKV GEMV that produces q and this step's new K / V rows.  A wave prefetches the
-// KV pages that hold only earlier tokens, then waits until every QKV tile of its kv
-// group has published (done[kvh] == expect; the tiles store write-through and count
-// themselves, gemv_core.h PUB), and reads q and the pages holding new tokens with sc1
-// loads, which no L1 / L2 line of this launch can have cached stale: no wave touches
-// those bytes before the wait.  Each layer of a forward has its own counter slot, and
-// the launch of layer l zeroes layer l-1's slot (the last layer's is zeroed by the next
-// forward's layer 0), so a slot is zero whenever its launch starts.  Work items that
-// are padding, or whose column tile holds no (query, head) column, exit at once.
-// Spins are bounded in wall time; a timeout is counted in *err (the runner then fails
-// the step).
-struct FuseWait {
-  unsigned* done;      // [Hkv]: QKV tiles of each kv group published in this launch
-  unsigned expect;     // QKV tiles per kv group: (G + 2) * 4
-  unsigned* err;       // timeouts
-  int ct_mult, ct_add; // column tile of this wave: work_ct[w] * ct_mult + ct_add
-};
-
-constexpr uint64_t kFuseSpinTicks = 50000000;   // 0.5 s at the 100 MHz realtime clock
-constexpr int kFuseStride = 32;                  // counter words per kv head (128 B)
-
-__device__ __forceinline__ void fuse_wait(const FuseWait& fw, int kvh) {
-  gu32* d = (gu32*)(fw.done + kFuseStride * kvh);   // one 128-B line per kv head
-  if ((threadIdx.x & 63) == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fw.expect) {
-      __builtin_amdgcn_s_sleep(4);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kFuseSpinTicks) {
-        __hip_atomic_fetch_add((gu32*)fw.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  // the wave's later loads are issued after lane 0's poll has matched (program order);
-  // keep the compiler from moving them above it
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// 16-byte sc1 load (two 8-byte agent-scope loads: L1 bypassed)
-__device__ __forceinline__ s16x8 ld16_sc1(const bf16_t* p) {
-  const gu64* a = (const gu64*)p;
-  const unsigned long long lo = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long hi = __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const u32x4 r = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-  return __builtin_bit_cast(s16x8, r);
-}
-
-template <int NT, int MODE = 0, int NWV = 1, bool NTK = false, bool FUSED = false>
+template <int NT, int MODE = 0, bool NTK = false>
 __device__ __forceinline__ void attn_decode_body(
     const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables,
@@ -114,12 +45,7 @@ __device__ __forceinline__ void attn_decode_body(
     const int32_t* __restrict__ work_ct, bf16_t* __restrict__ out, int64_t out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale_log2,
     int num_splits, const PrefixArgs& px, int32_t* __restrict__ tickets, int split, int kvh,
-    int w, int wv, bf16_t* __restrict__ v_lds_all, const FuseWait& fw) {
-  static_assert(!FUSED || (NT == 1 && MODE == 0 && NWV == 1), "fused: one tile, one wave");
-  bf16_t* v_lds = v_lds_all + wv * kPage * kD;
-  // split: the workgroup's (outer) split, which the partial / merge epilogue indexes;
-  // gsplit / nsplit: this wave's KV range among all NWV * num_splits
-  const int gsplit = split * NWV + wv, nsplit = num_splits * NWV;
+    int w, bf16_t* __restrict__ v_lds) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;   // 16-lane group
   const int c = lane & 15;   // MFMA column
@@ -150,7 +76,7 @@ __device__ __forceinline__ void attn_decode_body(
     // NT column tiles per work item share every K fragment and V tile they load
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int tile = FUSED ? work_ct[w] * fw.ct_mult + fw.ct_add : work_ct[w] * NT + t;
+      const int tile = work_ct[w] * NT + t;
       act[t] = tile * 16 < ql * G;                       // wave-uniform
       const int col = tile * 16 + c;
       cvalid[t] = col < ql * G;
@@ -159,14 +85,11 @@ __device__ __forceinline__ void attn_decode_body(
       qrow[t] = seq_q_start[seq] + qi;
       lim[t] = kvl - ql + qi + 1;                        // keys [0, lim) visible
     }
-    if constexpr (FUSED) {
-      if (!act[0]) return;     // this wave's column tile holds no (query, head) column
-    }
   }
 
-  int tps = (kvl - base + nsplit - 1) / nsplit;
+  int tps = (kvl - base + num_splits - 1) / num_splits;
   tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = base + gsplit * tps;
+  const int start = base + split * tps;
   const int end = min(kvl, start + tps);
 
   float m_run[NT], l_run[NT];
@@ -182,19 +105,15 @@ __device__ __forceinline__ void attn_decode_body(
   if (start < end && ql > 0) {
     // Q^T fragments: B[k = dh][col]; lane holds Q[qrow, h][32ks + 8g .. +7]
     s16x8 qf[NT][4];
-    auto load_q = [&](bool sc) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const bf16_t* qp = q + (int64_t)qrow[t] * q_stride + (int64_t)h[t] * kD;
+    for (int t = 0; t < NT; ++t) {
+      const bf16_t* qp = q + (int64_t)qrow[t] * q_stride + (int64_t)h[t] * kD;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          qf[t][ks] = sc ? ld16_sc1(qp + 32 * ks + 8 * g)
-                         : reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
-          if (!cvalid[t]) qf[t][ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
-        }
+      for (int ks = 0; ks < 4; ++ks) {
+        qf[t][ks] = reinterpret_cast<const s16x8*>(qp + 32 * ks + 8 * g)[0];
+        if (!cvalid[t]) qf[t][ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
       }
-    };
-    if constexpr (!FUSED) load_q(false);
+    }
     const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
     const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
     const int np = pg_last - pg0 + 1;
@@ -204,20 +123,12 @@ __device__ __forceinline__ void attn_decode_body(
     int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
     // issue page j's K fragments (A operand: row = key, k = dh) and V rows (g + 4i,
     // chunk c) into registers; must be called with j = 0, 1, 2, ...
-    auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8], bool sc = false) {
+    auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
       const int64_t page = pg_next;
       pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
-      if (FUSED && sc) {             // a page that holds this step's new K / V rows
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-            kf[mt][ks] = ld16_sc1(kb + (16 * mt + c) * kD + 32 * ks + 8 * g);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) vr[i] = ld16_sc1(vb + (g + 4 * i) * kD + 8 * c);
-      } else if (NTK && pg0 + j >= kNtFromPage) {
+      if (NTK && pg0 + j >= kNtFromPage) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -293,7 +204,7 @@ __device__ __forceinline__ void attn_decode_body(
         pb[t] = pack8(p);
       }
 
-      wave_lds_sync<FUSED ? 2 : NWV>();  // V tile visible (one wave per tile buffer)
+      __syncthreads();  // V tile visible
 
       // ---- O^T += V^T P^T (one transposed V read feeds every tile) ----
       const int q4 = c >> 2, p4 = c & 3;
@@ -310,28 +221,11 @@ __device__ __forceinline__ void attn_decode_body(
             o[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(pb[t]),
                                                               o[t][m], 0, 0, 0);
       }
-      wave_lds_sync<FUSED ? 2 : NWV>();  // before the next tile overwrites v_lds
+      __syncthreads();  // before the next tile overwrites v_lds
     };
 
     s16x8 kA[2][4], vA[8];
-    if constexpr (FUSED) {
-      // pages before first_new hold only earlier tokens: fetch them before the wait;
-      // the rest (this step's rows, written by the QKV tiles of this launch) after it
-      // One page register set: the fused kernel runs 8-wave workgroups at <= 256 VGPRs,
-      // and a second set (the stand-alone NT 1 form's) spilled to scratch.
-      constexpr int kVmcnt0 = 0x0F70;          // vmcnt(0), expcnt / lgkmcnt untouched
-      const int first_new = (kvl - ql) / kPage;
-      const bool p0 = pg0 < first_new;
-      if (p0) fetch(0, kA, vA);
-      fuse_wait(fw, kvh);
-      load_q(true);
-      if (!p0) fetch(0, kA, vA, true);
-      for (int j = 0; j < np; ++j) {
-        __builtin_amdgcn_s_waitcnt(kVmcnt0);
-        process(j, kA, vA);
-        if (j + 1 < np) fetch(j + 1, kA, vA, pg0 + j + 1 >= first_new);
-      }
-    } else if constexpr (NT == 1) {
+    if constexpr (NT == 1) {
       // NT 1 has the registers for a second page in flight: page j+1's K / V loads
       // are issued before page j is processed (two register sets, unrolled by two), so
       // a split walking several pages pays one memory round trip, not one per page
@@ -356,74 +250,6 @@ __device__ __forceinline__ void attn_decode_body(
         fetch(j, kA, vA);
         process(j, kA, vA);
       }
-    }
-  }
-
-  if constexpr (NWV > 1) {
-    // ---- merge the NWV waves' splits through LDS (the V tile buffers are reused) ----
-    __shared__ float ml_lds[NWV][NT][16][2];
-    float* obuf = reinterpret_cast<float*>(v_lds_all);   // (NWV-1) x 8 x 64 f32x4 <= v_lds
-    static_assert((NWV - 1) * 8 * 64 * 16 <= NWV * kPage * kD * 2, "merge buffer");
-    float lt[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      lt[t] = l_run[t];
-      lt[t] += __shfl_xor(lt[t], 16, 64);
-      lt[t] += __shfl_xor(lt[t], 32, 64);
-    }
-    __syncthreads();                                   // every wave is done with v_lds
-    if (g == 0) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        ml_lds[wv][t][c][0] = m_run[t];
-        ml_lds[wv][t][c][1] = lt[t];
-      }
-    }
-    __syncthreads();
-    float a_self[NT], l_all[NT], m_all[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float ms = -INFINITY;
-#pragma unroll
-      for (int v2 = 0; v2 < NWV; ++v2) ms = fmaxf(ms, ml_lds[v2][t][c][0]);
-      const float mu = ms == -INFINITY ? 0.f : ms;
-      float l = 0.f;
-#pragma unroll
-      for (int v2 = 0; v2 < NWV; ++v2) {
-        const float mw = ml_lds[v2][t][c][0];
-        l += (mw == -INFINITY ? 0.f : fast_exp2(mw - mu)) * ml_lds[v2][t][c][1];
-      }
-      a_self[t] = m_run[t] == -INFINITY ? 0.f : fast_exp2(m_run[t] - mu);
-      m_all[t] = ms;
-      l_all[t] = l;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if (wv > 0) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-          reinterpret_cast<f32x4*>(obuf)[((wv - 1) * 8 + m) * 64 + lane] = o[t][m] * a_self[t];
-      }
-      __syncthreads();
-      if (wv == 0) {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          f32x4 acc = o[t][m] * a_self[t];
-#pragma unroll
-          for (int v2 = 1; v2 < NWV; ++v2)
-            acc += reinterpret_cast<const f32x4*>(obuf)[((v2 - 1) * 8 + m) * 64 + lane];
-          o[t][m] = acc;
-        }
-      }
-      __syncthreads();
-    }
-    if (wv != 0) return;
-    // wave 0 carries the workgroup's merged state into the epilogue below: the
-    // per-lane partial sums must add up to the merged denominator over the 4 groups
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      m_run[t] = m_all[t];
-      l_run[t] = g == 0 ? l_all[t] : 0.f;
     }
   }
 

@@ -507,64 +507,6 @@ void launch_gemv_splitk_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int 
                                   NormEpi{}, re, 0, s);
 }
 
-// The o projection with the decode attention's split merge as its prologue (AM in
-// gemv_core.h): y = merge(part_o, part_ml) . W^T [+ residual-add RMSNorm], K = Hq * 128.
-template <int NW, int U, int EPI, bool TL, bool NTL>
-__global__ __launch_bounds__(NW * 64) void gemv_splitk_merge_kernel(
-    AttnMerge am, const bf16_t* __restrict__ W, int K, bf16_t* __restrict__ Y, int64_t ldy,
-    int M, int KS, float* __restrict__ part, int Nn, unsigned* __restrict__ tile_cnt, NormEpi ep,
-    int units) {
-  gemv_splitk_unit<NW, U, EPI, TL, NTL, false, true>(blockIdx.x, units / KS, nullptr, 0, W, K, Y,
-                                                      ldy, M, KS, part, Nn, tile_cnt, ep,
-                                                      RopeEpi{}, 0, nullptr, am);
-}
-
-// Host-side shape rule of the merge prologue (the LDS copy of the slice's X rows).
-bool gemv_merge_fits(int M, int K, int cfg, int S) {
-  const int KS = 2 << (cfg & 3), nks_all = K >> 7;
-  const int nks_max = (nks_all + KS - 1) / KS;
-  return M >= 1 && M <= 16 && S >= 2 && S <= kAmMaxS && K % 128 == 0 && nks_all >= KS &&
-         M * nks_max * 128 <= kAmLdsElems && !(cfg & 64);
-}
-
-void launch_gemv_splitk_merge(const float* part_o, const float* part_ml, int S, const bf16_t* W,
-                              int N, int K, bf16_t* Y, int64_t ldy, int M, int cfg, float* part,
-                              unsigned* tile_cnt, bf16_t* residual, int64_t res_stride,
-                              const bf16_t* norm_w, bf16_t* out, int64_t out_stride, float eps,
-                              unsigned* counter, hipStream_t s) {
-  const int KS = 2 << (cfg & 3);
-  const int units = (N / 16) * KS;
-  const AttnMerge am{part_o, part_ml, S};
-  // residual == nullptr: plain epilogue; else the residual-add RMSNorm (NormEpi)
-  const NormEpi e{residual, res_stride, norm_w, out, out_stride, eps, counter, nullptr, 0};
-  const NormEpi* ep = residual != nullptr ? &e : nullptr;
-#define GM_LAUNCH1(nw, u, epi, tl, nt)                                                         \
-  hipLaunchKernelGGL((gemv_splitk_merge_kernel<nw, u, epi, tl, nt>), dim3(units), dim3(nw * 64), \
-                     0, s, am, W, K, Y, ldy, M, KS, part, N, tile_cnt, e, units)
-#define GM_LAUNCH(nw, u, epi)                                                                  \
-  switch ((cfg >> 4) & 3) {                                                                    \
-    case 0: GM_LAUNCH1(nw, u, epi, false, false); break;                                       \
-    case 1: GM_LAUNCH1(nw, u, epi, true, false); break;                                        \
-    case 2: GM_LAUNCH1(nw, u, epi, false, true); break;                                        \
-    default: GM_LAUNCH1(nw, u, epi, true, true); break;                                        \
-  }
-#define GM_EPI(epi)                                                                            \
-  switch ((cfg >> 2) & 3) {                                                                    \
-    case 0: GM_LAUNCH(4, 4, epi); break;                                                       \
-    case 1: GM_LAUNCH(8, 4, epi); break;                                                       \
-    case 2: GM_LAUNCH(4, 2, epi); break;                                                       \
-    default: GM_LAUNCH(8, 2, epi); break;                                                      \
-  }
-  if (ep != nullptr) {
-    GM_EPI(kGvNorm);
-  } else {
-    GM_EPI(kGvPlain);
-  }
-#undef GM_EPI
-#undef GM_LAUNCH
-#undef GM_LAUNCH1
-}
-
 // ---------------------------------------------------------------------------
 // MoE latency path: the same weight-streaming structure applied per expert.
 //

@@ -1,9 +1,7 @@
-// Split-K weight-streaming GEMV core (M <= 16) and its epilogues, shared by
-// gemm_skinny.hip (gemv_splitk / skinny kernels) and decode_fused.hip (the fused
-// QKV + RoPE + KV-append + decode-attention launch of the latency path).
+// Split-K weight-streaming GEMV core (M <= 16) and its epilogues, used by
+// gemm_skinny.hip (gemv_splitk / skinny kernels).
 #pragma once
 #include "common.h"
-#include "../comm/car_core.h"
 
 namespace rfq {
 
@@ -149,62 +147,7 @@ struct RopeEpi {
 //             +16) of one head (RopeEpi): NeoX RoPE on q / k, q to Y, k / v appended
 //             to the paged cache.  The TP = 8 QKV shard (N = 1,280) has only 40 such
 //             pairs: split K is what lets it use more than 40 CUs.
-//   kGvPush   (TP row-parallel o / down, M <= kGvPushMaxM) the tile's bf16 outputs go
-//             straight into slot [parity][rank][row] of every TP rank's custom
-//             all-reduce staging (remote stores, car_core.h); each workgroup releases
-//             them at system scope before its ticket on ep.counter, and the grid's last
-//             one raises this rank's flag on every peer, waits for every peer's flag and
-//             runs the all-reduce sum + residual-add RMSNorm of car_push_add_norm_kernel
-//             (car_push_sum_norm_row) -- the o / down GEMV, the all-reduce and the norm
-//             in one launch, bit-identical to gemv_splitk + the push all-reduce.
-enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3, kGvPush = 4 };
-constexpr int kGvPushMaxM = 4;
-
-// kGvPush: the custom all-reduce regions (every rank's base, own included).
-struct PushEpi {
-  char* base[kCarMaxRanks];
-  int rank, world;
-};
-
-// The all-reduce tail of kGvPush, run by the grid's last workgroup once every tile of
-// this rank has pushed its rows: raise flag push[par_b][b][rank] on every peer for the
-// M rows, wait for every peer's flags (bounded, car_wait), then per row the rank-order
-// sum + residual-add RMSNorm of the push all-reduce (car_push_sum_norm_row: the same
-// code, so bit-identical), and advance the row counters.
-__device__ __forceinline__ void gemv_push_tail(const PushEpi& pe, const NormEpi& ep, int M, int d,
-                                            float* scratch) {
-  CarSignal* self = reinterpret_cast<CarSignal*>(pe.base[pe.rank]);
-  const int tid = threadIdx.x;
-  __shared__ uint32_t cnt_s[kGvPushMaxM];
-  __shared__ int fail_s;
-  if (tid < M) cnt_s[tid] = self->counter[tid] + 1;
-  if (tid == 0) fail_s = 0;
-  __syncthreads();
-  const int nf = pe.world * M;
-  if (tid < nf) {
-    const int p = tid % pe.world, b = tid / pe.world;
-    const uint32_t c = cnt_s[b];
-    CarSignal* peer = reinterpret_cast<CarSignal*>(pe.base[p]);
-    car_store(&peer->push[c & 1u][b][pe.rank], c);
-  }
-  constexpr int NCH = 4;                     // d <= 8192 = 8 * 256 * 4
-  s16x8 rv[NCH], wv[NCH];
-  car_push_preload<NCH>(0, ep.residual, ep.res_stride, ep.w, d, rv, wv);
-  if (tid < nf) {
-    const int p = tid % pe.world, b = tid / pe.world;
-    const uint32_t c = cnt_s[b];
-    if (!car_wait(self, &self->push[c & 1u][b][p], c, kCarPush, b, p)) fail_s = 1;
-  }
-  __syncthreads();
-  for (int b = 0; b < M; ++b) {
-    if (b > 0) car_push_preload<NCH>(b, ep.residual, ep.res_stride, ep.w, d, rv, wv);
-    car_push_sum_norm_row<NCH>(pe.base[pe.rank], (int)(cnt_s[b] & 1u), pe.world, b,
-                               ep.residual, ep.res_stride, rv, wv, ep.out, ep.out_stride, d,
-                               ep.eps, scratch);
-  }
-  if (tid < M) self->counter[tid] = cnt_s[tid];
-  if (tid == 0 && fail_s) atomicAdd(&self->error, 1u);
-}
+enum { kGvPlain = 0, kGvNorm = 1, kGvSwi = 2, kGvRope = 3 };
 
 //
 // TL (cfg bit 4): W is stored in the decode-tiled layout (ops.tile_weight): for
@@ -217,45 +160,15 @@ __device__ __forceinline__ void gemv_push_tail(const PushEpi& pe, const NormEpi&
 // step by one CU, so it need not displace the activations / partials in L2.
 // One work unit (16-row tile bt = unit / KS, K slice unit % KS) of the split-K GEMV;
 // every early return below is workgroup-uniform.
-// PUB (kGvRope only; decode_fused.hip): the tile's q / k / v results are stored
-// write-through (8-byte sc1 stores), drained by the storing wave's vmcnt(0), and the
-// tile is then counted on done[kv group] (relaxed agent-scope add): the decode
-// attention waves of that kv head, running in the same launch, poll that counter and
-// read q and the new KV rows with sc1 loads (cdna_hip_programming.md §6 Guideline 16,
-// R1 counter form; the producer is one wave, so no workgroup barrier is needed).
-//
-// AM (attention-merge prologue; kGvPlain / kGvNorm): X is not read from memory but is
-// the decode attention output still in its split-K partials (attn_decode.hip with
-// num_splits > 1 and no reduce launch): part_o [rows][Hq][S][128], part_ml
-// [rows][Hq][S][2] fp32, K = Hq * 128, so a unit's K slice is a run of whole heads.
-// The unit first issues its first weight round, then every thread merges float4
-// granules of the slice's heads (all S partials in flight at once, the same
-// arithmetic and order as attn_decode_reduce_kernel, so bit-identical rows) into a
-// bf16 LDS copy of the M x slice rows, and the MFMA loop reads X from there.  This is
-// the o projection with the separate merge launch folded in: the partial reads (a few
-// KB per head, L2-resident) overlap the unit's own weight stream instead of costing a
-// launch boundary plus the merge kernel's latency chain.
-struct AttnMerge {
-  const float* po;
-  const float* ml;
-  int S;                          // splits, 2..16
-};
-constexpr int kAmMaxS = 16;
-constexpr int kAmLdsElems = 16384;  // M * (slice heads) * 128 bf16 <= 32 KB
-
-template <int NW, int U, int EPI, bool TL, bool NTL, bool PUB = false, bool AM = false>
+template <int NW, int U, int EPI, bool TL, bool NTL>
 __device__ __forceinline__ void gemv_splitk_unit(
     int unit, int ntile, const bf16_t* __restrict__ X, int64_t ldx,
     const bf16_t* __restrict__ W, int K, bf16_t* __restrict__ Y, int64_t ldy, int M, int KS,
     float* __restrict__ part, int Nn, unsigned* __restrict__ tile_cnt, const NormEpi& ep,
-    const RopeEpi& re, int up_off, unsigned* __restrict__ done = nullptr,
-    AttnMerge am = AttnMerge{}, PushEpi pe = PushEpi{}) {
-  static_assert(!PUB || EPI == kGvRope, "PUB: the rope epilogue only");
-  static_assert(!AM || EPI == kGvPlain || EPI == kGvNorm, "AM: plain / norm epilogues only");
+    const RopeEpi& re, int up_off) {
   constexpr int NT = (EPI == kGvSwi || EPI == kGvRope) ? 2 : 1;
   __shared__ f32x4 red[NW][NT][64];
   __shared__ float nscratch[17];
-  __shared__ __attribute__((aligned(16))) bf16_t xs[AM ? kAmLdsElems : 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int bt = unit / KS, slice = unit - bt * KS;
@@ -282,86 +195,21 @@ __device__ __forceinline__ void gemv_splitk_unit(
                : W + (int64_t)(row0[a] + r) * K + g * 8;
   const bool xv = r < M;
 
-  // AM: X rows live in LDS as [M][nks * 128] (slice-relative k); else in global memory
-  const bf16_t* xp = AM ? xs + (int64_t)(xv ? r : 0) * nks * 128 - sl0 * 128 + g * 8
-                        : X + (int64_t)(xv ? r : 0) * ldx + g * 8;
+  const bf16_t* xp = X + (int64_t)(xv ? r : 0) * ldx + g * 8;
   const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
   f32x4 acc[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
   int ks = ks0;
-  s16x8 w0[U][NT][4];
-  bool pre = false;
-  if constexpr (AM) {
-    // the first weight round goes out before the merge so the two overlap
-    if (ks + U <= ks1) {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int a = 0; a < NT; ++a)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            w0[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
-      pre = true;
-    }
-    const int Hq = K >> 7, S = am.S;
-    for (int it = threadIdx.x; it < M * nks * 32; it += NW * 64) {
-      const int d4 = it & 31, rest = it >> 5;
-      const int rr = rest / nks, hl = rest - rr * nks;
-      const int64_t bh = (int64_t)rr * Hq + sl0 + hl;
-      const float* mlp = am.ml + bh * S * 2;
-      const float* pop = am.po + bh * S * 128 + d4 * 4;
-      float2 m2[kAmMaxS];
-      f32x4 p[kAmMaxS];
-#pragma unroll
-      for (int s = 0; s < kAmMaxS; ++s)
-        if (s < S) {
-          m2[s] = *reinterpret_cast<const float2*>(mlp + 2 * s);
-          p[s] = *reinterpret_cast<const f32x4*>(pop + s * 128);
-        }
-      float gm = -INFINITY;
-#pragma unroll
-      for (int s = 0; s < kAmMaxS; ++s)
-        if (s < S) gm = fmaxf(gm, m2[s].x);
-      f32x4 num = {0.f, 0.f, 0.f, 0.f};
-      float den = 0.f;
-      if (gm != -INFINITY) {
-#pragma unroll
-        for (int s = 0; s < kAmMaxS; ++s) {   // no break / continue: keeps m2 / p in VGPRs
-          if (s < S && m2[s].x != -INFINITY) {
-            const float wgt = fast_exp2(m2[s].x - gm);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) num[i] += wgt * p[s][i];
-            den += wgt * m2[s].y;
-          }
-        }
-      }
-      uint2 v;
-      v.x = pack_bf16x2(den > 0.f ? num[0] / den : 0.f, den > 0.f ? num[1] / den : 0.f);
-      v.y = pack_bf16x2(den > 0.f ? num[2] / den : 0.f, den > 0.f ? num[3] / den : 0.f);
-      *reinterpret_cast<uint2*>(xs + (rr * nks + hl) * 128 + d4 * 4) = v;
-    }
-    __syncthreads();
-  }
   for (; ks + U <= ks1; ks += U) {
     s16x8 w[U][NT][4], x[U][4];
-    if (AM && pre) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int a = 0; a < NT; ++a)
+      for (int a = 0; a < NT; ++a)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) w[u][a][j] = w0[u][a][j];
-      pre = false;
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int a = 0; a < NT; ++a)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
-    }
+        for (int j = 0; j < 4; ++j)
+          w[u][a][j] = ldw<NTL>(wp[a] + (int64_t)(ks + u) * KSTEP + j * JSTEP);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -500,30 +348,8 @@ __device__ __forceinline__ void gemv_splitk_unit(
         }
       }
       if (dst != nullptr) {
-        if constexpr (PUB) {
-          __hip_atomic_store((gu64*)(dst + d0), (unsigned long long)v1.x |
-                             ((unsigned long long)v1.y << 32), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store((gu64*)(dst + 64 + d0), (unsigned long long)v2.x |
-                             ((unsigned long long)v2.y << 32), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          *reinterpret_cast<uint2*>(dst + d0) = v1;
-          *reinterpret_cast<uint2*>(dst + 64 + d0) = v2;
-        }
-      }
-    } else if constexpr (EPI == kGvPush) {
-      // the tile's bf16 outputs (= the GEMV's Y) into slot [parity][rank][r] of every
-      // rank's staging: remote stores over xGMI, own region included
-      uint2 v;
-      v.x = pack_bf16x2(s[0][0], s[0][1]);
-      v.y = pack_bf16x2(s[0][2], s[0][3]);
-      // row r's all-reduce call counter + 1 (read by the tile's final workgroup only)
-      const uint32_t push_c = reinterpret_cast<const CarSignal*>(pe.base[pe.rank])->counter[r] + 1;
-      const int par = (int)(push_c & 1u);
-      for (int p = 0; p < pe.world; ++p) {
-        bf16_t* dst = reinterpret_cast<bf16_t*>(car_push_slot(pe.base[p], par, pe.rank, r));
-        *reinterpret_cast<uint2*>(dst + row0[0] + g * 4) = v;
+        *reinterpret_cast<uint2*>(dst + d0) = v1;
+        *reinterpret_cast<uint2*>(dst + 64 + d0) = v2;
       }
     } else {
       uint2 v;
@@ -536,37 +362,6 @@ __device__ __forceinline__ void gemv_splitk_unit(
       else
         *reinterpret_cast<uint2*>(yp) = v;
     }
-  }
-  if constexpr (PUB) {
-    if (wave == 0) {                       // the only wave that stored results
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        const int h = bt >> 2, G = re.Hq / re.Hkv;
-        const int grp = h < re.Hq ? h / G : (h < re.Hq + re.Hkv ? h - re.Hq : h - re.Hq - re.Hkv);
-        __hip_atomic_fetch_add(done + 32 * grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  if constexpr (EPI == kGvPush) {
-    // drain the pushed rows, count the tile; the grid's last workgroup (every tile's
-    // rows acknowledged by every peer's memory) runs the all-reduce tail.  No per-
-    // workgroup fence: the staging is uncached (hipDeviceMallocUncached), so there is no
-    // dirty L2 line to write back, and a store's vmcnt acknowledgement is its completion
-    // at the target -- a system-scope release here (an L2 writeback per workgroup) made
-    // the launch 5-10x slower (profiles/r4_gemv_push.md).  The flags that publish the
-    // rows are release stores (car_store).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned prev =
-          __hip_atomic_fetch_add(ep.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      nscratch[16] = (prev == (unsigned)ntile - 1) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (nscratch[16] == 0.f) return;
-    if (threadIdx.x == 0)
-      __hip_atomic_store(ep.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    gemv_push_tail(pe, ep, M, ntile * 16, nscratch);
   }
   if constexpr (EPI == kGvNorm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -144,11 +144,14 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
   for (int m = 0; m < MM; ++m) ssq[m] = 0.f;
   if (valid) {
     const int nch = K >> 9;
-    // W: the wave's RW rows (wave-uniform base, RW * K * 2 bytes); X: the M token rows,
-    // records end at row M so the loads of rows m >= M return zeros (no branch)
+    // W: the wave's RW rows (wave-uniform base, RW * K * 2 bytes; the plain form's last
+    // wave may own fewer than RW rows when RW does not divide N: its records stop at row
+    // N, so loads of rows past the weight return zeros instead of reading past it); X: the
+    // M token rows, records end at row M so the loads of rows m >= M return zeros
+    const int rows_here = EPI == kRwPlain ? min(RW, N - row0) : RW;
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(W + (int64_t)__builtin_amdgcn_readfirstlane(row0) * K), (short)0,
-        ((RW - 1) * rstride + 1) * K * 2, 0x00020000);
+        ((rows_here - 1) * rstride + 1) * K * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t xr =
         __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(M * ldx * 2), 0x00020000);
     const int voff = lane * 16;

@@ -44,11 +44,6 @@ from .weights import init_weights
 # 512 / 1024 / 2048), off with 8 columns per kv head (70B at TP=8 and TP=1: two merge
 # rounds, the reduce launch is 0.6-0.9 µs faster) -- profiles/r5_tp8_rank_emulation.md.
 SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "auto").lower()
-# RFQ_DECODE_WG_MERGE=1: with >= 4 splits, four splits share a workgroup and merge
-# through LDS (attn_decode.hip NWV = 4) and the workgroups' partials merge in-kernel:
-# one launch per layer.  Off by default: measured 1-2 us per layer SLOWER than one wave
-# per split + the reduce launch at batch 1 (profiles/r3_decode_attention_wg_merge.md).
-DECODE_WG_MERGE = os.environ.get("RFQ_DECODE_WG_MERGE", "0") == "1"
 
 
 @dataclass
@@ -257,23 +252,11 @@ class DecoderLM:
         # TP = 1 latency path: the o / down skinny GEMM runs the residual-add
         # RMSNorm in its last workgroup when the start-up plan measured it faster
         fuse = not self.tp.enabled and T <= ops.NORM_FUSE_MAX_M
-        mcfg = self._merge_cfg(m, x, dec_parts, shared, fuse)
         for li in range(L):
             lw = w["layers"][li]
-            self._attend(li, x, attn, m, dec_parts, shared, merge=mcfg >= 0)
-            if mcfg >= 0:
-                # the attention left its split partials: the o GEMV merges them itself
-                po, pm = dec_parts
-                if fuse:
-                    ops.linear_merge(po, pm, m.decode_splits, lw["o"], T, mcfg,
-                                     norm=(residual, lw["mlp_norm"], eps, x))
-                else:
-                    o = ops.linear_merge(po, pm, m.decode_splits, lw["o"], T, mcfg)
-                    self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
-            elif not ((fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"],
-                                                    eps, x))
-                      or self.tp.linear_add_norm_(attn, lw["o"], residual, lw["mlp_norm"], eps,
-                                                  x)):
+            self._attend(li, x, attn, m, dec_parts, shared)
+            if not (fuse and ops.linear_add_norm(attn, lw["o"], residual, lw["mlp_norm"], eps,
+                                                 x)):
                 o = ops.linear(attn, lw["o"])
                 self.tp.all_reduce_add_norm_(o, residual, lw["mlp_norm"], eps, x)
             nxt = w["layers"][li + 1]["attn_norm"] if li + 1 < L else w["final_norm"]
@@ -286,9 +269,6 @@ class DecoderLM:
                 act = ops.linear_swiglu(x, lw["gate_up"]) if T <= ops.NORM_FUSE_MAX_M else None
                 if act is not None:
                     if fuse and ops.linear_add_norm(act, lw["down"], residual, nxt, eps, x):
-                        continue
-                    # TP: down + all-reduce + norm in one launch (RFQ_GEMV_PUSH=1)
-                    if self.tp.linear_add_norm_(act, lw["down"], residual, nxt, eps, x):
                         continue
                     mo = ops.linear(act, lw["down"])
                 else:
@@ -382,14 +362,13 @@ class DecoderLM:
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])
 
-    def _dec_tickets(self, work_items: int, waves: int = 1):
+    def _dec_tickets(self, work_items: int):
         """Zeroed int32 tickets for single-pass split decode attention (the kernel resets
         each entry it uses, so one persistent buffer serves every layer and graph replay).
         Sized once, before any capture: split decode only runs below 1024 (work item, kv
         head) waves (engine/runner.py _decode_splits), extend rows at most 4x that.
-        Used by the 4-wave workgroup form (its few partials merge in-kernel) and, with
-        RFQ_SINGLE_PASS_DECODE, by the one-wave form."""
-        if self.device.type != "cuda" or not (self.single_pass or waves > 1):
+        Used where the single-pass merge is on (RFQ_SINGLE_PASS_DECODE)."""
+        if self.device.type != "cuda" or not self.single_pass:
             return None
         if self._tickets is None:
             self._tickets = torch.zeros(4096 * self.hkv, dtype=torch.int32, device=self.device)
@@ -412,29 +391,14 @@ class DecoderLM:
                       torch.empty(D * hq * 2, device=self.device))
         return dec_parts, shared
 
-    def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared,
-                merge: bool = False, qkv=None) -> None:
-        """QKV GEMM + RoPE + paged-KV append, then decode / prefill attention into
-        ``attn`` (rows [0, T) of x and attn; rows past T are SP padding).  ``merge``:
-        the decode attention leaves its split partials in ``dec_parts`` for the o
-        projection (ops.linear_merge) instead of merging them into ``attn``."""
+    def _attend(self, li: int, x, attn, m: ForwardMeta, dec_parts, shared, qkv=None) -> None:
+        """QKV GEMM + RoPE + paged-KV append (unless ``qkv`` comes precomputed, as on the
+        folded-norm path), then decode / prefill attention into ``attn`` (rows [0, T) of x
+        and attn; rows past T are SP padding)."""
         T, D = m.num_tokens, m.num_decode
         hq, hkv = self.hq, self.hkv
         lw = self.w["layers"][li]
         kc, vc = self.kv_k[li], self.kv_v[li]
-        fcfg = self._fused_cfg(m, x, lw["qkv"], shared) if qkv is None else -1
-        if fcfg >= 0:
-            # one launch: QKV GEMV + RoPE + KV append + decode attention (decode_fused.hip)
-            ns = m.decode_splits if dec_parts is not None else 1
-            po, pm = dec_parts if dec_parts is not None else (attn, attn)
-            run_tiles = 1 if T == m.dec_q_len.shape[0] else m.decode_tiles
-            ops.qkv_attn(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc, vc,
-                         hq, hkv, fcfg, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
-                         m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, m.decode_tiles, run_tiles,
-                         attn[:D], po, pm, self.scale, ns, li, self.cfg.n_layers)
-            if ns > 1:
-                ops.attn_decode_merge(po, pm, attn[:D], hq, ns)
-            return
         if qkv is None:
             qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc,
                                vc, hq, hkv)
@@ -446,47 +410,14 @@ class DecoderLM:
         elif D > 0:
             po, pm = dec_parts if dec_parts is not None else (attn, attn)
             ns = m.decode_splits if dec_parts is not None else 1
-            waves = 4 if (DECODE_WG_MERGE and ns >= 4 and ns % 4 == 0) else 1
             ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                             m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
                             hq, hkv, self.scale, ns, m.decode_tiles,
-                            None if merge else self._dec_tickets(m.dec_work_seq.numel(), waves),
-                            waves, reduce=not merge)
+                            self._dec_tickets(m.dec_work_seq.numel()))
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
                              m.pf_kv_len, m.work_seq, m.work_qblk, attn[D:T], hq, hkv,
                              self.scale, m.prefill_qblk)
-
-    def _merge_cfg(self, m: ForwardMeta, x, dec_parts, shared, norm: bool) -> int:
-        """Split-K cfg of the o projection that merges the decode attention's split
-        partials in its prologue (ops.linear_merge), or -1: decode / jump-forward rows
-        only, split attention through the one-wave kernel and the separate merge launch
-        (no tickets, no 4-wave form, no cascade, no fused QKV + attention launch), and a
-        start-up plan entry that measured the fold faster."""
-        T, D = m.num_tokens, m.num_decode
-        if (not x.is_cuda or D == 0 or T != D or T > 16 or dec_parts is None
-                or shared is not None or self.single_pass):
-            return -1
-        ns = m.decode_splits
-        if DECODE_WG_MERGE and ns >= 4 and ns % 4 == 0:
-            return -1
-        if self._fused_cfg(m, x, self.w["layers"][0]["qkv"], shared) >= 0:
-            return -1
-        wo = self.w["layers"][0]["o"]
-        return ops.merge_plan(T, wo.shape[0], wo.shape[1], ns, norm)
-
-    def _fused_cfg(self, m: ForwardMeta, x, w_qkv, shared) -> int:
-        """Split-K cfg for the fused QKV + attention launch, or -1 to run the two
-        launches: decode / jump-forward rows only (no prefill rows in the step, at most
-        16), the split-K rope plan chose a GEMV for this shape, and the work list has one
-        or two column tiles per item."""
-        T, D = m.num_tokens, m.num_decode
-        if (not ops.FUSED_QKV_ATTN or not x.is_cuda or D == 0 or T != D or T > 16
-                or shared is not None or m.decode_tiles not in (1, 2)
-                or m.dec_work_seq is None or self.cfg.n_layers > ops.FUSE_SLOTS
-                or 32 * self.hkv > ops.FUSE_SLOT_WORDS or x.stride(1) != 1 or x.stride(0) % 8):
-            return -1
-        return ops.qkv_attn_cfg(T, w_qkv.shape[0], x.shape[1])
 
     # ------------------------------------------------------------- conveniences
     def weight_bytes(self) -> int:

@@ -304,75 +304,6 @@ def linear_add_norm(x, w, residual, norm_w, eps, out, gated: bool = False) -> bo
     return True
 
 
-# (M, N, K, S, norm) -> split-K GEMV cfg (| SPLITK_BIT) of the o projection that merges
-# the decode attention's S split partials in its prologue (gemv_splitk_merge), filled
-# by autotune.tune_merge where it beat merge launch + planned o path; absent = unfused.
-_MERGE_PLAN: dict[tuple, int] = {}
-MERGE_AM_MAX_S = 16
-MERGE_AM_LDS = 16384
-
-
-def set_merge_plan(plan: dict) -> None:
-    _MERGE_PLAN.clear()
-    _MERGE_PLAN.update(plan)
-
-
-def gemv_merge_fits(M: int, K: int, cfg: int, S: int) -> bool:
-    """Host mirror of gemm_skinny.hip gemv_merge_fits: the slice's merged rows fit the
-    kernel's LDS copy."""
-    KS = 2 << (cfg & 3)
-    nks_all = K // 128
-    nks_max = -(-nks_all // KS)
-    return (1 <= M <= 16 and 2 <= S <= MERGE_AM_MAX_S and K % 128 == 0 and nks_all >= KS
-            and M * nks_max * 128 <= MERGE_AM_LDS and not cfg & SPLITK_PERSIST)
-
-
-def merge_plan(M: int, N: int, K: int, S: int, norm: bool) -> int:
-    return _MERGE_PLAN.get((M, N, K, S, norm), -1) if _MERGE_PLAN else -1
-
-
-def linear_merge(part_o, part_ml, S: int, w, M: int, cfg: int, norm=None) -> torch.Tensor:
-    """y [M, N] = attn . w^T where attn [M, K] is still split into the decode attention's
-    S partials (attn_decode reduce=False): the merge runs in the split-K GEMV's prologue.
-    ``norm`` = (residual, norm_w, eps, out): the residual-add RMSNorm epilogue too."""
-    N, K = w.shape
-    y = torch.empty((M, N), dtype=w.dtype, device=w.device)
-    part, tiles = splitk_ws(w.device)
-    if norm is None:
-        _native.ops().gemv_splitk_merge(part_o, part_ml, S, _wsel(w, cfg), y, part, tiles,
-                                        cfg & 127, None, None, 0.0, None, None)
-    else:
-        residual, norm_w, eps, out = norm
-        _native.ops().gemv_splitk_merge(part_o, part_ml, S, _wsel(w, cfg), y, part, tiles,
-                                        cfg & 127, residual, norm_w, eps, out,
-                                        norm_counter(w.device))
-    return y
-
-
-GEMV_PUSH_MAX_M = 4
-PUSH_DEFAULT_CFG = 8                   # KS 2, 4 waves, U 2 (+ tiled / nt when available)
-
-
-def gemv_push_fits(world: int, M: int, N: int, K: int, cfg: int) -> bool:
-    """Host mirror of csrc/comm/gemv_push.hip gemv_push_fits."""
-    KS = 2 << (cfg & 3)
-    return (1 <= world <= 8 and 1 <= M <= GEMV_PUSH_MAX_M and N % 16 == 0 and N <= 8192
-            and K % 128 == 0 and K // 128 >= KS and not cfg & SPLITK_PERSIST)
-
-
-def push_gemv_cfg(M: int, N: int, K: int, w: torch.Tensor) -> int:
-    """Split-K GEMV cfg (low 7 bits) for the fused GEMV + all-reduce: the linear plan's
-    split-K entry for this shape, else KS 2 / 4 waves / U 2 on the tiled layout with
-    non-temporal loads when the weight has a tiled copy (row-major otherwise); -1 when
-    the weight only exists tiled and no tiled cfg is known."""
-    c = linear_plan(M, N, K) if _LINEAR_PLAN else -1
-    if c >= 0 and c & SPLITK_BIT:
-        return c & 127
-    if tiled_of(w) is not None:
-        return PUSH_DEFAULT_CFG | SPLITK_TILED | SPLITK_NT
-    return -1 if tiled_only(w) else PUSH_DEFAULT_CFG
-
-
 # (M, F, K) -> skinny cfg of the gate|up projection with the SwiGLU epilogue
 # (gemm_skinny.hip SWI: out [M, F] = silu(x Wg^T) * (x Wu^T)), or absent = unfused.
 _SWI_PLAN: dict[tuple[int, int, int], int] = {}
@@ -532,73 +463,9 @@ def qkv_rope(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
     return qkv
 
 
-# Fused QKV + RoPE + KV append + decode attention (decode_fused.hip): one launch per
-# layer instead of the split-K QKV GEMV followed by the decode-attention launch, on
-# steps of <= 16 decode / jump-forward rows with no prefill rows.  Bit-identical to the
-# two launches (tests/kernels test_qkv_attn_fused) but measured SLOWER on MI355X at
-# batch 1 (profiles/r4_fused_qkv_attn.md: the in-launch hand-off -- write-through
-# results, a drained count, a poll, sc1 reads -- costs what the launch boundary plus the
-# attention's metadata chain cost, and holding each tile's last workgroup for its
-# write-through drain delays the QKV grid), so it is off by default:
-# RFQ_FUSED_QKV_ATTN=1 turns it on.
-FUSED_QKV_ATTN = os.environ.get("RFQ_FUSED_QKV_ATTN", "0") == "1"
-FUSE_SLOTS = 128            # per-layer counter slots (>= layers of any model served)
-FUSE_SLOT_WORDS = 256       # Hkv <= 8 counters per slot, one 128-B line each
-
-
-def fuse_ws(device):
-    """(zeroed int32 counter slots [FUSE_SLOTS, 256], int32 timeout counter [4]) of the
-    fused QKV + attention launch; allocated before any graph capture (stable pointers).
-    Slot l belongs to layer l; layer l's launch zeroes slot l - 1 (layer 0 zeroes the
-    last layer's), so every slot is zero when its launch starts."""
-    d = torch.device(device)
-    key = ("fuse", d)
-    ws = _NORM_COUNTERS.get(key)
-    if ws is None:
-        ws = _NORM_COUNTERS[key] = (torch.zeros(FUSE_SLOTS, FUSE_SLOT_WORDS, dtype=torch.int32,
-                                                device=d),
-                                    torch.zeros(4, dtype=torch.int32, device=d))
-    return ws
-
-
-def qkv_attn_cfg(M: int, N: int, K: int) -> int:
-    """The split-K GEMV cfg the fused launch streams the QKV weight with: the rope
-    plan's split-K entry for this shape (8 waves: the fused kernel's attention waves
-    set its occupancy), or -1 when the plan has none."""
-    cfg = rope_plan(M, N, K)
-    if cfg < 0 or not (cfg & SPLITK_BIT):
-        return -1
-    return (cfg & 127) | 4
-
-
-def qkv_attn(x, w, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv, cfg,
-             block_tables, q_start, q_len, kv_len, work_seq, work_ct, list_tpi, run_tiles,
-             out, part_o, part_ml, scale, num_splits, layer: int, num_layers: int):
-    """One launch: qkv = x w^T with NeoX RoPE and the paged KV append, plus the decode
-    attention of the rows [0, out.shape[0]) into ``out`` (num_splits == 1) or into the
-    split partials (merge them with :func:`attn_decode_merge`).  ``layer`` picks the
-    counter slot; the launch zeroes slot ``layer - 1`` (mod ``num_layers``)."""
-    done, err = fuse_ws(x.device)
-    part, tiles = splitk_ws(x.device)
-    qkv = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-    zero = done[(layer - 1) % num_layers] if num_layers > 1 else None
-    _native.ops().qkv_attn(x, _wsel(w, cfg | SPLITK_BIT), qkv, positions, cos_sin, slot_mapping,
-                           k_cache, v_cache, Hq, Hkv, part, tiles, cfg & 127, block_tables,
-                           q_start, q_len, kv_len, work_seq, work_ct, list_tpi, run_tiles, out,
-                           part_o, part_ml, scale, num_splits, done[layer], zero, err)
-    return qkv
-
-
 def attn_decode_merge(part_o, part_ml, out, Hq, num_splits):
     """Merge split-K decode-attention partials into bf16 rows of ``out``."""
     _native.ops().attn_decode_merge(part_o, part_ml, out, Hq, num_splits)
-
-
-def fuse_errors(device) -> int:
-    """Wait timeouts the fused QKV + attention launch counted (0 = all hand-offs met)."""
-    key = ("fuse", torch.device(device))
-    ws = _NORM_COUNTERS.get(key)
-    return int(ws[1][0].item()) if ws is not None else 0
 
 
 # (N, K) -> (quantum q, table) where table[j] is the row-chunk split (in units of q
@@ -827,20 +694,18 @@ def rope_kv(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, Hq, Hkv):
 
 def attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, work_seq, work_ct,
                 out, part_o, part_ml, Hq, Hkv, scale, num_splits=1, tiles_per_item=1,
-                tickets=None, waves: int = 1, reduce: bool = True):
+                tickets=None, reduce: bool = True):
     """Paged attention for decode / short-extend rows (see csrc/kernels/attn_decode.hip).
     A work item (work_seq[w], work_ct[w]) covers column tiles
     [work_ct*tiles_per_item, +tiles_per_item) of its sequence's q_len*G (query, head) pairs.
     With num_splits > 1, ``tickets`` (int32 zeros, >= work items * Hkv, reset by the kernel)
     makes it single-pass: the last split to finish merges the partials in-kernel.
-    ``waves`` = 4 (num_splits % 4 == 0): four splits per workgroup merged through LDS,
-    so only num_splits / 4 partials reach the in-kernel (or reduce-launch) merge.
     ``reduce=False`` (num_splits > 1, no tickets): the split partials are left in
-    part_o / part_ml for the o projection to merge (:func:`linear_merge`)."""
+    part_o / part_ml (merge them with :func:`attn_decode_merge`)."""
     if _gpu(q):
         _native.ops().attn_decode(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len,
                                   work_seq, work_ct, out, part_o, part_ml, Hq, Hkv, scale,
-                                  num_splits, tiles_per_item, tickets, waves, reduce)
+                                  num_splits, tiles_per_item, tickets, reduce)
     else:
         ref.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_len, kv_len, None, None,
                          out, Hq, Hkv, scale)
@@ -1051,7 +916,7 @@ def moe_combine(y, inv_pos, weights, topk, out):
 def reset_plans() -> None:
     """Forget every start-up plan (tests that build bare models after an engine: the
     plans are keyed by shape and may name a decode-tiled copy the new weights lack)."""
-    for d in (_LINEAR_PLAN, _SILU_PLAN, _NORM_PLAN, _MERGE_PLAN, _SWI_PLAN, _ROWS_BEST,
+    for d in (_LINEAR_PLAN, _SILU_PLAN, _NORM_PLAN, _SWI_PLAN, _ROWS_BEST,
               _ROPE_PLAN, _SPLIT_PLAN):
         d.clear()
     _TUNED_MS.clear()

@@ -17,7 +17,7 @@ import torch
 
 from . import (ROWS_BIT, ROWS_CFGS, ROWS_CFGS_PAIRED, SPLITK_BIT, SPLITK_CFGS, SPLITK_NT,
                SPLITK_TILED, _native, _wsel, gemm_dense_ok, gemm_w4_ok, rows_ok, set_rows_best,
-               set_linear_plan, set_merge_plan, set_norm_plan, set_rope_plan, set_silu_plan,
+               set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan,
                set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
                tiled_only)
@@ -260,66 +260,6 @@ def decode_splits_for(rows: int, hkv: int) -> int:
     while rows * hkv * s < 1024 and s < 16:
         s *= 2
     return s
-
-
-def tune_merge(ws: list[torch.Tensor], ms: list[int], hq: int, hkv: int, norm_w, reps: int = 2,
-               margin: float = 0.98, eps: float = 1e-5):
-    """o projection on split decode-attention partials: attn_decode_merge + the planned
-    o path (linear, or linear_add_norm when ``norm_w`` is given, TP = 1) vs the split-K
-    GEMV that merges the partials in its prologue (gemv_splitk_merge, one launch fewer
-    per layer).  Plan key (M, N, K, S, norm) with S the graphs' split count for M rows."""
-    from . import (NORM_FUSE_MAX_M, fused_add_rms_norm, gemv_merge_fits, linear,
-                   linear_add_norm, norm_counter)
-
-    ops = _native.ops()
-    N, K = ws[0].shape
-    plan, report = {}, []
-    if K != hq * 128 or N % 16 or (norm_w is not None and N > 8192):
-        return plan, report
-    dev, dt = ws[0].device, ws[0].dtype
-    part, tiles = splitk_ws(dev)
-    norm = norm_w is not None
-    for M in ms:
-        if M > NORM_FUSE_MAX_M:
-            continue
-        S = decode_splits_for(M, hkv)
-        if S < 2:
-            continue
-        po = torch.randn(M * hq * S * 128, device=dev)
-        ml = torch.rand(M * hq * S * 2, device=dev) + 0.5
-        attn = torch.empty(M, K, device=dev, dtype=dt)
-        y = torch.empty(M, N, device=dev, dtype=dt)
-        res = torch.randn(M, N, device=dev, dtype=dt)
-        out = torch.empty(M, N, device=dev, dtype=dt)
-
-        def ref(w):
-            ops.attn_decode_merge(po, ml, attn, hq, S)
-            if not norm:
-                linear(attn, w, out=y)
-            elif not linear_add_norm(attn, w, res, norm_w, eps, out):
-                linear(attn, w, out=y)
-                fused_add_rms_norm(y, res, norm_w, eps, out=out)
-
-        t_ref = _time(ref, ws, reps)
-        best, t_best = -1, t_ref * margin
-        for c in _splitk_cands(ws, (8, 9, 12, 13, 4, 5, 0, 1)):
-            if not gemv_merge_fits(M, K, c, S):
-                continue
-            if norm:
-                fn = (lambda w, c=c: ops.gemv_splitk_merge(po, ml, S, _wsel(w, c), y, part, tiles,
-                                                           c, res, norm_w, eps, out,
-                                                           norm_counter(dev)))
-            else:
-                fn = (lambda w, c=c: ops.gemv_splitk_merge(po, ml, S, _wsel(w, c), y, part, tiles,
-                                                           c, None, None, 0.0, None, None))
-            t = _time(fn, ws, reps)
-            if t < t_best:
-                best, t_best = c | SPLITK_BIT, t
-        if best >= 0:
-            plan[(M, N, K, S, norm)] = best
-        report.append(("merge+o+norm" if norm else "merge+o", M, N, K, round(t_ref, 1), best,
-                       round(min(t_best, t_ref), 1)))
-    return plan, report
 
 
 def tune_swiglu(ws: list[torch.Tensor], ms: list[int], reps: int = 2, margin: float = 0.97):
@@ -648,16 +588,6 @@ def tune_model(model, ms: list[int], lm_ms: list[int], max_tokens: int = 0,
             nreport += [("down(act)+norm",) + tuple(r[1:]) for r in r3]
         set_norm_plan(nplan)
         report += nreport
-    if os.environ.get("RFQ_FUSE_ATTN_MERGE", "0") == "1" and hasattr(model, "hq"):
-        # after the norm plan: the reference path is the planned o (+ norm) launch.  Off
-        # by default: every o tile re-reads its heads' S split partials (S x the merged
-        # row), which cost more than the merge launch it saves
-        # (profiles/r4_attn_merge_fold.md); RFQ_FUSE_ATTN_MERGE=1 tunes it anyway
-        tp_on = tp is not None and tp.enabled
-        norm_w = None if tp_on else w["layers"][0]["mlp_norm"]
-        mplan, mreport = tune_merge(groups["o"], ms, model.hq, model.hkv, norm_w)
-        set_merge_plan(mplan)
-        report += mreport
     if max_tokens > 0:
         mm = {k: max_tokens for k in groups}
         mm["lm_head"] = max_seqs

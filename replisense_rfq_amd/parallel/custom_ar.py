@@ -31,13 +31,6 @@ FUSE_NORM = os.environ.get("RFQ_CAR_NORM", "1") != "0"
 # decode rows, staged above; 1 = always the staged one-shot (flag, remote read, end flag)
 CAR_NORM_ALGO = 1 if os.environ.get("RFQ_CAR_PUSH", "1") == "0" else 0
 
-# RFQ_GEMV_PUSH=1: the row-parallel o / down GEMV pushes its rows into the peers' slots and
-# runs the all-reduce + norm in its own last workgroup (linear_add_norm_).  Off by default:
-# bit-identical at world 2/4/8, but measured slower than the GEMV followed by the push
-# kernel (16 -> 21 µs for the TP=8 o projection at one row, profiles/r4_gemv_push.md): the
-# last workgroup's chain of dependent round trips (ticket, counter, flag, remote slots)
-# costs more than the launch boundary it removes.
-GEMV_PUSH = os.environ.get("RFQ_GEMV_PUSH", "0") == "1"
 
 class CustomAllReduce:
     def __init__(self, rank: int, world: int, group=None, capacity_bytes: int = 8 << 20):
@@ -114,32 +107,6 @@ class CustomAllReduce:
                                                  CAR_NORM_ALGO if algo is None else algo)
         self.calls += 1
         return out
-
-    def linear_add_norm_(self, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
-                         norm_w: torch.Tensor, eps: float, out: torch.Tensor) -> bool:
-        """The row-parallel projection, its all-reduce and the residual-add RMSNorm in ONE
-        launch (csrc/comm/gemv_push.hip: the split-K GEMV pushes its rows into every
-        rank's slots, its last workgroup sums and normalises; bit-identical to
-        ``linear`` + :meth:`all_reduce_add_norm_` with the push form).  Returns False
-        (nothing done) when the call does not fit: GEMV_PUSH off, more than 4 rows, a
-        shape or layout the kernel does not take."""
-        if not GEMV_PUSH or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1:
-            return False
-        from .. import ops
-
-        M, K = x.shape
-        N = w.shape[0]
-        cfg = ops.push_gemv_cfg(M, N, K, w)
-        if cfg < 0 or not ops.gemv_push_fits(len(self.bases), M, N, K, cfg) \
-                or tuple(residual.shape) != (M, N) or tuple(out.shape) != (M, N) \
-                or x.stride(0) % 8:
-            return False
-        part, tiles = ops.splitk_ws(x.device)
-        torch.ops.rfq_amd.gemv_push_norm(x, ops._wsel(w, cfg), part, tiles, cfg, residual,
-                                         norm_w, eps, out, ops.norm_counter(x.device),
-                                         self.bases, self.rank, self.capacity)
-        self.calls += 1
-        return True
 
     def errors(self) -> int:
         return int(_native.ops().car_error(self.ptr))

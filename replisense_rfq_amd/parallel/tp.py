@@ -59,15 +59,6 @@ class TPContext:
         self.all_reduce_(t)
         return ops.fused_add_rms_norm(t, residual, w, eps, out=out)
 
-    def linear_add_norm_(self, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
-                         norm_w: torch.Tensor, eps: float, out: torch.Tensor) -> bool:
-        """Row-parallel projection + all-reduce + residual-add RMSNorm in one launch on
-        the custom xGMI path (CustomAllReduce.linear_add_norm_, RFQ_GEMV_PUSH=1); False
-        = not taken, the caller runs linear + all_reduce_add_norm_."""
-        if self.world > 1 and self.car is not None:
-            return self.car.linear_add_norm_(x, w, residual, norm_w, eps, out)
-        return False
-
     def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
         """Switch all-reduces up to ``capacity_bytes`` to the xGMI one-/two-shot kernels
         (GPU groups only).  A start-up self-test runs both algorithms against the known
@@ -187,9 +178,6 @@ class EmulatedTP(TPContext):
 
     def enable_custom_allreduce(self, capacity_bytes: int = 8 << 20) -> bool:
         self.car_status = "emulated (collectives skipped)"
-        return False
-
-    def linear_add_norm_(self, x, w, residual, norm_w, eps, out) -> bool:
         return False
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:

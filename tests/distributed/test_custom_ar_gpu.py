@@ -108,36 +108,6 @@ def _worker(rank, world, port, q):
                 torch.cuda.synchronize()
                 (ra, oa), (rb, ob) = outs
                 errs.append(0.0 if (torch.equal(ra, rb) and torch.equal(oa, ob)) else 98.0)
-        # the row-parallel GEMV with the push all-reduce + norm in its own launch
-        # (gemv_push.hip) is bit identical to gemv_splitk followed by the push kernel;
-        # calls alternate with the standalone push form on the same row counters, and the
-        # norm ticket and tile tickets are left at zero
-        part, tiles = ops.splitk_ws(torch.device("cuda"))
-        cnt = ops.norm_counter(torch.device("cuda"))
-        for M, N, K in ((1, 8192, 1024), (2, 8192, 3584), (4, 4096, 2048)):
-            g = torch.Generator(device="cuda").manual_seed(M * 31 + K + rank)
-            wr = ((torch.rand(N, K, generator=g, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
-            wt = ops.tile_weight(wr)
-            for cfg in (8, 9, 12, 8 | 16 | 32, 13 | 16):
-                ww = wt if cfg & 16 else wr
-                for it in range(3):
-                    g2 = torch.Generator(device="cuda").manual_seed(M * 7 + cfg * 13 + it)
-                    xs = [torch.randn(M, K, generator=g2, device="cuda").to(torch.bfloat16)
-                          for _ in range(world)]
-                    resid = torch.randn(M, N, generator=g2, device="cuda").to(torch.bfloat16)
-                    nw = (1 + 0.1 * torch.randn(N, generator=g2, device="cuda")).to(torch.bfloat16)
-                    x = xs[rank]
-                    r1, o1 = resid.clone(), torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-                    torch.ops.rfq_amd.gemv_push_norm(x, ww, part, tiles, cfg, r1, nw, 1e-5, o1,
-                                                     cnt, car.bases, car.rank, car.capacity)
-                    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-                    torch.ops.rfq_amd.gemv_splitk(x, ww, y, part, tiles, cfg)
-                    r2, o2 = resid.clone(), torch.empty_like(o1)
-                    car.all_reduce_add_norm_(y, r2, nw, 1e-5, o2, algo=2)
-                    torch.cuda.synchronize()
-                    errs.append(0.0 if (torch.equal(r1, r2) and torch.equal(o1, o2)) else 97.0)
-        torch.cuda.synchronize()
-        errs.append(0.0 if int(cnt[0]) == 0 and int(tiles.abs().sum()) == 0 else 96.0)
         dist.barrier()
         # ... and inside a captured graph, replayed with fresh inputs (the default form
         # for 4 decode rows is the push kernel)

@@ -77,10 +77,8 @@ def test_split_linear_equals_one_gemm(monkeypatch):
     assert list(itertools.accumulate(rows))[-1] == 77
 
 
-def test_merge_plan_keys_match_runner_splits():
-    """The merge-fold plan is keyed by the split count the decode graphs use: the tuner's
-    copy of the rule equals ModelRunner._decode_splits(graph=True); the host shape rule
-    mirrors the kernel's LDS bound."""
+def test_decode_splits_rule_matches_runner():
+    """The tuner's copy of the decode split rule equals ModelRunner._decode_splits(graph=True)."""
     from types import SimpleNamespace
 
     from replisense_rfq_amd.engine.runner import ModelRunner
@@ -91,18 +89,6 @@ def test_merge_plan_keys_match_runner_splits():
         for rows in (1, 2, 4, 8, 16, 64, 200):
             assert decode_splits_for(rows, hkv) == ModelRunner._decode_splits(fake, rows, 4096,
                                                                              True)
-    # TP=8 o (K 1024): KS 2 -> 4 heads per slice
-    assert ops.gemv_merge_fits(16, 1024, 0, 16)
-    assert not ops.gemv_merge_fits(16, 1024, 0, 32)          # S > 16
-    assert not ops.gemv_merge_fits(16, 8192, 0, 16)          # 32 heads x 16 rows > 32 KB
-    assert ops.gemv_merge_fits(16, 8192, 2, 16)              # KS 8: 8 heads x 16 rows
-    assert not ops.gemv_merge_fits(1, 4096, 16 | 64, 16)     # persistent grid
-    ops.set_merge_plan({(1, 4096, 4096, 16, True): 128 | 8})
-    try:
-        assert ops.merge_plan(1, 4096, 4096, 16, True) == 128 | 8
-        assert ops.merge_plan(1, 4096, 4096, 16, False) == -1
-    finally:
-        ops.set_merge_plan({})
 
 
 def test_plan_hybrid_whole_rounds():

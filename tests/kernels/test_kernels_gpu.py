@@ -155,53 +155,6 @@ def test_attn_decode(gpu, Hq, Hkv, splits, single, tiles):
     _close(out, exp, 2e-2, 0, f"attn_decode Hq={Hq} splits={splits} tiles={tiles}")
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
-@pytest.mark.parametrize("splits", [4, 8, 16])
-@pytest.mark.parametrize("tiles", [1, 2])
-@pytest.mark.parametrize("tickets_on", [True, False])
-@pytest.mark.parametrize("waves", [4, 8])
-def test_attn_decode_wg_merge(gpu, Hq, Hkv, splits, tiles, tickets_on, waves):
-    """4- / 8-wave workgroups (one split per wave, LDS merge): vs the fp32 oracle, decode and
-    extend rows, contexts shorter than the split count (empty splits), a padding work
-    item; the workgroups' partials merged in-kernel (tickets, reset after every launch)
-    or by the reduce launch."""
-    if splits % waves:
-        pytest.skip("splits must be a multiple of the workgroup's waves")
-    torch.manual_seed(7 + splits)
-    G = Hq // Hkv
-    cases = [(1, 1), (1, 31), (1, 33), (1, 700), (5, 129), (9, 2049), (3, 3), (1, 1100)]
-    qlens = [c[0] for c in cases]
-    kvlens = [c[1] for c in cases]
-    k, v = _paged_cache(512, Hkv, gpu, seed=9)
-    bt = _block_tables(kvlens, 512, gpu)
-    T = sum(qlens)
-    qs = [sum(qlens[:i]) for i in range(len(qlens))]
-    ws, wct = [], []
-    for i, ql in enumerate(qlens):
-        for ct in range(((ql * G + 15) // 16 + tiles - 1) // tiles):
-            ws.append(i)
-            wct.append(ct)
-    ws.append(-1)
-    wct.append(0)
-    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
-    q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
-    po = torch.empty(T * Hq * splits * 128, device=gpu)
-    pm = torch.empty(T * Hq * splits * 2, device=gpu)
-    scale = 1 / math.sqrt(128)
-    tickets = torch.zeros(len(ws) * Hkv, dtype=torch.int32, device=gpu) if tickets_on else None
-    exp = torch.zeros(T, Hq * 128, dtype=BF)
-    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), torch.tensor(qs), torch.tensor(qlens),
-                     torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
-    for it in range(3):
-        out = torch.full((T, Hq * 128), float("nan"), device=gpu, dtype=BF)
-        ops.attn_decode(q, k, v, bt, i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct), out,
-                        po, pm, Hq, Hkv, scale, splits, tiles, tickets, waves)
-        torch.cuda.synchronize()
-        if tickets is not None:
-            assert int(tickets.abs().sum()) == 0, "tickets not reset"
-        _close(out, exp, 2e-2, 0, f"wg-merge Hq={Hq} splits={splits} tiles={tiles} it={it}")
-
-
 @pytest.mark.parametrize("Hq,Hkv,tiles", [(32, 8, 1), (32, 8, 2), (8, 1, 1)])
 @pytest.mark.parametrize("share", [True, False])
 def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
@@ -736,64 +689,6 @@ def test_gemv_splitk(gpu, M, cfg, N, K):
 
 
 @pytest.mark.parametrize("M", [1, 3, 16])
-@pytest.mark.parametrize("S", [2, 8, 16])
-@pytest.mark.parametrize("cfg", [0, 1, 9, 13 | 16 | 32, 14 | 16])
-@pytest.mark.parametrize("Hq,N", [(8, 8192), (32, 4096)])
-def test_gemv_splitk_merge(gpu, M, S, cfg, Hq, N):
-    """o projection with the decode attention's split merge as its prologue
-    (gemv_splitk_merge) == attn_decode_merge followed by gemv_splitk, bit for bit (plain
-    and residual-add RMSNorm epilogues, row-major and tiled weights, splits with no keys
-    (m = -inf)); the merged rows vs an fp32 merge; tickets and the norm counter left at
-    zero over repeated launches."""
-    K = Hq * 128
-    if not ops.gemv_merge_fits(M, K, cfg, S):
-        pytest.skip("slice rows exceed the LDS copy")
-    torch.manual_seed(M * 31 + S + cfg + Hq)
-    po = torch.randn(M, Hq, S, 128, device=gpu)
-    ml = torch.empty(M, Hq, S, 2, device=gpu)
-    ml[..., 0] = torch.randn(M, Hq, S, device=gpu) * 4
-    ml[..., 1] = torch.rand(M, Hq, S, device=gpu) * 30 + 0.5
-    empty = torch.rand(M, Hq, S, device=gpu) < 0.2
-    ml[..., 0][empty] = float("-inf")
-    ml[..., 1][empty] = 0.0
-    ml[0, 0, :, 0] = float("-inf")                      # a head with no keys at all -> 0
-    ml[0, 0, :, 1] = 0.0
-    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
-    ww = ops.tile_weight(w) if cfg & ops.SPLITK_TILED else w
-    part, tiles = ops.splitk_ws(gpu)
-    attn = torch.empty(M, K, device=gpu, dtype=BF)
-    torch.ops.rfq_amd.attn_decode_merge(po, ml, attn, Hq, S)
-    # fp32 merge oracle for the rows the prologue builds
-    m = ml[..., 0]
-    gm = m.amax(-1, keepdim=True)
-    wgt = torch.where(m == float("-inf"), torch.zeros_like(m), torch.exp2(m - gm))
-    wgt = torch.nan_to_num(wgt)
-    den = (wgt * ml[..., 1]).sum(-1)
-    num = (wgt[..., None] * po).sum(-2)
-    want_attn = torch.where(den[..., None] > 0, num / den.clamp_min(1e-30)[..., None],
-                            torch.zeros_like(num)).reshape(M, K)
-    _close(attn, want_attn, 2e-2, 1e-2, "merge oracle")
-    y0, y1 = (torch.empty(M, N, device=gpu, dtype=BF) for _ in range(2))
-    torch.ops.rfq_amd.gemv_splitk(attn, ww, y0, part, tiles, cfg)
-    for it in range(3):
-        y1.fill_(float("nan"))
-        torch.ops.rfq_amd.gemv_splitk_merge(po, ml, S, ww, y1, part, tiles, cfg, None, None, 0.0,
-                                            None, None)
-        assert torch.equal(y0, y1), f"plain it={it}"
-    nw = (1 + 0.1 * torch.randn(N, device=gpu)).to(BF)
-    res = torch.randn(M, N, device=gpu, dtype=BF)
-    counter = torch.zeros(4, dtype=torch.int32, device=gpu)
-    r0, r1 = res.clone(), res.clone()
-    o0, o1 = (torch.empty(M, N, device=gpu, dtype=BF) for _ in range(2))
-    torch.ops.rfq_amd.gemv_splitk_norm(attn, ww, y0, r0, nw, 1e-5, o0, counter, part, tiles, cfg)
-    torch.ops.rfq_amd.gemv_splitk_merge(po, ml, S, ww, y1, part, tiles, cfg, r1, nw, 1e-5, o1,
-                                        counter)
-    assert torch.equal(r0, r1) and torch.equal(o0, o1), "norm epilogue"
-    torch.cuda.synchronize()
-    assert int(tiles.abs().sum()) == 0 and int(counter[0]) == 0
-
-
-@pytest.mark.parametrize("M", [1, 3, 16])
 @pytest.mark.parametrize("cfg", [0, 2, 9, 13, 14])
 @pytest.mark.parametrize("F,K", [(3584, 8192), (512, 1024)])
 def test_gemv_splitk_swiglu(gpu, M, cfg, F, K):
@@ -1020,95 +915,6 @@ def test_moe_gemm_dense(gpu, T, swiglu):
         _close(out[a:b], r, atol=2e-2, rtol=2e-2, what=f"expert {e} rows {a}:{b}")
     if off[E] < cap:                                       # rows past the live segments
         assert bool((out[off[E]:].float() == 7.0).all())
-
-
-@pytest.mark.parametrize("Hq,Hkv,K", [(32, 8, 1024), (8, 1, 8192), (64, 8, 1024)])
-@pytest.mark.parametrize("cfg", [4, 1 | 4, 8 | 4, 2 | 8 | 4, 16 | 32 | 8 | 4])
-@pytest.mark.parametrize("splits", [1, 4, 16])
-def test_qkv_attn_fused(gpu, Hq, Hkv, K, cfg, splits):
-    """The fused QKV + RoPE + KV append + decode attention launch (decode_fused.hip) ==
-    the two launches it replaces (split-K rope GEMV, then attn_decode) bit for bit --
-    same GEMV arithmetic, same attention arithmetic on q / new KV rows read back with
-    sc1 loads -- over decode rows and extend rows whose new tokens start mid-page, end a
-    page or open a new one, plus a padding work item; and close to the fp32 oracle.
-    Three layers in a row: every launch zeroes the previous layer's counter slot, no
-    wait times out."""
-    torch.manual_seed(Hq * 7 + splits + cfg)
-    G = Hq // Hkv
-    tiles = 2
-    cases = [(1, 700), (1, 33), (1, 32), (5, 129), (3, 3), (1, 1), (2, 64)]
-    qlens = [c[0] for c in cases]
-    kvlens = [c[1] for c in cases]
-    T = sum(qlens)
-    N = (Hq + 2 * Hkv) * 128
-    nblk = 128
-    k0, v0 = _paged_cache(nblk, Hkv, gpu, seed=9)
-    bt = _block_tables(kvlens, nblk, gpu, seed=3)
-    btc = bt.cpu()
-    pos, slots = [], []
-    for b, (ql, kl) in enumerate(cases):
-        for i in range(ql):
-            p = kl - ql + i
-            pos.append(p)
-            slots.append(int(btc[b, p // 32]) * 32 + p % 32)
-    qs = [sum(qlens[:i]) for i in range(len(qlens))]
-    ws, wct = [], []
-    for i, ql in enumerate(qlens):
-        for ct in range(((ql * G + 15) // 16 + tiles - 1) // tiles):
-            ws.append(i)
-            wct.append(ct)
-    ws.append(-1)
-    wct.append(0)
-    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=gpu)  # noqa: E731
-    pos_t, slots_t = i32(pos), i32(slots)
-    qs_t, ql_t, kl_t, ws_t, wct_t = i32(qs), i32(qlens), i32(kvlens), i32(ws), i32(wct)
-    x = torch.randn(T, K, device=gpu, dtype=BF)
-    w = (torch.randn(N, K, device=gpu) / math.sqrt(K)).to(BF)
-    if cfg & ops.SPLITK_TILED:
-        ops.register_tiled(w, ops.tile_weight(w))
-    cs = ref.rope_cos_sin(4096, 128, 500000.0, device=gpu)
-    scale = 1 / math.sqrt(128)
-    part, tls = ops.splitk_ws(gpu)
-    # the two-launch reference
-    k1, v1 = k0.clone(), v0.clone()
-    qkv1 = torch.empty(T, N, device=gpu, dtype=BF)
-    torch.ops.rfq_amd.gemv_splitk_rope(x, ops._wsel(w, cfg), qkv1, pos_t, cs, slots_t, k1, v1,
-                                       Hq, Hkv, part, tls, cfg)
-    out1 = torch.empty(T, Hq * 128, device=gpu, dtype=BF)
-    po = torch.empty(T * Hq * splits * 128, device=gpu)
-    pm = torch.empty(T * Hq * splits * 2, device=gpu)
-    ops.attn_decode(qkv1, k1, v1, bt, qs_t, ql_t, kl_t, ws_t, wct_t, out1, po, pm, Hq, Hkv,
-                    scale, splits, tiles)
-    done, err = ops.fuse_ws(gpu)
-    done.zero_()
-    err.zero_()
-    L = 3
-    for layer in (0, 1, 2, 0):
-        k2, v2 = k0.clone(), v0.clone()
-        out2 = torch.full((T, Hq * 128), float("nan"), device=gpu, dtype=BF)
-        po2 = torch.full_like(po, float("nan"))
-        pm2 = torch.full_like(pm, float("nan"))
-        qkv2 = ops.qkv_attn(x, w, pos_t, cs, slots_t, k2, v2, Hq, Hkv, cfg, bt, qs_t, ql_t, kl_t,
-                            ws_t, wct_t, tiles, tiles, out2, po2, pm2, scale, splits, layer, L)
-        if splits > 1:
-            ops.attn_decode_merge(po2, pm2, out2, Hq, splits)
-        torch.cuda.synchronize()
-        assert int(err[0]) == 0, "fused wait timed out"
-        assert torch.equal(qkv2[:, :Hq * 128], qkv1[:, :Hq * 128]), f"q layer={layer}"
-        assert torch.equal(k2, k1) and torch.equal(v2, v1), f"kv cache layer={layer}"
-        assert torch.equal(out2, out1), f"attention out layer={layer} splits={splits}"
-        prev = (layer - 1) % L
-        assert int(done[prev].abs().sum()) == 0, "previous layer's slot not zeroed"
-        assert done[layer][::32][:Hkv].tolist() == [(G + 2) * 4] * Hkv
-    assert int(tls.abs().sum()) == 0
-    # the fp32 oracle (q / k RoPE'd, paged attention)
-    exp_qkv = (x.float() @ w.float().t()).cpu()
-    kc_e, vc_e = k0.float().cpu(), v0.float().cpu()
-    ref.rope_kv(exp_qkv, pos_t.cpu(), cs.cpu(), slots_t.cpu(), kc_e, vc_e, Hq, Hkv)
-    exp = torch.zeros(T, Hq * 128)
-    ref.attn_prefill(exp_qkv[:, :Hq * 128].contiguous(), kc_e, vc_e, btc, torch.tensor(qs),
-                     torch.tensor(qlens), torch.tensor(kvlens), None, None, exp, Hq, Hkv, scale)
-    _close(out1, exp, 3e-2, 0, f"fused attention vs fp32 Hq={Hq} splits={splits}")
 
 
 ROWS_CFGS_PLAIN = (0 | 4, 0 | 8, 0 | 12, 1 | 4, 1 | 8, 2 | 0, 2 | 4, 3 | 0)   # (RW, CU) pairs

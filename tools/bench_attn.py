@@ -118,7 +118,7 @@ def run_cascade(B, C, P, Hq=32, Hkv=8, q=1, tiles=2, iters=20):
     return min(res[0], res[2]), min(res[1], res[3]), diff
 
 
-def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1, single=False):
+def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, single=False):
     """Batch-1 decode attention as the latency path runs it: L layers with their own
     KV caches, the L (split kernel [+ reduce]) launches captured in one hipGraph;
     returns µs per layer."""
@@ -138,13 +138,12 @@ def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, waves=1, single=Fals
     out = torch.empty_like(qt)
     po = torch.empty(Hq * splits * 128, device=dev)
     pm = torch.empty(Hq * splits * 2, device=dev)
-    tickets = (torch.zeros(items * Hkv, dtype=torch.int32, device=dev)
-               if (waves > 1 or single) else None)
+    tickets = torch.zeros(items * Hkv, dtype=torch.int32, device=dev) if single else None
 
     def body():
         for k, v in zip(ks, vs):
             ops.attn_decode(qt, k, v, bt, qs, ql, kvl, ws, wct, out, po, pm, Hq, Hkv,
-                            1 / math.sqrt(128), splits, tiles, tickets, waves)
+                            1 / math.sqrt(128), splits, tiles, tickets)
 
     body()
     torch.cuda.synchronize()
@@ -200,29 +199,6 @@ def main():
             for sp in (8, 16, 32):
                 row[f"s{sp}_us"] = round(run_latency(C, 8, 1, sp, L=80), 2)
             print(json.dumps(row), flush=True)
-        return
-    if os.environ.get("LAT_WG"):
-        # one split per wave (+ reduce launch) vs 4-wave workgroups merged in LDS with the
-        # in-kernel merge of the workgroups' partials; batch-1, 8B / 70B-TP1 / 70B-TP8 heads
-        for Hq, Hkv, L in ((32, 8, 32), (64, 8, 80), (8, 1, 80)):
-            for C in (512, 1024, 2048):
-                row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
-                for sp in (8, 16, 32):
-                    row[f"s{sp}_w1_us"] = round(run_latency(C, Hq, Hkv, sp, L=L), 2)
-                    row[f"s{sp}_w4_us"] = round(run_latency(C, Hq, Hkv, sp, L=L, waves=4), 2)
-                print(json.dumps(row), flush=True)
-        return
-    if os.environ.get("LAT_W8"):
-        # one split per wave + the reduce launch (default) vs 8-wave workgroups merged in
-        # LDS: s8 w8 = ONE workgroup per kv head, no cross-workgroup merge at all
-        for Hq, Hkv, L in ((32, 8, 32), (64, 8, 80), (8, 1, 80)):
-            for C in (512, 1024, 2048, 3072):
-                row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
-                row["s16_w1_us"] = round(run_latency(C, Hq, Hkv, 16, L=L), 2)
-                row["s8_w8_us"] = round(run_latency(C, Hq, Hkv, 8, L=L, waves=8), 2)
-                row["s16_w8_us"] = round(run_latency(C, Hq, Hkv, 16, L=L, waves=8), 2)
-                row["s32_w8_us"] = round(run_latency(C, Hq, Hkv, 32, L=L, waves=8), 2)
-                print(json.dumps(row), flush=True)
         return
     if os.environ.get("CASCADE"):
         # the headline's operating point: ~1,536 decode rows, 407-token shared prompt

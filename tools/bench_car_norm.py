@@ -59,39 +59,6 @@ def _worker(rank, world, port, rows_list, q):
 
     car = CustomAllReduce(rank, world, None, capacity_bytes=4 << 20)
     out = []
-    if rows_list == ["gemv"]:
-        # row-parallel GEMV + push all-reduce + norm: two launches vs one (gemv_push.hip)
-        part, tiles = ops.splitk_ws(torch.device("cuda"))
-        cnt = ops.norm_counter(torch.device("cuda"))
-        for name, N, K in (("tp8 o", 8192, 1024), ("tp8 down", 8192, 3584)):
-            w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
-            wt = ops.tile_weight(w)
-            for M in (1, 4):
-                x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-                r = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
-                o = torch.empty_like(r)
-                y = torch.empty_like(r)
-                nw = torch.ones(N, device="cuda", dtype=torch.bfloat16)
-                for cfg in (8 | 16 | 32, 9 | 16 | 32, 12 | 16 | 32):
-                    def gemv(cfg=cfg):
-                        torch.ops.rfq_amd.gemv_splitk(x, wt, y, part, tiles, cfg)
-
-                    def two(cfg=cfg):
-                        torch.ops.rfq_amd.gemv_splitk(x, wt, y, part, tiles, cfg)
-                        car.all_reduce_add_norm_(y, r, nw, 1e-5, o, algo=2)
-
-                    def fused(cfg=cfg):
-                        torch.ops.rfq_amd.gemv_push_norm(x, wt, part, tiles, cfg, r, nw, 1e-5,
-                                                         o, cnt, car.bases, car.rank,
-                                                         car.capacity)
-
-                    out.append((name, M, cfg, _time_graph(gemv, dist), _time_graph(two, dist),
-                                _time_graph(fused, dist)))
-        q.put((rank, out, car.errors()))
-        dist.barrier()
-        car.close()
-        dist.destroy_process_group()
-        return
     for rows in rows_list:
         d = 8192
         t = torch.randn(rows, d, device="cuda").to(torch.bfloat16)
@@ -119,10 +86,7 @@ def _worker(rank, world, port, rows_list, q):
 
 def main():
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-    if sys.argv[2:] == ["gemv"]:
-        rows_list = ["gemv"]
-    else:
-        rows_list = [int(x) for x in sys.argv[2:]] or [1, 4, 8, 16, 32]
+    rows_list = [int(x) for x in sys.argv[2:]] or [1, 4, 8, 16, 32]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -134,15 +98,6 @@ def main():
     for p in procs:
         p.join(timeout=60)
     res.sort(key=lambda r: r[0])
-    if rows_list == ["gemv"]:
-        print(f"world {world} (ranks share one GPU), us per call; flag timeouts "
-              f"{[e for _, _, e in res]}")
-        print("| shape | M | split-K cfg | GEMV alone | GEMV + push all-reduce + norm (2 launches) "
-              "| fused (gemv_push_norm, 1 launch) |")
-        print("|---|---|---|---|---|---|")
-        for name, M, cfg, g1, two, fused in res[0][1]:
-            print(f"| {name} | {M} | {cfg} | {g1:.2f} | {two:.2f} | {fused:.2f} |")
-        return
     print(f"world {world} (ranks share one GPU), d 8192, us per call; flag timeouts "
           f"{[e for _, _, e in res]}")
     print("| rows | all-reduce + add-norm (2 launches) | fused staged (flag, remote read, "

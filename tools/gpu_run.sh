@@ -71,20 +71,6 @@ for task in "$@"; do
         --latency-runs 0 --phases none
       python3 tools/trace_window_stats.py gpurun_out/prof_tput 6 > gpurun_out/tput_window.md
       find gpurun_out/prof_tput -name '*_trace.csv' -delete ;;
-    latab)
-      # 8B single-stream latency with the fused QKV + attention launch on vs off
-      for f in 1 0; do
-        RFQ_FUSED_QKV_ATTN=$f timeout -k 10 400 python -u bench.py --steps 1 --warmup 0 \
-          --docs-per-step 1 --max-num-seqs 64 --latency-runs ${LAT_RUNS:-10} --phases none \
-          > gpurun_out/lat_fused$f.json 2> gpurun_out/lat_fused$f.err
-        python3 -c "import json,sys; d=json.loads(open('gpurun_out/lat_fused$f.json').read().strip().splitlines()[-1]); print('fused=$f', d['p50_parse_text_latency_s'], d['single_stream'])"
-      done ;;
-    tp8ab)
-      for f in 1 0; do
-        RFQ_FUSED_QKV_ATTN=$f timeout -k 10 400 python -u tools/tp8_rank_emulation.py ${TP8_ARGS:-} \
-          --md gpurun_out/tp8_proj_fused$f.md > gpurun_out/tp8_fused$f.json 2> gpurun_out/tp8_fused$f.err
-        tail -c 300 gpurun_out/tp8_fused$f.json; echo
-      done ;;
     gemv)
       timeout -k 10 400 python -u tools/bench_decode_gemv.py ${GEMV_ARGS:-} \
         > gpurun_out/gemv.jsonl 2> gpurun_out/gemv.err ;;
