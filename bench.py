@@ -41,7 +41,8 @@ import sys
 import threading
 import time
 
-from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, loaded_latency,
+from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, latency_reference,
+                                                  loaded_latency,
                                                   single_stream as _single_stream, token_shape,
                                                   validate)
 
@@ -83,14 +84,14 @@ def parse():
     ap.add_argument("--phases", default="auto",
                     help="extra phases after the timed window: comma list of http, mixtral, "
                          "70b; 'auto' = all on the 1-GPU run of the 8B bench, 'none' = off")
-    ap.add_argument("--phase-budget", type=float, default=330.0,
+    ap.add_argument("--phase-budget", type=float, default=310.0,
                     help="seconds for all extra phases together (each is bounded; a watchdog "
                          "prints the JSON line if they overrun)")
     ap.add_argument("--http-open-rate", type=float, default=0.0,
                     help="open-loop HTTP phase: offered requests/s (0 = 90 %% of the "
                          "timed window's docs/s per replica)")
-    ap.add_argument("--http-open-warm", type=float, default=25.0)
-    ap.add_argument("--http-open-measure", type=float, default=35.0)
+    ap.add_argument("--http-open-warm", type=float, default=20.0)
+    ap.add_argument("--http-open-measure", type=float, default=30.0)
     ap.add_argument("--http-open-burst", type=float, default=0.75,
                     help="open-loop HTTP phase: initial burst as a fraction of the "
                          "in-flight depth (starts the queue near its steady state)")
@@ -104,13 +105,13 @@ def parse():
     ap.add_argument("--depth-docs", type=int, default=640)
     ap.add_argument("--mixtral-model", default="mixtral-8x7b")
     ap.add_argument("--mixtral-in-flight", type=int, default=768)
-    ap.add_argument("--mixtral-warm", type=int, default=768)
-    ap.add_argument("--mixtral-docs", type=int, default=1536)
+    ap.add_argument("--mixtral-warm", type=int, default=512)
+    ap.add_argument("--mixtral-docs", type=int, default=1024)
     ap.add_argument("--big-model", default="llama3-70b")
     ap.add_argument("--big-latency-runs", type=int, default=14,
                     help="70B phase: single requests over the reference's 14 recorded prompts "
                          "(a fixed set; fewer if the phase budget runs out)")
-    ap.add_argument("--tp-latency-runs", type=int, default=7)
+    ap.add_argument("--tp-latency-runs", type=int, default=14)
     ap.add_argument("--tp-docs", type=int, default=256,
                     help="TP phase: documents timed in a continuous stream (0 = skip)")
     ap.add_argument("--tp-in-flight", type=int, default=128,
@@ -267,11 +268,17 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
                                                     "not enabled on this device")
             if wctx.rank == 0:
                 try:
-                    lat, detail = latency(eng, 0, args.tp_latency_runs)
+                    # the same FIXED set as the one-GPU 70B phase: the
+                    # reference's 14 recorded prompts, per-row sampled steps reported
+                    lat, detail, rows = latency_reference(eng, args.tp_latency_runs)
+                    res["latency_set"] = "reference prompts (cache.db rows 1-14), bench hints"
                     res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
                     res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
                     res["single_stream"] = _single_stream(detail)
                     res["runs"] = len(lat)
+                    res["sampled_steps_p50"] = statistics.median(r[1] for r in rows)
+                    res["per_row"] = [{"row": a, "sampled": b, "tokens": c, "prompt": d,
+                                       "s": round(t, 3)} for (a, b, c, d), t in zip(rows, lat)]
                     if args.tp_docs > 0:
                         stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
                         warm = max(1, args.tp_in_flight // 2)
@@ -593,13 +600,19 @@ def main():
             out["phases"]["mixtral"] = ph.model_phase(
                 args.mixtral_model, seed=args.seed, in_flight=args.mixtral_in_flight,
                 warm_docs=args.mixtral_warm, docs=args.mixtral_docs, formats=("pdf", "xlsx"),
-                budget_s=min(160.0, left() - 60 if "70b" in phases else left()),
+                budget_s=min(160.0, left() - 120 if "70b" in phases else left()),
                 max_batched_tokens=args.prefill_chunk)
         if "70b" in phases and left() > 30:
             mark("phase:70b")
             out["phases"]["llama3_70b"] = ph.model_phase(
                 args.big_model, seed=args.seed, latency_runs=args.big_latency_runs,
-                budget_s=left(), in_flight=8, reference_set=True)
+                budget_s=left(), in_flight=8, reference_set=True,
+                # one request at a time: decode graphs / start-up plans for one sequence
+                # (M = 1..8 with jump-forward extends) -- the 64-row plans took 86 s
+                graph_buckets=(1,),
+                # prompts of the reference set are <= 640 tokens past the cached prefix:
+                # the prefill split plans stop at 1024 rows (halves the 70B start-up tune)
+                max_batched_tokens=min(args.prefill_chunk, 1024))
         guard.cancel()
         out["phases"]["phase_s"] = round(time.perf_counter() - t_ph, 1)
         out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)

@@ -34,6 +34,12 @@ from .stream import (DocStream, latency, latency_reference, loaded_latency, pcts
                      validate)
 
 BASELINE_P50_S = 0.883            # Groq llama3-70b p50 server time per request
+# uvicorn closes an idle keep-alive connection after 5 s by default; the open-loop
+# client reuses pooled connections, and a request written onto one the server is just
+# closing fails as a connection error (2 of 6,969 in r5's first reference-shaped run).
+# Idle gaps in these phases stay far below this.
+KEEP_ALIVE_S = 300
+UNFINISHED = "unfinished_at_phase_end"
 
 
 def _free_port() -> int:
@@ -124,7 +130,8 @@ def http_upload_phase(engine, n_docs: int = 512, clients: int = 64, client_procs
     os.environ["RFQ_PARSER_PROCS"] = str(parse_procs)
     port = _free_port()
     server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
-                                           log_level="warning", access_log=False))
+                                           log_level="warning", access_log=False,
+                                           timeout_keep_alive=KEEP_ALIVE_S))
     th = threading.Thread(target=server.run, name="bench-uvicorn", daemon=True)
     th.start()
     procs = []
@@ -201,8 +208,11 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
 
     out = []
 
+    sent = {}
+
     async def one(sess, off, kind, payload):
         t_send = time.perf_counter()
+        sent[off] = t_send
         status, body, why = 0, {}, ""
         try:
             if kind == "text":
@@ -238,7 +248,7 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
     conn = aiohttp.TCPConnector(limit=0)
     tasks = []
     async with aiohttp.ClientSession(connector=conn,
-                                     timeout=aiohttp.ClientTimeout(total=60)) as sess:
+                                     timeout=aiohttp.ClientTimeout(total=120)) as sess:
         for off, kind, payload in sched:
             delay = t0 + off - time.perf_counter()
             if delay > 0:
@@ -247,7 +257,18 @@ async def _open_loop(url: str, sched: list, t0: float, deadline: float):
                 break
             tasks.append(asyncio.ensure_future(one(sess, off, kind, payload)))
         if tasks:
-            await asyncio.wait(tasks, timeout=max(1.0, deadline - time.time()))
+            _, pending = await asyncio.wait(tasks, timeout=max(1.0, deadline - time.time()))
+            # still in flight when the phase's deadline came: the bench, not the service,
+            # ended them (reported apart from the failures)
+            t_end = time.perf_counter()
+            for t in pending:
+                t.cancel()
+            if pending:
+                await asyncio.gather(*pending, return_exceptions=True)
+            done = {r[0] for r in out}
+            for off, _, _ in sched[:len(tasks)]:
+                if off in sent and off not in done:
+                    out.append((off, t_end - t0, t_end - sent[off], False, UNFINISHED))
     return out
 
 
@@ -342,7 +363,7 @@ def _api_server_proc(cfg_dict: dict, inq, outq, parse_procs: int, port_q, stop_e
     port = _free_port()
     server = uvicorn.Server(uvicorn.Config(api.app, host="127.0.0.1", port=port,
                                            log_level="warning", access_log=False,
-                                           backlog=4096))
+                                           backlog=4096, timeout_keep_alive=KEEP_ALIVE_S))
     th = threading.Thread(target=server.run, daemon=True)
     th.start()
     t0 = time.time()
@@ -476,9 +497,16 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
         res.update(requests=len(recs), docs=ok, responses=len(done_in),
                    docs_per_s=round(ok / measure_s, 3),
                    valid=round(ok / max(1, len(done_in)), 3),
-                   http_latency_s=pcts([r[2] for r in sent_in]),
-                   failed=sum(not r[3] for r in recs),
-                   failed_by=dict(collections.Counter(r[4] for r in recs if not r[3])),
+                   http_latency_s=pcts([r[2] for r in sent_in if r[4] != UNFINISHED]),
+                   failed=sum(not r[3] and r[4] != UNFINISHED for r in recs),
+                   unfinished=sum(r[4] == UNFINISHED for r in recs),
+                   failed_by=dict(collections.Counter(r[4] for r in recs
+                                                      if not r[3] and r[4] != UNFINISHED)),
+                   # client latency of the failed requests (a generation that hit the
+                   # service's 30 s deadline returns the error dict with an empty
+                   # message -- rfq_agent.py:178-182 passes str(TimeoutError()))
+                   failed_s=sorted(round(r[2], 2) for r in recs
+                                   if not r[3] and r[4] != UNFINISHED)[:20],
                    burst_depth=burst_depth,
                    engine_depth={"mean": round(statistics.mean(win_depth), 1),
                                  "min": min(win_depth), "max": max(win_depth)}
@@ -494,7 +522,8 @@ def http_open_loop_phase(engine, rate: float, warm_s: float = 20.0, measure_s: f
                              args=(url, idle_requests, 20_000_000 + seed, idle_q), daemon=True)
             ip.start()
             try:
-                recs_i = idle_q.get(timeout=max(30.0, 10.0 * idle_requests))
+                # spawn + imports + the requests; generous for a loaded CPU test host
+                recs_i = idle_q.get(timeout=max(120.0, 15.0 * idle_requests))
             finally:
                 ip.join(timeout=10)
                 if ip.is_alive():
@@ -609,6 +638,8 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
         cfg = EngineConfig.from_env(model=model, seed=seed, max_num_seqs=nseq, **cfg_over)
         eng = LLMEngine(cfg)
         res["init_s"] = round(time.perf_counter() - t_start, 1)
+        res["gemm_tune_s"] = round(getattr(eng, "tune_s", 0.0), 1)
+        res["graph_capture_s"] = round(getattr(eng, "capture_s", 0.0), 1)
         if latency_runs and reference_set:
             # a FIXED latency set -- the reference's 14 recorded prompts
             lat, detail, rows = latency_reference(eng, latency_runs,
@@ -652,6 +683,8 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
                     res["status"] = "timeout"
             else:
                 res["status"] = "timeout"
+        elif docs:
+            res["status"] = "timeout"        # the budget ran out before the stream
         if res["status"] == "running":
             res["status"] = "ok"
     except Exception as e:  # noqa: BLE001 -- reported in the JSON line

@@ -84,6 +84,7 @@ class EngineConfig:
             warm_prefix=_env("RFQ_WARM_PREFIX", cls.warm_prefix, bool),
             check_finite=_env("RFQ_CHECK_FINITE", cls.check_finite, bool),
             decode_hints=_env("RFQ_DECODE_HINTS", cls.decode_hints, bool),
+            request_timeout_s=_env("RFQ_REQUEST_TIMEOUT_S", cls.request_timeout_s, float),
         )
         gb = os.environ.get("RFQ_GRAPH_BUCKETS")
         if gb:
