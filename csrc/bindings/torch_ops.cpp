@@ -85,6 +85,8 @@ void launch_gemm_dense(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, 
                        int, int, bool, int, hipStream_t);
 void launch_gemm_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
                          int, int64_t, bool, hipStream_t);
+void launch_gemm_w4_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
+                            int, int64_t, bool, hipStream_t);
 int64_t car_signal_bytes();
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -927,8 +929,10 @@ void gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out, bool swiglu
 
 // Grouped MoE GEMM on the dense kernel's structure (gemm_dense.hip GROUPED): x = the
 // expert-sorted rows padded to 128 per expert, w [E, N, K], expert_offsets [E+1] (device).
+// cfg bit 3: the one-wave-per-SIMD gemm_w4 structure (gemm_w4.hip GROUPED, K % 128),
+// else gemm_dense's 8-wave ping-pong
 void moe_gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out,
-                    const Tensor& expert_offsets, bool swiglu) {
+                    const Tensor& expert_offsets, bool swiglu, int64_t cfg) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_I32(expert_offsets);
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && out.is_contiguous(), "contiguous");
   TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
@@ -942,8 +946,13 @@ void moe_gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out,
   TORCH_CHECK(expert_offsets.numel() >= E + 1, "expert_offsets too short");
   TORCH_CHECK((int64_t)x.size(0) * K < (int64_t)INT32_MAX && (int64_t)N * K < (int64_t)INT32_MAX,
               "moe_gemm_dense: offsets exceed int32");
-  rfq::launch_gemm_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
-                           x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
+  TORCH_CHECK(!(cfg & 8) || K % 128 == 0, "moe_gemm_dense: the gemm_w4 form needs K % 128");
+  if (cfg & 8)
+    rfq::launch_gemm_w4_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
+                                x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
+  else
+    rfq::launch_gemm_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
+                             x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
 }
 
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
@@ -1036,7 +1045,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("moe_combine(Tensor y, Tensor inv_pos, Tensor weights, int topk, Tensor(a!) out) -> ()");
   m.def("gemm_dense(Tensor x, Tensor w, Tensor(a!) out, bool swiglu=False, int cfg=0) -> ()");
   m.def("moe_gemm_dense(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_offsets, "
-        "bool swiglu) -> ()");
+        "bool swiglu, int cfg=0) -> ()");
   m.def("moe_skinny_splitk(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) yf, int max_rows, int splits) -> ()");
   m.def("moe_combine_splitk(Tensor yf, int splits, Tensor inv_pos, Tensor weights, int topk, "

@@ -69,27 +69,67 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 // (160 KB): W pieces go out two K-tiles ahead of their first reader instead of one
 // (the weights are the operand that misses L2; a panel of activations is shared by
 // every weight tile of its row group).
+// GROUPED (Mixtral's routed experts, the gemm_dense.hip grouped form's contract): x =
+// the expert-sorted, 128-row-padded gathered rows (moe_align / moe_gather), w = [E, N,
+// K] (expert stride w_estride elements), expert_offsets[E + 1] = padded row offsets on
+// the device.  A tile is two consecutive 128-row blocks of ONE expert (the second absent
+// when the expert has an odd block count: its rows are read clamped and not stored);
+// live tiles are enumerated expert-major -> weight tile -> 256-row chunk from the
+// offsets, so no host sync and a grid fixed by the capacity (blocks past the live
+// tiles leave before any barrier).
 template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false, int MF = 16,
-          bool W3 = false>
+          bool W3 = false, bool GROUPED = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
-                    int tiles_m, int tiles_n, int group_m) {
+                    int tiles_m, int tiles_n, int group_m,
+                    const int32_t* __restrict__ expert_offsets = nullptr, int E = 0,
+                    int64_t w_estride = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem_w4[];
   w4_lds_c* const lds = (w4_lds_c*)smem_w4;
 
   // ---- block -> (row tile, weight tile): bijective XCD remap, then L2 groups
-  const int nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
-  const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
-  const int per_group = group_m * tiles_n;
-  const int gid = wg / per_group, first_m = gid * group_m;
-  const int gm = min(tiles_m - first_m, group_m);
-  const int rin = wg - gid * per_group;
-  const int tm = first_m + rin % gm, tn = rin / gm;
-  const int row0 = tm * kW4M;
-  const int m_valid = min(M - row0, kW4M);
+  int row0, tn, m_valid, m_store;         // first row, weight tile, rows readable / stored
+  if constexpr (GROUPED) {
+    constexpr int kB = 128;
+    int nchunks = 0;
+    for (int e = 0; e < E; ++e)
+      nchunks += ((expert_offsets[e + 1] - expert_offsets[e]) / kB + 1) >> 1;
+    const int nlive = nchunks * tiles_n;
+    const int bid = blockIdx.x;
+    if (bid >= nlive) return;               // before any barrier: the whole block leaves
+    const int q8 = nlive >> 3, r8 = nlive & 7, xg = bid & 7;
+    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    int e = 0, p0 = 0, s0 = 0, nbe = 0, che = 0;
+    for (; e < E; ++e) {
+      s0 = expert_offsets[e] / kB;
+      nbe = expert_offsets[e + 1] / kB - s0;
+      che = (nbe + 1) >> 1;
+      if (wg < (p0 + che) * tiles_n) break;
+      p0 += che;
+    }
+    if (e >= E) return;
+    const int local = wg - p0 * tiles_n;
+    tn = local / che;
+    const int chunk = local % che;
+    row0 = (s0 + 2 * chunk) * kB;
+    m_store = 2 * chunk + 1 < nbe ? 256 : 128;
+    m_valid = min(expert_offsets[E] - row0, kW4M);
+    w += (int64_t)e * w_estride;
+  } else {
+    const int nwg = tiles_m * tiles_n;
+    const int bid = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xg = bid & 7;
+    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    const int per_group = group_m * tiles_n;
+    const int gid = wg / per_group, first_m = gid * group_m;
+    const int gm = min(tiles_m - first_m, group_m);
+    const int rin = wg - gid * per_group;
+    const int tm = first_m + rin % gm;
+    tn = rin / gm;
+    row0 = tm * kW4M;
+    m_valid = m_store = min(M - row0, kW4M);
+  }
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -392,7 +432,7 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int trow = 128 * wm + 16 * j + rr;
-    if (trow >= m_valid) continue;
+    if (trow >= m_store) continue;
     bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
     if constexpr (EPI == kW4Swiglu) {
 #pragma unroll
@@ -423,7 +463,7 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int trow = 128 * wm + 32 * j + r32;
-    if (trow >= m_valid) continue;
+    if (trow >= m_store) continue;
     bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
     if constexpr (EPI == kW4Swiglu) {
 #pragma unroll
@@ -786,6 +826,28 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 #undef W4_READ
+
+// Grouped (MoE) form of the W3 kernel (cfg 5768's structure: DMA spread over the MFMA
+// groups, early fragment reads, the weight image in three LDS slots); the contract of
+// gemm_dense.hip launch_gemm_grouped.  K % 128 == 0.
+void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
+                            const int32_t* expert_offsets, int max_blocks, int n_out, int K,
+                            int E, int64_t w_rows, bool swiglu, hipStream_t s) {
+  if (max_blocks <= 0) return;
+  const int tiles_n = swiglu ? n_out / 128 : n_out / kW4N;
+  const int chunks = (max_blocks + E) / 2 + 1;    // live 256-row tiles <= this
+  const int grid = chunks * tiles_n;
+  const int64_t estride = w_rows * K;
+  constexpr int lds3 = 5 * kW4Img * 2;            // 160 KB
+  if (swiglu)
+    gemm_w4_kernel<kW4Swiglu, 0, true, true, 16, true, true><<<grid, 256, lds3, s>>>(
+        x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, 4, expert_offsets, E,
+        estride);
+  else
+    gemm_w4_kernel<kW4Store, 0, true, true, 16, true, true><<<grid, 256, lds3, s>>>(
+        x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, 4, expert_offsets, E,
+        estride);
+}
 
 // out = x w^T ([M, N]) or, swiglu, act = silu(x Wg^T) * (x Wu^T) ([M, F], w = [2F, K], up
 // rows at up_off = F).  n_out = N or F.

@@ -873,11 +873,19 @@ def moe_gemm8(x, w, out, expert_of_block, num_blocks, expert_offsets, swiglu: bo
                             tile or MOE_TILE_ROWS)
 
 
-def moe_gemm_dense(x, w, out, expert_offsets, swiglu: bool = False):
-    """Grouped GEMM over expert segments (moe_align with block 128) on the dense
-    kernel's 8-wave ping-pong MFMA structure (gemm_dense.hip GROUPED): no host sync,
-    fixed grid; swiglu: w = [E, 2F, K] gate|up and out = silu(x Wg^T) * (x Wu^T)."""
-    _native.ops().moe_gemm_dense(x, w, out, expert_offsets, swiglu)
+# RFQ_MOE_W4=0: the grouped expert GEMMs on gemm_dense's 8-wave ping-pong instead of the
+# one-wave-per-SIMD gemm_w4 structure
+MOE_W4 = os.environ.get("RFQ_MOE_W4", "1") != "0"
+
+
+def moe_gemm_dense(x, w, out, expert_offsets, swiglu: bool = False, cfg: int | None = None):
+    """Grouped GEMM over expert segments (moe_align with block 128): no host sync, fixed
+    grid; swiglu: w = [E, 2F, K] gate|up and out = silu(x Wg^T) * (x Wu^T).  cfg bit 3
+    (default with RFQ_MOE_W4, K % 128): the one-wave-per-SIMD 256 x 256 structure of
+    gemm_w4.hip (GROUPED), else gemm_dense.hip's 8-wave ping-pong (GROUPED)."""
+    if cfg is None:
+        cfg = 8 if MOE_W4 and w.shape[2] % 128 == 0 else 0
+    _native.ops().moe_gemm_dense(x, w, out, expert_offsets, swiglu, cfg)
 
 
 def moe_gemm_dense_ok(w, swiglu: bool) -> bool:

@@ -879,10 +879,12 @@ def test_gemm_dense_strided_rows(gpu):
 
 @pytest.mark.parametrize("T", [65, 300, 1000])
 @pytest.mark.parametrize("swiglu", [False, True])
-def test_moe_gemm_dense(gpu, T, swiglu):
-    """The grouped form of the dense MFMA GEMM over moe_align's 128-row expert segments
-    (odd block counts, empty experts) against the per-expert fp32 oracle; padding rows
-    of an expert with an odd block count must not spill into the next expert."""
+@pytest.mark.parametrize("cfg", [0, 8])
+def test_moe_gemm_dense(gpu, T, swiglu, cfg):
+    """The grouped forms of the dense MFMA GEMMs (cfg 0: gemm_dense's 8-wave ping-pong,
+    8: gemm_w4's one wave per SIMD) over moe_align's 128-row expert segments (odd block
+    counts, empty experts) against the per-expert fp32 oracle; padding rows of an expert
+    with an odd block count must not spill into the next expert."""
     from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
 
     d, F, E, k = 256, 384, 8, 2
@@ -901,7 +903,7 @@ def test_moe_gemm_dense(gpu, T, swiglu):
                   bufs.expert_of_block[:cap // BLOCK_M], bufs.expert_offsets, bufs.num_blocks)
     xs = (torch.rand(cap, K, device="cuda", generator=g) * 2 - 1).to(BF)
     out = torch.full((cap, F if swiglu else N), 7.0, device="cuda", dtype=BF)
-    ops.moe_gemm_dense(xs, w, out, bufs.expert_offsets, swiglu)
+    ops.moe_gemm_dense(xs, w, out, bufs.expert_offsets, swiglu, cfg)
     off = bufs.expert_offsets.tolist()
     assert off[4] == off[3]
     for e in range(E):

@@ -55,9 +55,9 @@ def main():
         # numerics: dense grouped vs the per-expert torch oracle on the real rows
         offl = off.tolist()
         act_d = torch.empty_like(act)
-        ops.moe_gemm_dense(xs, w13, act_d, off, True)
+        ops.moe_gemm_dense(xs, w13, act_d, off, True, 8)
         y_d = torch.empty_like(y)
-        ops.moe_gemm_dense(act_d, w2, y_d, off, False)
+        ops.moe_gemm_dense(act_d, w2, y_d, off, False, 8)
         err13 = err2 = 0.0
         for e in range(E):
             a, b = offl[e], offl[e + 1]
@@ -71,8 +71,12 @@ def main():
             err2 = max(err2, (y_d[a:b].float() - r2).abs().max().item() / r2.abs().max().item())
 
         def dense():
-            ops.moe_gemm_dense(xs, w13, act, off, True)
-            ops.moe_gemm_dense(act, w2, y, off, False)
+            ops.moe_gemm_dense(xs, w13, act, off, True, 0)
+            ops.moe_gemm_dense(act, w2, y, off, False, 0)
+
+        def w4():
+            ops.moe_gemm_dense(xs, w13, act, off, True, 8)
+            ops.moe_gemm_dense(act, w2, y, off, False, 8)
 
         def gemm8():
             ops.moe_gemm8(xs, w13, act, eob, bufs.num_blocks, off, True, 256)
@@ -90,7 +94,7 @@ def main():
                 if b > a:
                     torch.matmul(act[a:b], w2[e].t(), out=y[a:b])
 
-        ts = {name: timeit(fn) for name, fn in (("dense", dense), ("gemm8", gemm8),
+        ts = {name: timeit(fn) for name, fn in (("dense", dense), ("w4", w4), ("gemm8", gemm8),
                                                 ("per_expert", per_expert))}
         fl = 2.0 * n * (2 * F * d + d * F)
         print(json.dumps({"T": T, "pairs": n, "rows_padded": offl[E],
