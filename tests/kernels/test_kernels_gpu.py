@@ -880,14 +880,16 @@ def test_gemm_dense_strided_rows(gpu):
 @pytest.mark.parametrize("T", [65, 300, 1000])
 @pytest.mark.parametrize("swiglu", [False, True])
 @pytest.mark.parametrize("cfg", [0, 8])
-def test_moe_gemm_dense(gpu, T, swiglu, cfg):
+@pytest.mark.parametrize("d,F", [(256, 384), (512, 512)])
+def test_moe_gemm_dense(gpu, T, swiglu, cfg, d, F):
     """The grouped forms of the dense MFMA GEMMs (cfg 0: gemm_dense's 8-wave ping-pong,
     8: gemm_w4's one wave per SIMD) over moe_align's 128-row expert segments (odd block
-    counts, empty experts) against the per-expert fp32 oracle; padding rows of an expert
-    with an odd block count must not spill into the next expert."""
+    counts, empty experts) against the per-expert fp32 oracle, at two model widths;
+    padding rows of an expert with an odd block count must not spill into the next
+    expert."""
     from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
 
-    d, F, E, k = 256, 384, 8, 2
+    E, k = 8, 2
     g = torch.Generator(device="cuda").manual_seed(T)
     N = 2 * F if swiglu else d
     K = d if swiglu else F
