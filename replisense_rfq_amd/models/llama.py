@@ -410,9 +410,18 @@ class DecoderLM:
         elif D > 0:
             po, pm = dec_parts if dec_parts is not None else (attn, attn)
             ns = m.decode_splits if dec_parts is not None else 1
+            # every decode row one query (D rows = D sequences) and 8-16 query columns per
+            # kv head: one column tile per work item is the whole work list already, and
+            # the one-tile kernel's lighter register set is faster at batch 1 (TP = 8 rank
+            # shape: 8.0 / 9.6 / 11.4 vs 8.2 / 10.1 / 12.7 µs at ctx 512 / 1K / 2K,
+            # profiles/r5/attn_single_pass_lat.jsonl); the work list is the same, so
+            # graphs captured this way replay any pure-decode step of their bucket
+            tiles = m.decode_tiles
+            if tiles > 1 and D == m.dec_q_len.shape[0] and 8 <= hq // hkv <= 16:
+                tiles = 1
             ops.attn_decode(qkv[:D], kc, vc, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
                             m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, attn[:D], po, pm,
-                            hq, hkv, self.scale, ns, m.decode_tiles,
+                            hq, hkv, self.scale, ns, tiles,
                             self._dec_tickets(m.dec_work_seq.numel()))
         if m.num_prefill_tokens > 0:
             ops.attn_prefill(qkv[D:T], kc, vc, m.pf_block_tables, m.pf_q_start, m.pf_q_len,
