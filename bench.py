@@ -47,6 +47,7 @@ from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, latency_re
                                                   validate)
 
 BASELINE_P50_S = 0.883          # Groq llama3-70b p50 server time per request
+REFERENCE_SAMPLED_STEPS_P50 = 160   # the reference's recorded completions (r5_decode_shape.md)
 
 
 def parse():
@@ -274,9 +275,13 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
                     res["latency_set"] = "reference prompts (cache.db rows 1-14), bench hints"
                     res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)
                     res["latency_vs_baseline_p50"] = round(BASELINE_P50_S / statistics.median(lat), 2)
-                    res["single_stream"] = _single_stream(detail)
+                    ss = res["single_stream"] = _single_stream(detail)
                     res["runs"] = len(lat)
                     res["sampled_steps_p50"] = statistics.median(r[1] for r in rows)
+                    if ss and ss.get("sampled_steps_per_s_p50"):    # see phases.model_phase
+                        res["p50_at_reference_steps_s"] = round(
+                            ss["ttft_ms_p50"] / 1e3 + REFERENCE_SAMPLED_STEPS_P50
+                            / ss["sampled_steps_per_s_p50"], 4)
                     res["per_row"] = [{"row": a, "sampled": b, "tokens": c, "prompt": d,
                                        "s": round(t, 3)} for (a, b, c, d), t in zip(rows, lat)]
                     if args.tp_docs > 0:
@@ -610,9 +615,10 @@ def main():
                 # one request at a time: decode graphs / start-up plans for one sequence
                 # (M = 1..8 with jump-forward extends) -- the 64-row plans took 86 s
                 graph_buckets=(1,),
-                # prompts of the reference set are <= 640 tokens past the cached prefix:
-                # the prefill split plans stop at 1024 rows (halves the 70B start-up tune)
-                max_batched_tokens=min(args.prefill_chunk, 1024))
+                # 14 prompts of <= 640 new tokens each: their prefills run on the library
+                # GEMMs without the large-M split plans (the plans' start-up timing of
+                # the 70B projections took 65 s of this phase for 14 prefill steps)
+                max_batched_tokens=min(args.prefill_chunk, 1024), gemm_split=False)
         guard.cancel()
         out["phases"]["phase_s"] = round(time.perf_counter() - t_ph, 1)
         out["engine"]["wall_s"] = round(time.perf_counter() - t_start, 1)

@@ -75,6 +75,7 @@ def test_bench_tp_latency_phase_gloo():
     # the fixed latency set of the one-GPU 70B phase: the reference's recorded prompts
     assert tpl["latency_set"].startswith("reference prompts")
     assert [r["row"] for r in tpl["per_row"]] == [1, 2] and tpl["sampled_steps_p50"] > 0
+    assert tpl["p50_at_reference_steps_s"] > 0
     assert tpl["docs"] == 4 and tpl["docs_per_s"] > 0 and tpl["per_doc"]["valid"] == 1.0
 
 
@@ -245,6 +246,7 @@ def test_bench_extra_phases_cpu():
     # the fixed latency set is the reference's recorded prompts
     assert b["latency_set"].startswith("reference prompts")
     assert [r["row"] for r in b["per_row"]] == [1, 2] and all(r["sampled"] > 0 for r in b["per_row"])
+    assert b["p50_at_reference_steps_s"] > 0
     assert out["value"] > 0 and out["steps"] == 1
 
 

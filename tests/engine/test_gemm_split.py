@@ -172,3 +172,19 @@ def test_plan_hybrid_follows_cu_count():
     assert hyb[16] == 15
     # a CU count that is not a multiple of 8 rounds down like the launcher (244 -> 240)
     assert plan_hybrid(t_lib, t_dense, 16, 256, 0.0, 1.0, cus=244) == hyb
+
+
+def test_tuning_rotation_streams_from_hbm():
+    """The start-up plans time each candidate over the leading layers' weights that add
+    up to >= 1 GiB (>= 2 of them), not all of a 70B model's 80 layers."""
+    from replisense_rfq_amd.ops.autotune import _rotation
+
+    mb = 1 << 20
+    big = [torch.empty(84 * mb, dtype=torch.bfloat16) for _ in range(10)]     # 168 MB each
+    r = _rotation(big)
+    assert len(r) == 7 and sum(w.numel() * 2 for w in r) >= 1 << 30
+    small = [torch.empty(mb, dtype=torch.bfloat16) for _ in range(32)]        # 2 MB each
+    assert len(_rotation(small)) == 32                 # all of them, still under 1 GiB
+    huge = [torch.empty(600 * mb, dtype=torch.bfloat16) for _ in range(3)]   # 1.2 GB each
+    # (torch.empty never touches the pages: ~4 GB of address space, no resident memory)
+    assert len(_rotation(huge)) == 2
