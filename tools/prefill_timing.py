@@ -83,6 +83,12 @@ def run(B, S, Hq, Hkv, small):
                      "median": med,
                      "tile_us_median": round(statistics.median(per_tile), 2) if per_tile else None,
                      "last_start_us": round(max(us(r[0], t0) for r in ent), 2)})
+    if os.environ.get("RAW"):
+        # per workgroup of the last launch: blockIdx, start µs, tiles (-1 = left early), end µs
+        print(json.dumps({"raw": [[i, us(r[0], t0), (int(r[6]) & 0xFFFF) if r[1] > 0 else -1,
+                                   us(max(int(r[3]), int(r[4]), int(r[5])), t0) if r[1] > 0
+                                   else None] for i, r in enumerate(t.tolist()) if r[0] > 0]}),
+              flush=True)
     for r in rows:
         print(json.dumps(r), flush=True)
 
