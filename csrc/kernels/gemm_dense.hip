@@ -459,9 +459,10 @@ void launch_gemm_dense(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ld
   // bits 8-9: row tiles per L2 group (16, 8, 4, 32); bit 10 (with 128): fragment reads
   // early in each half; bit 11 (with 128 | 1024): the 32x32x16 MFMA form; bit 12 (with
   // 128 | 1024, not 2048): the weight image in three LDS slots, the activations in two;
-  // bit 13 (with 4096, K % 256 == 0): the persistent form (gemm_w4p_kernel)
+  // bit 13 (with 4096, K % 256 == 0): the persistent form (gemm_w4p_kernel); bit 14 (with
+  // 8192): stream-K over its last rounds (30344 = 13960 | 16384)
   if (cfg & 8) {
-    launch_gemm_w4(x, ldx, w, ldw, out, ldo, M, n_out, K, up_off, swiglu, (cfg >> 4) & 1023, s);
+    launch_gemm_w4(x, ldx, w, ldw, out, ldo, M, n_out, K, up_off, swiglu, (cfg >> 4) & 2047, s);
     return;
   }
   // cfg bit 0: the 32x32x16 MFMA variant (else 16x16x32); bit 1: 2 phases per K-tile;

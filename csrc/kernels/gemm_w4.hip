@@ -508,11 +508,28 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
 // profiles/r4_gemm_w4.md.)  The last tile's "next" pieces re-read its own K-tiles 0-2
 // (harmless; drained before exit).  Slots: W 3 (g % 3, g = K-tile counter over all the
 // workgroup's tiles), X 2 (g % 2), 160 KB.
-template <int EPI>
+//
+// SK (stream-K for the last rounds): the first nwg - sk_tiles tiles go round-robin as
+// above (whole rounds); the last sk_tiles tiles are cut into chunks of 4 K-tiles and
+// every workgroup takes an equal run of consecutive chunks, so no CU idles through a
+// partly filled last round.  A run is a sequence of units (tile, K-tile range); a unit
+// that is not a whole tile is a partial sum:
+//   * the unit that starts a tile's K range (its "owner": the lowest workgroup on it) is
+//     the LAST unit of its workgroup's run;
+//   * the others ("partners": higher workgroups, whose runs START inside that tile) are
+//     the FIRST unit of their runs: each publishes its fp32 accumulators (sc1 stores,
+//     drained, then one lane's agent-scope flag; cdna_hip_programming.md §6 Guideline 16
+//     recipe) and goes on to its next unit;
+//   * the owner polls each partner's flag (resetting it for the next launch), adds the
+//     partner's slab with sc1 loads and runs the ordinary epilogue.
+// A partner publishes before it waits for anything and all G <= CUs workgroups are
+// resident (one per CU, 160 KB LDS), so every wait ends; the spin is bounded anyway.
+template <int EPI, bool SK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                      int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
-                     int tiles_m, int tiles_n, int group_m) {
+                     int tiles_m, int tiles_n, int group_m, int sk_tiles = 0,
+                     float* __restrict__ sk_ws = nullptr, int* __restrict__ sk_flag = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem_w4[];
   w4_lds_c* const lds = (w4_lds_c*)smem_w4;
   const int nwg = tiles_m * tiles_n;
@@ -546,14 +563,15 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   };
   // a tile's DMA offsets: X rows (clamped to M - 1) with the tile's row offset folded in,
   // W piece rows in SGPRs
-  auto addrs = [&](int id, int (&xv)[8], int (&ws)[8]) {
+  // kb: the unit's first K-tile (stream-K partial units), folded into both offsets
+  auto addrs = [&](int id, int kb, int (&xv)[8], int (&ws)[8]) {
     int tm, tn;
     tile_of(id, tm, tn);
     const int row0 = tm * kW4M, mv = min(M - row0, kW4M);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int p = 8 * wid + q;
-      xv[q] = ((row0 + min(8 * p + lrow, mv - 1)) * (int)ldx + 8 * src_chunk(p)) * 2;
+      xv[q] = ((row0 + min(8 * p + lrow, mv - 1)) * (int)ldx + 8 * src_chunk(p) + kb * 64) * 2;
       int n0;
       if constexpr (EPI == kW4Swiglu) {
         const int i = (p >> 1) & 7, wc = p >> 4;
@@ -561,7 +579,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
       } else {
         n0 = tn * kW4N + 8 * p;
       }
-      ws[q] = __builtin_amdgcn_readfirstlane(n0 * (int)ldw * 2);
+      ws[q] = __builtin_amdgcn_readfirstlane((n0 * (int)ldw + kb * 64) * 2);
     }
   };
   auto wbase = [&](int slot) { return lds + slot * (kW4Img * 2); };
@@ -662,10 +680,40 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   using V40 = std::integral_constant<int, EPI == kW4Swiglu ? 24 : 40>;
   const int nk = K / 64;                          // >= 4, even
 
-  int id = blockIdx.x;
-  if (id >= nwg) return;
-  addrs(id, xv_c, ws_c);
-  addrs(id + G < nwg ? id + G : id, xv_n, ws_n);
+  // this workgroup's units: round-robin whole tiles g, g + G, ... < dp_end, then (SK) the
+  // chunk run [c0, c1) over tiles dp_end.. (a unit: tile id, K-tiles [kb, ke))
+  const int g = blockIdx.x;
+  const int dp_end = SK ? nwg - sk_tiles : nwg;
+  const int ndp = g < dp_end ? (dp_end - 1 - g) / G + 1 : 0;
+  const int cpt = nk >> 2;                        // 4-K-tile chunks per tile
+  const int csk = SK ? sk_tiles * cpt : 0;
+  const int c0 = (int)((int64_t)g * csk / G), c1 = (int)((int64_t)(g + 1) * csk / G);
+  auto unit = [&](int u, int& uid, int& kb, int& ke) {
+    if (u < ndp) {
+      uid = g + u * G;
+      kb = 0;
+      ke = nk;
+      return true;
+    }
+    if constexpr (!SK) {
+      return false;
+    } else {
+      const int tv = c0 / cpt + (u - ndp);
+      const int cs = u == ndp ? c0 : tv * cpt;
+      if (cs >= c1) return false;
+      const int ce = min(c1, (tv + 1) * cpt);
+      uid = dp_end + tv;
+      kb = (cs - tv * cpt) * 4;
+      ke = (ce - tv * cpt) * 4;
+      return true;
+    }
+  };
+  int u = 0, id, kb, ke, nid = 0, nkb = 0, nke = 0;
+  if (!unit(0, id, kb, ke)) return;
+  bool more = unit(1, nid, nkb, nke);
+  addrs(id, kb, xv_c, ws_c);
+  if (more) addrs(nid, nkb, xv_n, ws_n);
+  else addrs(id, kb, xv_n, ws_n);
   // ---- first tile's prologue: W0 X0 X1 W1 W2 (slots W 0-2, X 0-1)
 #pragma unroll
   for (int q = 0; q < 8; ++q) dma_w(q, 0, 0, ws_c);
@@ -694,6 +742,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
   }
   int wofs = 0;                                   // W slot of this tile's K-tile 0
   while (true) {
+    const int nku = __builtin_amdgcn_readfirstlane(ke - kb);   // K-tiles of this unit
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -707,7 +756,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     mid(V40{});
     half(f1, f0, T_{}, H0{}, (wofs + 1) % 3, 1, T_{}, F_{}, 0, 2 * 64, T_{}, F_{}, wofs % 3,
          3 * 64);
-    for (t = 1; t + 3 < nk; ++t) {
+    for (t = 1; t + 3 < nku; ++t) {
       wait_frags(f0);
       half(f0, f1, T_{}, H1{}, (wofs + t) % 3, t & 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
       mid(V8{});
@@ -718,7 +767,7 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     wait_frags(f0);
     half(f0, f1, T_{}, H1{}, (wofs + t) % 3, 1, F_{}, F_{}, 0, 0, F_{}, F_{}, 0, 0);
     mid(V8{});
-    half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 0, T_{}, F_{}, 1, (nk - 1) * 64, T_{}, T_{},
+    half(f1, f0, T_{}, H0{}, (wofs + t + 1) % 3, 0, T_{}, F_{}, 1, (nku - 1) * 64, T_{}, T_{},
          (wofs + t) % 3, 0);
     ++t;
     // t = nk-2: X(0), W(1) of the next tile
@@ -736,6 +785,32 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
     mid(V8{});
     half(f1, f0, F_{}, H0{}, 0, 0, T_{}, T_{}, 1, 64, T_{}, T_{}, (wofs + t) % 3, 128);
 
+    // ---- stream-K partial units (see above): a partner publishes its fp32 accumulators
+    // and moves on; an owner first waits for its partners' flags, then adds their slabs
+    // row block by row block inside the epilogue (the accumulators are only ever read
+    // there, in the epilogue's order: any other read or write of them spills)
+    const bool pub = SK && kb != 0;
+    const bool own = SK && kb == 0 && ke != nk;
+    const int tend = SK ? (id - dp_end + 1) * cpt : 0;      // chunk past this tile
+    const __amdgpu_buffer_rsrc_t sr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)sk_ws, (short)0, 0x7fffffff, 0x00020000);
+    if constexpr (SK) {
+      if (own) {
+        if (tid == 0) {
+          for (int pw = g + 1; pw < G && (int)((int64_t)pw * csk / G) < tend; ++pw) {
+            if ((int64_t)(pw + 1) * csk / G == (int64_t)pw * csk / G) continue;   // empty run
+            for (int spin = 0; spin < (1 << 22); ++spin) {
+              if (__hip_atomic_load(sk_flag + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                break;
+              __builtin_amdgcn_s_sleep(2);
+            }
+            __hip_atomic_store(sk_flag + pw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every slab load is sc1
+      }
+    }
     // ---- epilogue of tile id (the next tile's pieces are in flight).  A fixed number of
     // stores per wave (32, SwiGLU 16): buffer stores whose rows past M fall outside the
     // output range and are dropped; two lanes' 8-byte runs are paired into one 16-byte
@@ -749,7 +824,40 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
         // a never-taken, opaque branch per row block keeps the compiler from hoisting
         // every block's accumulator reads to the top (that spilled); the store count
         // stays fixed, which the next tile's vmcnt(40) relies on
-        if (__builtin_amdgcn_readfirstlane(nk + j) < 0) continue;
+        if (__builtin_amdgcn_readfirstlane(nku + j) < 0) continue;
+        float t[8][4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[i][e] = acc[i][j][e];
+        if constexpr (SK) {
+          // slab offset: lane part in one VGPR, (i, j) part as soffset
+          if (pub) {
+            const int base = (g * 64 * 256 + tid) * 16;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              u32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = __float_as_uint(t[i][e]);
+              __builtin_amdgcn_raw_buffer_store_b128(v, sr, base, (i * 8 + j) * 4096, 16);
+            }
+            continue;
+          }
+          if (own) {
+            for (int pw = g + 1; pw < G && (int)((int64_t)pw * csk / G) < tend; ++pw) {
+              if ((int64_t)(pw + 1) * csk / G == (int64_t)pw * csk / G) continue;
+              const int base = (pw * 64 * 256 + tid) * 16;
+              u32x4 v[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+                v[i] = __builtin_amdgcn_raw_buffer_load_b128(sr, base, (i * 8 + j) * 4096, 16);
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[i][e] += __uint_as_float(v[i][e]);
+            }
+          }
+        }
         const int trow = 128 * wm + 16 * j + rr;
         const int rowb = (row0 + trow) * (int)ldo * 2;        // byte offset of the row
         const bool odd = kq & 1;
@@ -762,9 +870,9 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
               float o[4];
 #pragma unroll
               for (int u = 0; u < 4; ++u) {
-                const float gf = bf2f(f2bf(acc[2 * pr + e][j][u]));
+                const float gf = bf2f(f2bf(t[2 * pr + e][u]));
                 const float sg = gf / (1.f + __expf(-gf));
-                o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(acc[4 + 2 * pr + e][j][u]));
+                o[u] = bf2f(f2bf(sg)) * bf2f(f2bf(t[4 + 2 * pr + e][u]));
               }
               h[e][0] = pack_bf16x2(o[0], o[1]);
               h[e][1] = pack_bf16x2(o[2], o[3]);
@@ -782,10 +890,10 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
         } else {
 #pragma unroll
           for (int pr = 0; pr < 4; ++pr) {
-            const uint32_t a0 = pack_bf16x2(acc[2 * pr][j][0], acc[2 * pr][j][1]);
-            const uint32_t a1 = pack_bf16x2(acc[2 * pr][j][2], acc[2 * pr][j][3]);
-            const uint32_t b0 = pack_bf16x2(acc[2 * pr + 1][j][0], acc[2 * pr + 1][j][1]);
-            const uint32_t b1 = pack_bf16x2(acc[2 * pr + 1][j][2], acc[2 * pr + 1][j][3]);
+            const uint32_t a0 = pack_bf16x2(t[2 * pr][0], t[2 * pr][1]);
+            const uint32_t a1 = pack_bf16x2(t[2 * pr][2], t[2 * pr][3]);
+            const uint32_t b0 = pack_bf16x2(t[2 * pr + 1][0], t[2 * pr + 1][1]);
+            const uint32_t b1 = pack_bf16x2(t[2 * pr + 1][2], t[2 * pr + 1][3]);
             // even kq keeps subtile 2 pr (its 4 columns + the partner's next 4), odd kq
             // subtile 2 pr + 1 (the partner's 4 columns + its own)
             const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(odd ? a0 : b0), 0x401F);
@@ -801,15 +909,27 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
         }
       }
     }
-    id += G;
-    if (id >= nwg) break;
+    if constexpr (SK) {
+      if (pub) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // every wave's slab stores landed
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(sk_flag + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (!more) break;
+    ++u;
+    id = nid;
+    kb = nkb;
+    ke = nke;
+    more = unit(u + 1, nid, nkb, nke);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       xv_c[q] = xv_n[q];
       ws_c[q] = ws_n[q];
     }
-    addrs(id + G < nwg ? id + G : id, xv_n, ws_n);
-    wofs = (wofs + nk) % 3;
+    if (more) addrs(nid, nkb, xv_n, ws_n);
+    else addrs(id, kb, xv_n, ws_n);
+    wofs = (wofs + nku) % 3;
     {
       w4_lds_c* const pw = wbase(wofs) + wo + lo0;
       w4_lds_c* const px = xbase(0) + xo + lo0;
@@ -847,6 +967,34 @@ void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
     gemm_w4_kernel<kW4Store, 0, true, true, 16, true, true><<<grid, 256, lds3, s>>>(
         x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, 4, expert_offsets, E,
         estride);
+}
+
+// Stream-K slabs (256 KB per workgroup: 64 accumulators x 256 lanes x 16 B) and
+// zeroed flags, one set per device, allocated on first use outside stream capture.
+static bool gemm_w4p_sk_ws(int g, float** ws, int** flags) {
+  constexpr int kMaxDev = 16, kMaxWg = 1024;
+  static float* s_ws[kMaxDev] = {};
+  static int* s_flags[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev >= kMaxDev || g > kMaxWg) return false;
+  if (s_ws[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(nullptr, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+      return false;
+    float* p = nullptr;
+    int* f = nullptr;
+    if (hipMalloc(&p, (size_t)kMaxWg * 64 * 256 * 16) != hipSuccess) return false;
+    if (hipMalloc(&f, kMaxWg * sizeof(int)) != hipSuccess || hipMemset(f, 0, kMaxWg * sizeof(int)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return false;
+    }
+    s_ws[dev] = p;
+    s_flags[dev] = f;
+  }
+  *ws = s_ws[dev];
+  *flags = s_flags[dev];
+  return true;
 }
 
 // out = x w^T ([M, N]) or, swiglu, act = silu(x Wg^T) * (x Wu^T) ([M, F], w = [2F, K], up
@@ -890,6 +1038,26 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
     }();
     const int g = grid < ncu ? grid : ncu;
     constexpr int lds3 = 5 * kW4Img * 2;
+    // abl bit 10 (cfg bit 14): stream-K over the last rounds, one workgroup per CU.  The
+    // stream-K region: the partly filled last round (or the whole grid, when it is below
+    // one round) when it is at least half full, else that round plus the full one before
+    // it, so a split tile has one or two partners; none on whole rounds.  Each workgroup
+    // needs >= 2 chunks of 4 K-tiles.
+    if (abl & 1024) {
+      const int r = grid % ncu, rounds = grid / ncu;
+      const int sk = r == 0 ? 0 : (2 * r >= ncu ? r : (rounds >= 1 ? r + ncu : 0));
+      float* ws = nullptr;
+      int* flags = nullptr;
+      if (sk > 0 && (int64_t)sk * (K / 256) >= 2 * ncu && gemm_w4p_sk_ws(ncu, &ws, &flags)) {
+        if (swiglu)
+          gemm_w4p_kernel<kW4Swiglu, true><<<ncu, 256, lds3, s>>>(
+              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags);
+        else
+          gemm_w4p_kernel<kW4Store, true><<<ncu, 256, lds3, s>>>(
+              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags);
+        return;
+      }
+    }
     if (swiglu)
       gemm_w4p_kernel<kW4Swiglu><<<g, 256, lds3, s>>>(x, ldx, w, ldw, out, ldo, M, K, up_off,
                                                       tiles_m, tiles_n, gmr);

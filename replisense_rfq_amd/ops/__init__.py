@@ -628,6 +628,21 @@ def gemm_w4_ok(M: int, N: int, K: int) -> bool:
     return K % 128 == 0 and N * K * 2 < lim and M * max(K, N) * 2 < lim
 
 
+def w4p_stream_k_applies(M: int, N: int, K: int, cus: int) -> bool:
+    """Whether gemm_dense cfg bit 14 (stream-K over gemm_w4p's last rounds) changes the
+    launch for this shape; the launcher's rule (gemm_w4.hip launch_gemm_w4): a partly
+    filled last round of 256 x 256 tiles (N = 2F under SwiGLU: F / 128 column tiles) on
+    ``cus`` (rounded down to 8) persistent workgroups, each with >= 2 chunks of 4
+    K-tiles.  Otherwise the plain persistent kernel runs."""
+    ncu = cus // 8 * 8
+    if K % 256 or ncu <= 0:
+        return False
+    grid = -(-M // 256) * (N // 256)
+    r, rounds = grid % ncu, grid // ncu
+    sk = 0 if r == 0 else (r if 2 * r >= ncu else (r + ncu if rounds >= 1 else 0))
+    return sk > 0 and sk * (K // 256) >= 2 * ncu
+
+
 def gemm_dense(x, w, out=None, swiglu: bool = False, cfg: int = 0):
     """out[M, N] = x[M, K] . w[N, K]^T on the 8-wave ping-pong MFMA kernel; swiglu:
     w = gate|up [2F, K] and out[M, F] = silu(x Wg^T) * (x Wu^T) (rounded like the

@@ -17,6 +17,7 @@ import torch
 
 from . import (ROWS_BIT, ROWS_CFGS, ROWS_CFGS_PAIRED, SPLITK_BIT, SPLITK_CFGS, SPLITK_NT,
                SPLITK_TILED, _native, _wsel, gemm_dense_ok, gemm_w4_ok, rows_ok, set_rows_best,
+               w4p_stream_k_applies,
                set_linear_plan, set_norm_plan, set_rope_plan, set_silu_plan,
                set_split_plan,
                set_swiglu_plan, silu_linear, silu_mul, splitk_fits, splitk_ws, tiled_of,
@@ -404,8 +405,10 @@ DENSE_ON = os.environ.get("RFQ_GEMM_DENSE", "1") != "0"
 # (one wave per SIMD), DMA spread over the MFMA groups, 4 row tiles per L2 group, fragment
 # reads early in each half, the weight image in three LDS slots, persistent over output
 # tiles with the K-tile pipeline crossing tile boundaries (K % 256; otherwise the same
-# kernel without persistence, 5768; 1672 without the third slot; profiles/r4_gemm_w4.md)
-DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,13960").split(","))
+# kernel without persistence, 5768; 1672 without the third slot; profiles/r4_gemm_w4.md);
+# 30344 = 13960 | 16384: the same with stream-K over its last rounds (timed only where
+# the launcher would use it: ops.w4p_stream_k_applies; profiles/r5_gemm_stream_k.md)
+DENSE_CFGS = tuple(int(c) for c in os.environ.get("RFQ_GEMM_DENSE_CFGS", "2,13960,30344").split(","))
 DENSE_MARGIN = 0.99              # the hand-written kernel must win by 1 %
 
 
@@ -485,6 +488,12 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
         if DENSE_ON and gemm_dense_ok(quantum, N, K):
             act = torch.empty(J * quantum, N // 2, device=w.device, dtype=w.dtype) \
                 if name == "gate_up" else None
+            cus = torch.cuda.get_device_properties(w.device).multi_processor_count
+
+            def skip(c, m):
+                # K % 128, < 2 GiB operands; a stream-K cfg only where it changes the launch
+                return (c & 8 and not gemm_w4_ok(m, N, K)) or \
+                    (c & 16384 and not w4p_stream_k_applies(m, N, K, cus))
             for j in range(1, J + 1):
                 m = j * quantum
                 t_lib = times[j] if table[j] is None else \
@@ -492,7 +501,7 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                 best_c, t_best = -1, t_lib * DENSE_MARGIN
                 t_lib_j[j] = t_lib
                 for c in DENSE_CFGS:
-                    if c & 8 and not gemm_w4_ok(m, N, K):   # K % 128, < 2 GiB operands
+                    if skip(c, m):
                         continue
                     t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, out[:m], False, c),
                               [w], reps, graph=False)
@@ -508,7 +517,7 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                     t_ref = min(t_lib, t_best) + t_silu
                     bs, ts = -1, t_ref * DENSE_MARGIN
                     for c in DENSE_CFGS:
-                        if c & 8 and not gemm_w4_ok(m, N, K):
+                        if skip(c, m):
                             continue
                         t = _time(lambda w_, m=m, c=c: ops.gemm_dense(x[:m], w_, act[:m], True, c),
                                   [w], reps, graph=False)
@@ -534,9 +543,11 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
         report.append(("lt:" + name, J * quantum, N, K, J, f"{n_lt}/{J} buckets", 0.0))
         w4 = sum(1 for c in dense if c >= 0 and c & 8)
         w4s = sum(1 for c in swi if c >= 0 and c & 8)
+        sk = sum(1 for c in dense if c >= 0 and c & 16384)
+        sks = sum(1 for c in swi if c >= 0 and c & 16384)
         report.append(("dense:" + name, J * quantum, N, K, J,
-                       f"{n_dense}/{J} buckets (w4 {w4}), hybrid {n_hyb}, swiglu {n_swi}/{J} "
-                       f"(w4 {w4s})", 0.0))
+                       f"{n_dense}/{J} buckets (w4 {w4}, stream-K {sk}), hybrid {n_hyb}, "
+                       f"swiglu {n_swi}/{J} (w4 {w4s}, stream-K {sks})", 0.0))
         for j, parts in enumerate(table):
             if parts is not None:
                 t_split = sum(times[c] for c in parts)

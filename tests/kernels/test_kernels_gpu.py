@@ -844,6 +844,32 @@ def test_gemm_dense(gpu, M, N, K, swiglu, cfg):
     _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_dense M{M} N{N} K{K} swiglu={swiglu}")
 
 
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("M,N,K", [(2048, 6144, 4096), (3000, 4096, 2048), (5000, 4096, 1024),
+                                   (4000, 4608, 512), (7000, 4096, 1024)])
+def test_gemm_w4p_stream_k(gpu, M, N, K, swiglu):
+    """Stream-K form of the persistent gemm_w4p (cfg bit 14): the last rounds' tiles cut
+    into runs of 4-K-tile chunks, partial tiles published as fp32 slabs and added by the
+    tile's owner.  Shapes: the whole grid below one round (192 tiles), a half-full last
+    round, a last round under half full (+ the full round before it), and 2-chunk runs
+    (K 512: every unit 4 K-tiles long).  Three launches each (the flags must be reset by
+    the owners), against the fp32 oracle and the non-stream-K kernel."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + swiglu)
+    x = ((torch.rand(M, K, device="cuda", generator=g) * 2 - 1)).to(BF)
+    w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / math.sqrt(K)).to(BF)
+    base = ops.gemm_dense(x, w, swiglu=swiglu, cfg=13960)
+    r = x.float() @ w.float().t()
+    if swiglu:
+        F = N // 2
+        gg, u = r[:, :F].to(BF).float(), r[:, F:].to(BF).float()
+        r = (gg * torch.sigmoid(gg)).to(BF).float() * u
+    for it in range(3):
+        out = ops.gemm_dense(x, w, swiglu=swiglu, cfg=13960 | 16384)
+        _close(out, r, atol=2e-2, rtol=2e-2, what=f"gemm_w4p stream-K M{M} N{N} K{K} it{it}")
+        # same products, only the fp32 summation order of split tiles differs
+        assert (out.float() - base.float()).abs().max().item() <= 2e-2 * r.abs().max().item()
+
+
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3, 8, 8 | 128 | 512 | 1024 | 2048, 8 | 128 | 512 | 1024 | 4096,
                                  8 | 128 | 512 | 1024 | 4096 | 8192])
 def test_gemm_dense_identity_asymmetric(gpu, cfg):
