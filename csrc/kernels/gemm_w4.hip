@@ -33,6 +33,7 @@
 //    w-tile (blocks sharing a weight panel run together on one XCD's L2).
 // Shapes: K % 128 == 0, N % 256 == 0 (F % 128 with SwiGLU), any M >= 1 (rows past M read
 // row M-1 and are not stored), 16-byte aligned rows.
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -969,29 +970,35 @@ void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
         estride);
 }
 
-// Stream-K slabs (256 KB per workgroup: 64 accumulators x 256 lanes x 16 B) and
-// zeroed flags, one set per device, allocated on first use outside stream capture.
-static bool gemm_w4p_sk_ws(int g, float** ws, int** flags) {
-  constexpr int kMaxDev = 16, kMaxWg = 1024;
+// Stream-K slabs (256 KB per workgroup: 64 accumulators x 256 lanes x 16 B) and zeroed
+// flags for g workgroups, one set per device, allocated on first use outside stream
+// capture (64 MB at 256 CUs); false = run the plain persistent kernel instead.
+static bool gemm_w4p_sk_ws(int g, hipStream_t stream, float** ws, int** flags) {
+  constexpr int kMaxDev = 16;
+  static std::mutex mu;
   static float* s_ws[kMaxDev] = {};
   static int* s_flags[kMaxDev] = {};
+  static int s_cap[kMaxDev] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev >= kMaxDev || g > kMaxWg) return false;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return false;
+  std::lock_guard<std::mutex> lock(mu);
   if (s_ws[dev] == nullptr) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(nullptr, &st) == hipSuccess && st != hipStreamCaptureStatusNone)
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
       return false;
     float* p = nullptr;
     int* f = nullptr;
-    if (hipMalloc(&p, (size_t)kMaxWg * 64 * 256 * 16) != hipSuccess) return false;
-    if (hipMalloc(&f, kMaxWg * sizeof(int)) != hipSuccess || hipMemset(f, 0, kMaxWg * sizeof(int)) != hipSuccess ||
+    if (hipMalloc(&p, (size_t)g * 64 * 256 * 16) != hipSuccess) return false;
+    if (hipMalloc(&f, g * sizeof(int)) != hipSuccess || hipMemset(f, 0, g * sizeof(int)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
       (void)hipFree(p);
       return false;
     }
     s_ws[dev] = p;
     s_flags[dev] = f;
+    s_cap[dev] = g;
   }
+  if (g > s_cap[dev]) return false;
   *ws = s_ws[dev];
   *flags = s_flags[dev];
   return true;
@@ -1048,7 +1055,7 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
       const int sk = r == 0 ? 0 : (2 * r >= ncu ? r : (rounds >= 1 ? r + ncu : 0));
       float* ws = nullptr;
       int* flags = nullptr;
-      if (sk > 0 && (int64_t)sk * (K / 256) >= 2 * ncu && gemm_w4p_sk_ws(ncu, &ws, &flags)) {
+      if (sk > 0 && (int64_t)sk * (K / 256) >= 2 * ncu && gemm_w4p_sk_ws(ncu, s, &ws, &flags)) {
         if (swiglu)
           gemm_w4p_kernel<kW4Swiglu, true><<<ncu, 256, lds3, s>>>(
               x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags);
