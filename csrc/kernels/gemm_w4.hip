@@ -972,7 +972,9 @@ void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
 
 // Stream-K slabs (256 KB per workgroup: 64 accumulators x 256 lanes x 16 B) and zeroed
 // flags for g workgroups, one set per device, allocated on first use outside stream
-// capture (64 MB at 256 CUs); false = run the plain persistent kernel instead.
+// capture (64 MB at 256 CUs); false = run the plain persistent kernel instead.  One set
+// per device means one stream-K launch in flight per device: the engine issues its
+// projections on one stream (a second concurrent stream would need its own set).
 static bool gemm_w4p_sk_ws(int g, hipStream_t stream, float** ws, int** flags) {
   constexpr int kMaxDev = 16;
   static std::mutex mu;

@@ -188,3 +188,19 @@ def test_tuning_rotation_streams_from_hbm():
     huge = [torch.empty(600 * mb, dtype=torch.bfloat16) for _ in range(3)]   # 1.2 GB each
     # (torch.empty never touches the pages: ~4 GB of address space, no resident memory)
     assert len(_rotation(huge)) == 2
+
+
+def test_stream_k_rule_matches_launcher():
+    """ops.w4p_stream_k_applies mirrors gemm_w4.hip launch_gemm_w4's stream-K region rule
+    (the start-up plan times cfg bit 14 only where it changes the launch): 256-row x
+    256-column tiles on the CU count rounded down to 8; a last round at least half full,
+    or (under half) that round plus the full one before it; >= 2 chunks of 4 K-tiles
+    per workgroup; K % 256."""
+    from replisense_rfq_amd.ops import w4p_stream_k_applies as sk
+    assert sk(2048, 6144, 4096, 256)          # 192 tiles, below one round, >= half
+    assert not sk(1024, 6144, 4096, 256)      # 96 tiles: under half a round, no full round
+    assert sk(5000, 4096, 1024, 256)          # 320 tiles: 64 past a full round -> 320
+    assert not sk(4096, 4096, 4096, 256)      # 256 tiles: whole rounds
+    assert not sk(2048, 6144, 4224, 256)      # K % 256
+    assert not sk(2048, 6144, 256, 256)       # 192 chunks < 2 per workgroup
+    assert sk(2048, 6144, 4096, 260) == sk(2048, 6144, 4096, 256)   # 260 CUs -> 256
