@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <cstring>
+#include <vector>
 
 namespace rfq {
 typedef uint16_t bf16_t;
@@ -88,6 +89,8 @@ void launch_gemm_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, 
 void launch_gemm_w4_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
                             int, int64_t, bool, hipStream_t);
 int64_t car_signal_bytes();
+uint32_t* kernel_error_words(hipStream_t);
+uint32_t kernel_error_read(int);
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 void launch_car_twoshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -765,6 +768,16 @@ void car_ipc_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<vo
 
 int64_t car_data_offset() { return rfq::car_signal_bytes(); }
 
+// Error words of the bounded in-launch waits (csrc/kernels/kerr.hip): allocated by the
+// first call (the engine calls it at start-up, before any graph capture); returns the
+// slots' counts (all 0 when no GPU / nothing allocated).
+std::vector<int64_t> kernel_errors() {
+  (void)rfq::kernel_error_words(nullptr);
+  std::vector<int64_t> out;
+  for (int i = 0; i < 3; ++i) out.push_back((int64_t)rfq::kernel_error_read(i));
+  return out;
+}
+
 int64_t car_error_info(int64_t ptr) {
   return (int64_t)rfq::car_read_info(reinterpret_cast<const void*>(ptr));
 }
@@ -1005,6 +1018,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("car_ipc_open(Tensor handle) -> int", &car_ipc_open);
   m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
   m.def("car_data_offset() -> int", &car_data_offset);
+  m.def("kernel_errors() -> int[]", &kernel_errors);
   m.def("car_error(int ptr) -> int", &car_error);
   m.def("car_error_info(int ptr) -> int", &car_error_info);
   m.def("moe_skinny(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "

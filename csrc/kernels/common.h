@@ -102,6 +102,21 @@ __device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* l) {
 #endif
 }
 
+// Error words of the bounded in-launch waits (kerr.hip): slot kErrStreamK counts stream-K
+// slab waits that gave up, kErrPersist the persistent decode layer's stage waits,
+// kErrPersistInfo keeps the first failing (layer, stage) of the latter.
+enum { kErrStreamK = 0, kErrPersist = 1, kErrPersistInfo = 2, kKernelErrorWords = 16 };
+uint32_t* kernel_error_words(hipStream_t s);
+uint32_t kernel_error_read(int slot);
+
+// Bounded waits are timed on the 100 MHz s_memrealtime clock: 1 s.
+constexpr uint64_t kSpinTicks = 100000000ull;
+
+__device__ __forceinline__ void report_error(uint32_t* words, int slot) {
+  if (words != nullptr)
+    __hip_atomic_fetch_add(words + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Counter-based RNG (splitmix/murmur style finaliser) — deterministic per
 // (seed, row, column), identical on every TP rank for the same global column.
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint32_t a, uint32_t b) {

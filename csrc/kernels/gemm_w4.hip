@@ -530,7 +530,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                      int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
                      int tiles_m, int tiles_n, int group_m, int sk_tiles = 0,
-                     float* __restrict__ sk_ws = nullptr, int* __restrict__ sk_flag = nullptr) {
+                     float* __restrict__ sk_ws = nullptr, int* __restrict__ sk_flag = nullptr,
+                     uint32_t* __restrict__ sk_err = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem_w4[];
   w4_lds_c* const lds = (w4_lds_c*)smem_w4;
   const int nwg = tiles_m * tiles_n;
@@ -800,12 +801,20 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
         if (tid == 0) {
           for (int pw = g + 1; pw < G && (int)((int64_t)pw * csk / G) < tend; ++pw) {
             if ((int64_t)(pw + 1) * csk / G == (int64_t)pw * csk / G) continue;   // empty run
-            for (int spin = 0; spin < (1 << 22); ++spin) {
-              if (__hip_atomic_load(sk_flag + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                break;
+            // bounded wait (1 s): on a timeout the owner counts an error (the runner then
+            // fails the step) and leaves the flag alone -- clearing a flag it never saw
+            // set would let the late partner's 1 satisfy the next launch early
+            bool seen = false;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (!(seen = __hip_atomic_load(sk_flag + pw, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) break;
               __builtin_amdgcn_s_sleep(2);
             }
-            __hip_atomic_store(sk_flag + pw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (seen)
+              __hip_atomic_store(sk_flag + pw, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+              report_error(sk_err, kErrStreamK);
           }
         }
         __syncthreads();
@@ -971,20 +980,28 @@ void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
 }
 
 // Stream-K slabs (256 KB per workgroup: 64 accumulators x 256 lanes x 16 B) and zeroed
-// flags for g workgroups, one set per device, allocated on first use outside stream
-// capture (64 MB at 256 CUs); false = run the plain persistent kernel instead.  One set
-// per device means one stream-K launch in flight per device: the engine issues its
-// projections on one stream (a second concurrent stream would need its own set).
+// flags for g workgroups, allocated on first use outside stream capture (64 MB at 256
+// CUs); false = run the plain persistent kernel instead.  One set per (device, stream):
+// two stream-K launches in flight on different streams (the runner's capture stream, an
+// overlap experiment) never share slabs or flags.  At most kSkStreams streams
+// per device get a set; launches on further streams take the plain kernel.
 static bool gemm_w4p_sk_ws(int g, hipStream_t stream, float** ws, int** flags) {
-  constexpr int kMaxDev = 16;
+  constexpr int kMaxDev = 16, kSkStreams = 4;
   static std::mutex mu;
-  static float* s_ws[kMaxDev] = {};
-  static int* s_flags[kMaxDev] = {};
-  static int s_cap[kMaxDev] = {};
+  static hipStream_t s_stream[kMaxDev][kSkStreams] = {};
+  static float* s_ws[kMaxDev][kSkStreams] = {};
+  static int* s_flags[kMaxDev][kSkStreams] = {};
+  static int s_cap[kMaxDev][kSkStreams] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return false;
   std::lock_guard<std::mutex> lock(mu);
-  if (s_ws[dev] == nullptr) {
+  int slot = -1;
+  for (int i = 0; i < kSkStreams && slot < 0; ++i)
+    if (s_ws[dev][i] != nullptr && s_stream[dev][i] == stream) slot = i;
+  if (slot < 0) {
+    for (int i = 0; i < kSkStreams && slot < 0; ++i)
+      if (s_ws[dev][i] == nullptr) slot = i;
+    if (slot < 0) return false;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
       return false;
@@ -996,13 +1013,14 @@ static bool gemm_w4p_sk_ws(int g, hipStream_t stream, float** ws, int** flags) {
       (void)hipFree(p);
       return false;
     }
-    s_ws[dev] = p;
-    s_flags[dev] = f;
-    s_cap[dev] = g;
+    s_stream[dev][slot] = stream;
+    s_ws[dev][slot] = p;
+    s_flags[dev][slot] = f;
+    s_cap[dev][slot] = g;
   }
-  if (g > s_cap[dev]) return false;
-  *ws = s_ws[dev];
-  *flags = s_flags[dev];
+  if (g > s_cap[dev][slot]) return false;
+  *ws = s_ws[dev][slot];
+  *flags = s_flags[dev][slot];
   return true;
 }
 
@@ -1058,12 +1076,13 @@ void launch_gemm_w4(const bf16_t* x, int64_t ldx, const bf16_t* w, int64_t ldw, 
       float* ws = nullptr;
       int* flags = nullptr;
       if (sk > 0 && (int64_t)sk * (K / 256) >= 2 * ncu && gemm_w4p_sk_ws(ncu, s, &ws, &flags)) {
+        uint32_t* err = kernel_error_words(s);
         if (swiglu)
           gemm_w4p_kernel<kW4Swiglu, true><<<ncu, 256, lds3, s>>>(
-              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags);
+              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags, err);
         else
           gemm_w4p_kernel<kW4Store, true><<<ncu, 256, lds3, s>>>(
-              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags);
+              x, ldx, w, ldw, out, ldo, M, K, up_off, tiles_m, tiles_n, gmr, sk, ws, flags, err);
         return;
       }
     }

@@ -87,6 +87,10 @@ class ModelRunner:
         # (captured into the decode graphs too) and read back with the sampled tokens
         self.check_finite = bool(getattr(cfg, "check_finite", False))
         self._nonfinite = torch.zeros(1, dtype=torch.int32, device=self.device)
+        # bounded in-launch waits (stream-K slabs, persistent decode stages) count their
+        # timeouts in host-mapped words (csrc/kernels/kerr.hip); allocated here, before
+        # any graph capture, and compared after every step's token readback
+        self._kerr0 = ops.kernel_errors()[:2] if self.is_cuda else [0, 0]
         if tp.enabled:
             self._setup_control_plane()
         # host-side split of a step: pack (scheduler), launch (upload + forward + sampler
@@ -288,6 +292,16 @@ class ModelRunner:
                 self._nonfinite.zero_()
                 raise RuntimeError(f"non-finite logits: {bad} Inf/NaN entries in step "
                                    f"{self.stats['steps']} (TP rank {self.tp.rank})")
+        if self.is_cuda:
+            kerr = ops.kernel_errors()
+            if kerr[:2] != self._kerr0:
+                # a hand-off inside a launch gave up after its bounded wait: this step's
+                # outputs may hold unpublished partial sums.  Fatal, like the custom
+                # all-reduce's flag timeout below.
+                self._kerr0 = kerr[:2]
+                raise RuntimeError(f"in-launch hand-off timeout (stream-K {kerr[0]}, persistent "
+                                   f"decode {kerr[1]}, first at {kerr[2] - 1:#x}) on TP rank "
+                                   f"{self.tp.rank}; results of this step are unreliable")
         car = self.tp.car
         if car is not None and car.errors():
             # a peer's flag never arrived inside the kernel's bounded spin: the sums of

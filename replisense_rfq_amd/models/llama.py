@@ -119,9 +119,13 @@ class DecoderLM:
 
             rmsnorm(x) diag(g) W^T = rsqrt(mean(x^2) + eps) * (x W'^T),   W' = W diag(g)
 
-        qkv <- qkv * attn_norm, gate|up <- gate|up * mlp_norm (in place, rounded to bf16
-        once), and both norm weights become ones, so every path of the forward stays exact
-        algebra.  What it buys is the TP = 1 small-step path (_forward_fold): the qkv and
+        qkv <- qkv * attn_norm, gate|up <- gate|up * mlp_norm (in place), and both norm
+        weights become ones.  The algebra is the same on every path of the forward, but the
+        numerics are not bit-identical: W' = bf16(W diag(g)) is rounded once, where the
+        unfolded model rounds the normalised activations bf16(rmsnorm(x) g) instead.  The
+        logits of the folded model stay within bf16 rounding of the unfolded one (pinned
+        at <= 2e-2 relative over a prefill + decode sequence, tests/engine/
+        test_fold_norms.py).  What it buys is the TP = 1 small-step path (_forward_fold): the qkv and
         gate|up row-streaming GEMVs read the UN-normalised residual and apply the norm's
         scale themselves (each wave reads the whole row anyway), and the o / down GEMVs add
         into the residual in their epilogue -- no norm launch and no cross-workgroup
@@ -143,8 +147,11 @@ class DecoderLM:
 
     def _fold_step(self, m: "ForwardMeta", T: int) -> bool:
         """Run this step through _forward_fold: folded weights, a small step whose
-        projections all fit the row-streaming GEMV, no cascade attention."""
+        projections all fit the row-streaming GEMV, no cascade (shared-prefix) attention
+        (_forward_fold has no normalised activations for it to read)."""
         if not self.norms_folded or T < 1:
+            return False
+        if 0 < ops.SHARED_PREFIX_MIN_ROWS <= m.num_decode:
             return False
         lw = self.w["layers"][0]
         d = self.cfg.hidden
@@ -309,7 +316,9 @@ class DecoderLM:
             qkv = ops.rows_rope_normx(residual, lw["qkv"], m.positions, self.cos_sin,
                                       m.slot_mapping, self.kv_k[li], self.kv_v[li], self.hq,
                                       self.hkv, eps)
-            self._attend(li, residual, attn, m, dec_parts, shared, qkv=qkv)
+            # x = None: with qkv precomputed _attend reads no activations (the residual
+            # here is not normalised)
+            self._attend(li, None, attn, m, dec_parts, shared, qkv=qkv)
             ops.rows_residual_add(attn, lw["o"], residual)
             act = ops.rows_swiglu_normx(residual, lw["gate_up"], eps)
             ops.rows_residual_add(act, lw["down"], residual)
@@ -400,6 +409,7 @@ class DecoderLM:
         lw = self.w["layers"][li]
         kc, vc = self.kv_k[li], self.kv_v[li]
         if qkv is None:
+            assert x is not None, "_attend: activations required without a precomputed qkv"
             qkv = ops.qkv_rope(x[:T], lw["qkv"], m.positions, self.cos_sin, m.slot_mapping, kc,
                                vc, hq, hkv)
         if shared is not None:

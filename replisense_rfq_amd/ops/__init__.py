@@ -25,6 +25,7 @@ __all__ = [
     "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT", "SPLITK_PERSIST",
     "ROWS_BIT", "ROWS_MAX_M", "ROWS_CFGS", "ROWS_CFGS_PAIRED", "rows_ok",
     "set_rows_best", "rows_rope_normx", "rows_swiglu_normx", "rows_residual_add", "fold_ok",
+    "kernel_errors",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -34,6 +35,16 @@ SKINNY_MAX_M = int(os.environ.get("RFQ_SKINNY_MAX_M", "64"))
 
 def native_available() -> bool:
     return _native.available()
+
+
+def kernel_errors() -> list[int]:
+    """Counts of the bounded in-launch waits that gave up (csrc/kernels/kerr.hip):
+    [stream-K slab waits, persistent decode stage waits, first failing persistent
+    (layer << 8 | stage) + 1].  The first call allocates the words (do it before any graph
+    capture); all zeros without the native library."""
+    if not _native.available():
+        return [0, 0, 0]
+    return list(torch.ops.rfq_amd.kernel_errors())
 
 
 def _gpu(t: torch.Tensor) -> bool:

@@ -137,6 +137,23 @@ def build_messages(raw_text: str) -> list[dict]:
             {"role": "user", "content": build_user_message(truncate(raw_text))}]
 
 
+# The reference's LLM client raises openai.APITimeoutError("Request timed out.") when
+# its 30 s timeout (rfq_agent.py:69) expires, and _generate_sync puts str(e) into the
+# error dict (rfq_agent.py:178-182).  Here the engine's deadline surfaces as
+# asyncio.TimeoutError / TimeoutError, whose str() is empty: map it to the client's
+# message so data.error is never blank.
+TIMEOUT_MESSAGE = "Request timed out."
+
+
+def error_text(e: BaseException) -> str:
+    """str(e) as the reference reports it, never empty."""
+    import asyncio
+
+    if isinstance(e, (TimeoutError, asyncio.TimeoutError)):
+        return str(e) or TIMEOUT_MESSAGE
+    return str(e) or type(e).__name__
+
+
 # ------------------------------------------------------------------- service
 class ExtractService:
     """Drop-in for RFQFieldGenerator with a pluggable inference backend."""
@@ -182,7 +199,7 @@ class ExtractService:
             return self._finish(reply, source_file, t0)
         except Exception as e:
             log.error("Exception during generation: %s", e)
-            return create_error_response(str(e))
+            return create_error_response(error_text(e))
 
     def generate(self, raw_text: str, source_file: str = "email-body") -> dict:
         return self._generate_sync(raw_text, source_file)
@@ -198,7 +215,7 @@ class ExtractService:
             return self._finish(reply, source_file, t0)
         except Exception as e:
             log.error("Exception during generation: %s", e)
-            return create_error_response(str(e))
+            return create_error_response(error_text(e))
 
 
 # ------------------------------------------------------------------ backends

@@ -89,3 +89,37 @@ def test_fold_norms_gpu_matches_plain_forward(gpu):
         lb = b.forward(_meta(T, gpu)).float()
         rel = (la - lb).norm() / la.norm()
         assert rel < 3e-2, (T, rel)
+
+
+def _decode_meta(tok, pos, device):
+    """One decode row at position ``pos`` of sequence 0 (KV blocks 0, 1)."""
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32)  # noqa: E731
+    m = dict(input_ids=i32([tok]), positions=i32([pos]), slot_mapping=i32([pos]), num_decode=1,
+             dec_block_tables=i32([[0, 1]]), dec_q_start=i32([0]), dec_q_len=i32([1]),
+             dec_kv_len=i32([pos + 1]), dec_work_seq=i32([0]), dec_work_ct=i32([0]),
+             logits_idx=torch.tensor([0], dtype=torch.int64))
+    return ForwardMeta(**{k: (v.to(device) if isinstance(v, torch.Tensor) else v)
+                          for k, v in m.items()})
+
+
+def test_fold_norms_logits_parity_prefill_then_decode():
+    """the fold rounds W' = bf16(W diag(g)) once, so it is not bit-exact; pin
+    the logits of the folded model (prefill on the plain forward with unit norms, then
+    decode steps on _forward_fold) against the unfolded model over a whole sequence:
+    relative L2 error <= 2e-2 per step and the same greedy token on every step."""
+    torch.manual_seed(0)
+    a, b = _pair("cpu")
+    T = 12
+    la = a.forward(_meta(T, "cpu")).float()
+    lb = b.forward(_meta(T, "cpu")).float()
+    assert (la - lb).norm() / la.norm() < 2e-2
+    tok = int(la[-1].argmax())
+    for step in range(6):
+        ma, mb = _decode_meta(tok, T + step, "cpu"), _decode_meta(tok, T + step, "cpu")
+        assert b._fold_step(mb, 1)
+        la = a.forward(ma).float()
+        lb = b.forward(mb).float()
+        rel = (la - lb).norm() / la.norm()
+        assert rel < 2e-2, (step, rel)
+        assert int(la.argmax()) == int(lb.argmax()), step
+        tok = int(la.argmax())

@@ -179,3 +179,22 @@ def test_router_custom_allreduce_error_restarts_on_rccl(monkeypatch):
         assert router.restarts == 1
     finally:
         router.shutdown()
+
+
+def test_timed_out_request_reports_a_nonempty_error():
+    """the reference's 30 s LLM timeout (rfq_agent.py:69) surfaces as
+    openai's APITimeoutError("Request timed out.") inside the error dict
+    (rfq_agent.py:178-182).  The engine's deadline raises asyncio.TimeoutError, whose
+    str() is empty; the service must still report a non-empty error."""
+    from replisense_rfq_amd.service.extract import TIMEOUT_MESSAGE, error_text
+
+    eng = LLMEngine(_cfg())
+    eng.faults = FaultInjector(",".join(f"step_sleep:{eng.num_steps + i}:300" for i in range(4)))
+    aeng = AsyncEngine(eng)
+    svc = ExtractService(EngineBackend(eng, aeng, timeout_s=0.5))
+    out = asyncio.run(svc.generate_async(synth.make_rfq(12).text, "email-body"))
+    assert out["success"] is False and out["error"] == TIMEOUT_MESSAGE
+    assert out["missing_fields"] == ["all"] and out["source_file"] == "unknown"
+    assert error_text(asyncio.TimeoutError()) == TIMEOUT_MESSAGE
+    assert error_text(ValueError("bad")) == "bad"
+    aeng.shutdown()
