@@ -10,6 +10,7 @@
 #include <stdint.h>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 namespace rfq {
 typedef uint16_t bf16_t;
@@ -90,6 +91,15 @@ void launch_gemm_w4_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t
                             int, int64_t, bool, hipStream_t);
 int64_t car_signal_bytes();
 uint32_t* kernel_error_words(hipStream_t);
+int decode_persist_counter_words(int);
+int decode_persist_lds_bytes(int, int, int);
+int decode_persist_grid();
+void launch_decode_persist_op(const int64_t*, int, int, int, int, int, int, int, int, bf16_t*,
+                              bf16_t*, int, bf16_t*, bf16_t*, const int32_t*, const float*,
+                              const int32_t*, int, const int32_t*, int, const int32_t*,
+                              const int32_t*, const int32_t*, const int32_t*, const int32_t*, int,
+                              int, float*, float*, int32_t*, float, uint32_t*, float, int,
+                              hipStream_t);
 uint32_t kernel_error_read(int);
 hipError_t car_alloc(int64_t, void**);
 void launch_car_oneshot(char* const*, int, int, const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -768,6 +778,74 @@ void car_ipc_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<vo
 
 int64_t car_data_offset() { return rfq::car_signal_bytes(); }
 
+// Persistent decode layers (decode_persist.hip): [counter words, LDS bytes, grid] for a
+// launch of nst stages at M tokens, hidden d and widest stage input Kx.
+std::vector<int64_t> decode_persist_info(int64_t M, int64_t d, int64_t Kx, int64_t nst) {
+  return {(int64_t)rfq::decode_persist_counter_words((int)nst),
+          (int64_t)rfq::decode_persist_lds_bytes((int)M, (int)d, (int)Kx),
+          (int64_t)rfq::decode_persist_grid()};
+}
+
+void decode_persist(const Tensor& residual, const Tensor& layers, const Tensor& qbuf,
+                    const Tensor& attn, const Tensor& act, const Tensor& positions,
+                    const Tensor& cos_sin, const Tensor& slots, const Tensor& block_tables,
+                    const Tensor& q_start, const Tensor& q_len, const Tensor& kv_len,
+                    const Tensor& work_seq, const Tensor& work_ct, const Tensor& part_o,
+                    const Tensor& part_ml, const Tensor& tickets, const Tensor& counters,
+                    int64_t l0, int64_t l1, int64_t stages, int64_t Hq, int64_t Hkv, int64_t F,
+                    int64_t BS, int64_t splits, double scale, double eps, int64_t flags) {
+  CHECK_DEV(residual); CHECK_BF16(residual); CHECK_BF16(qbuf); CHECK_BF16(attn); CHECK_BF16(act);
+  CHECK_I32(positions); CHECK_I32(slots); CHECK_I32(block_tables); CHECK_I32(q_start);
+  CHECK_I32(q_len); CHECK_I32(kv_len); CHECK_I32(work_seq); CHECK_I32(work_ct);
+  CHECK_I32(tickets); CHECK_I32(counters);
+  TORCH_CHECK(residual.is_contiguous() && residual.dim() == 2, "decode_persist: residual [M, d]");
+  const int64_t M = residual.size(0), d = residual.size(1);
+  TORCH_CHECK(M >= 1 && M <= 4, "decode_persist: 1 <= M <= 4 tokens");
+  TORCH_CHECK(d % 512 == 0 && (Hq * 128) % 512 == 0 && F % 512 == 0,
+              "decode_persist: d, Hq * 128 and F must be multiples of 512");
+  TORCH_CHECK(Hkv >= 1 && Hq % Hkv == 0 && Hq / Hkv <= 16, "decode_persist: GQA group <= 16");
+  TORCH_CHECK(layers.scalar_type() == at::kLong && layers.is_cuda() && layers.dim() == 2 &&
+              layers.size(1) == 8 && layers.is_contiguous(), "decode_persist: layers [L, 8] int64");
+  TORCH_CHECK(0 <= l0 && l0 < l1 && l1 <= layers.size(0), "decode_persist: layer range");
+  TORCH_CHECK(stages > 0 && stages < 32, "decode_persist: stage mask in [1, 31]");
+  TORCH_CHECK(qbuf.dim() == 2 && qbuf.stride(1) == 1 && qbuf.size(0) >= M &&
+              qbuf.size(1) >= Hq * 128, "decode_persist: qbuf [M, >= Hq * 128]");
+  TORCH_CHECK(attn.is_contiguous() && attn.size(0) >= M && attn.size(1) == Hq * 128,
+              "decode_persist: attn [M, Hq * 128]");
+  TORCH_CHECK(act.is_contiguous() && act.size(0) >= M && act.size(1) == F, "decode_persist: act [M, F]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == 128,
+              "decode_persist: cos_sin fp32 [max_pos, 128]");
+  TORCH_CHECK(positions.numel() >= M && slots.numel() >= M, "decode_persist: positions / slots");
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.stride(1) == 1, "decode_persist: block tables");
+  const int64_t W = work_seq.numel();
+  TORCH_CHECK(work_ct.numel() == W && W >= 1, "decode_persist: work list");
+  TORCH_CHECK(splits >= 1 && splits <= 16, "decode_persist: 1 <= splits <= 16");
+  if (splits > 1) {
+    TORCH_CHECK(part_o.numel() >= M * Hq * splits * 128 && part_ml.numel() >= M * Hq * splits * 2,
+                "decode_persist: split partial buffers too small");
+    TORCH_CHECK(tickets.numel() >= W * Hkv, "decode_persist: ticket buffer too small");
+  }
+  int nper = 0;
+  for (int i = 0; i < 5; ++i) nper += (stages >> i) & 1;
+  const int64_t nst = (l1 - l0) * nper;
+  TORCH_CHECK(counters.numel() >= rfq::decode_persist_counter_words((int)nst),
+              "decode_persist: counter buffer too small");
+  const int64_t Kx = std::max<int64_t>(Hq * 128, F);
+  TORCH_CHECK(rfq::decode_persist_lds_bytes((int)M, (int)d, (int)Kx) <= 160 * 1024,
+              "decode_persist: the step's rows do not fit in LDS (M * (d + max(Hq*128, F)))");
+  rfq::launch_decode_persist_op(
+      reinterpret_cast<const int64_t*>(layers.data_ptr()), (int)l0, (int)l1, (int)stages, (int)M,
+      (int)d, (int)Hq, (int)Hkv, (int)F, bpm(residual), bpm(qbuf), (int)qbuf.stride(0), bpm(attn),
+      bpm(act), positions.data_ptr<int32_t>(), cos_sin.data_ptr<float>(), slots.data_ptr<int32_t>(),
+      (int)BS, block_tables.data_ptr<int32_t>(), (int)block_tables.stride(0),
+      q_start.data_ptr<int32_t>(), q_len.data_ptr<int32_t>(), kv_len.data_ptr<int32_t>(),
+      work_seq.data_ptr<int32_t>(), work_ct.data_ptr<int32_t>(), (int)W, (int)splits,
+      splits > 1 ? part_o.data_ptr<float>() : nullptr,
+      splits > 1 ? part_ml.data_ptr<float>() : nullptr, tickets.data_ptr<int32_t>(), (float)scale,
+      reinterpret_cast<uint32_t*>(counters.data_ptr<int32_t>()), (float)eps, (int)flags,
+      cur_stream());
+}
+
 // Error words of the bounded in-launch waits (csrc/kernels/kerr.hip): allocated by the
 // first call (the engine calls it at start-up, before any graph capture); returns the
 // slots' counts (all 0 when no GPU / nothing allocated).
@@ -1019,6 +1097,13 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("car_ipc_close(int ptr) -> ()", &car_ipc_close);
   m.def("car_data_offset() -> int", &car_data_offset);
   m.def("kernel_errors() -> int[]", &kernel_errors);
+  m.def("decode_persist_info(int M, int d, int Kx, int nst) -> int[]", &decode_persist_info);
+  m.def("decode_persist(Tensor(a!) residual, Tensor layers, Tensor(b!) qbuf, Tensor(c!) attn, "
+        "Tensor(d!) act, Tensor positions, Tensor cos_sin, Tensor slots, Tensor block_tables, "
+        "Tensor q_start, Tensor q_len, Tensor kv_len, Tensor work_seq, Tensor work_ct, "
+        "Tensor(e!) part_o, Tensor(f!) part_ml, Tensor(g!) tickets, Tensor(h!) counters, int l0, "
+        "int l1, int stages, int Hq, int Hkv, int F, int BS, int splits, float scale, float eps, "
+        "int flags) -> ()");
   m.def("car_error(int ptr) -> int", &car_error);
   m.def("car_error_info(int ptr) -> int", &car_error_info);
   m.def("moe_skinny(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
@@ -1075,6 +1160,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("skinny_gemm_rope", &skinny_gemm_rope);
   m.impl("skinny_gemm_swiglu", &skinny_gemm_swiglu);
   m.impl("gemv_rows", &gemv_rows);
+  m.impl("decode_persist", &decode_persist);
   m.impl("gemv_rows_swiglu", &gemv_rows_swiglu);
   m.impl("gemv_rows_rope", &gemv_rows_rope);
   m.impl("gemv_splitk", &gemv_splitk);

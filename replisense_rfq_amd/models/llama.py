@@ -46,6 +46,19 @@ from .weights import init_weights
 SINGLE_PASS_DECODE = os.environ.get("RFQ_SINGLE_PASS_DECODE", "auto").lower()
 
 
+# RFQ_PERSIST: persistent decode layers (csrc/kernels/decode_persist.hip) for steps whose
+# rows are all decode / short-extend rows, at most PERSIST_MAX_M of them, on folded norm
+# weights:
+#   "1" / "all"  every layer of the step in ONE launch (qkv -> attention -> o -> gate|up ->
+#                down, next layer ...; each stage's first weights in flight across its seam)
+#   "ao"         per layer: the qkv and MLP row-streaming launches, with attention + o in
+#                one persistent launch (the o weights stream while the attention runs)
+#   "0"          off: the multi-launch path (_forward_fold)
+PERSIST = os.environ.get("RFQ_PERSIST", "0").lower()
+PERSIST_MAX_M = 4
+PERSIST_FLAGS = int(os.environ.get("RFQ_PERSIST_FLAGS", "0"))
+
+
 @dataclass
 class ForwardMeta:
     """Device-side description of one engine step (all int32 unless noted)."""
@@ -111,6 +124,11 @@ class DecoderLM:
         self.norms_folded = False       # fold_norms: attn / mlp RMSNorm weights in qkv / gate|up
         self.single_pass = (SINGLE_PASS_DECODE in ("1", "on", "true")
                             or (SINGLE_PASS_DECODE == "auto" and self.hq // self.hkv <= 4))
+        self.persist = PERSIST if PERSIST in ("0", "1", "all", "ao") else "0"
+        self._persist_tab = None        # int64 [L, 8] device table of layer pointers
+        self._persist_key = None
+        self._persist_tk = None         # split-merge tickets of the persistent attention
+        self._persist_cnt = None        # seam counters (zeroed; each launch re-zeroes them)
 
     # ------------------------------------------------------------ folded norms
     def fold_norms(self) -> bool:
@@ -132,7 +150,7 @@ class DecoderLM:
         reduction left in a decode layer (2 launches fewer per layer).  Dense models at
         TP = 1 only (RFQ_NORM_FOLD=0 turns it off); the final norm before the LM head
         stays.  Returns whether the weights were folded."""
-        if (self.norms_folded or self.cfg.is_moe or self.tp.enabled
+        if (self.norms_folded or self.cfg.is_moe or (self.tp.enabled and not self.tp.emulated)
                 or os.environ.get("RFQ_NORM_FOLD", "1") == "0"):
             return self.norms_folded
         with torch.no_grad():
@@ -144,6 +162,90 @@ class DecoderLM:
                 lw["mlp_norm"] = torch.ones_like(lw["mlp_norm"])
         self.norms_folded = True
         return True
+
+    # ------------------------------------------------------- persistent decode layers
+    def _persist_step(self, m: "ForwardMeta", T: int) -> bool:
+        """Run this step through _forward_persist (RFQ_PERSIST): GPU, folded norms, dense,
+        every row a decode / short-extend row (no prefill section), at most PERSIST_MAX_M
+        rows, no cascade attention, row-major projections, no real collectives (TP = 1 or
+        the one-GPU rank emulation), and the step's rows fit the kernel's LDS."""
+        if self.persist == "0" or not self.norms_folded or self.device.type != "cuda":
+            return False
+        if self.tp.enabled and not self.tp.emulated:
+            return False
+        if m.num_prefill_tokens or T < 1 or T > PERSIST_MAX_M or T != m.num_decode:
+            return False
+        if 0 < ops.SHARED_PREFIX_MIN_ROWS <= m.num_decode or m.decode_splits > 16:
+            return False
+        lw = self.w["layers"][0]
+        if any(ops.tiled_only(lw[k]) for k in ("qkv", "o", "gate_up", "down")):
+            return False
+        d, qd, F = self.cfg.hidden, self.hq * self.cfg.head_dim, self.ffn_local
+        if d % 512 or qd % 512 or F % 512:
+            return False
+        mm = 1 if T <= 1 else 2 if T <= 2 else 4
+        return 2112 + mm * (d + max(qd, F)) * 2 <= 160 * 1024
+
+    def _persist_state(self):
+        """Layer pointer table, tickets and counters of the persistent launch (built once,
+        outside graph capture: the engine's warm-up step runs before any capture)."""
+        layers = self.w["layers"]
+        key = (self.kv_k.data_ptr(), self.kv_v.data_ptr(),
+               tuple(lw[k].data_ptr() for lw in layers for k in ("qkv", "o", "gate_up", "down")))
+        if self._persist_key != key:
+            rows = [[lw["qkv"].data_ptr(), lw["o"].data_ptr(), lw["gate_up"].data_ptr(),
+                     lw["down"].data_ptr(), self.kv_k[li].data_ptr(), self.kv_v[li].data_ptr(),
+                     0, 0] for li, lw in enumerate(layers)]
+            self._persist_tab = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            self._persist_key = key
+        if self._persist_tk is None:
+            self._persist_tk = torch.zeros(4096 * self.hkv, dtype=torch.int32, device=self.device)
+            qd = self.hq * self.cfg.head_dim
+            words, _, _ = ops.decode_persist_info(1, self.cfg.hidden, max(qd, self.ffn_local),
+                                                  self.cfg.n_layers * 5)
+            self._persist_cnt = torch.zeros(words, dtype=torch.int32, device=self.device)
+        return self._persist_tab, self._persist_tk, self._persist_cnt
+
+    def _forward_persist(self, m: ForwardMeta) -> torch.Tensor:
+        """Small decode step on the persistent kernel (csrc/kernels/decode_persist.hip):
+        "all" runs every layer in one launch, "ao" keeps qkv / MLP on the row-streaming
+        launches and fuses attention + o per layer.  Same numerics as _forward_fold except
+        the attention's split boundaries (one wave per (kv head, split), in-kernel merge)."""
+        cfg, w = self.cfg, self.w
+        T = m.num_tokens
+        eps, L = cfg.rms_eps, cfg.n_layers
+        qd, F = self.hq * cfg.head_dim, self.ffn_local
+        tab, tk, cnt = self._persist_state()
+        residual = ops.embed(m.input_ids[:T], w["embed"])
+        attn = torch.empty((T, qd), dtype=self.dtype, device=self.device)
+        act = torch.empty((T, F), dtype=self.dtype, device=self.device)
+        S = max(1, m.decode_splits)
+        if S > 1:
+            po = torch.empty(T * self.hq * S * 128, device=self.device)
+            pm = torch.empty(T * self.hq * S * 2, device=self.device)
+        else:
+            po = pm = torch.empty(1, device=self.device)
+        meta = (m.positions, self.cos_sin, m.slot_mapping, m.dec_block_tables, m.dec_q_start,
+                m.dec_q_len, m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, po, pm, tk, cnt)
+        if self.persist == "ao":
+            for li in range(L):
+                lw = w["layers"][li]
+                qkv = ops.rows_rope_normx(residual, lw["qkv"], m.positions, self.cos_sin,
+                                          m.slot_mapping, self.kv_k[li], self.kv_v[li], self.hq,
+                                          self.hkv, eps)
+                ops.decode_persist(residual, tab, qkv, attn, act, *meta, li, li + 1,
+                                   ops.PERSIST_ATTN | ops.PERSIST_O, self.hq, self.hkv, F,
+                                   self.kv_k.shape[3], S, self.scale, eps, PERSIST_FLAGS)
+                a = ops.rows_swiglu_normx(residual, lw["gate_up"], eps)
+                ops.rows_residual_add(a, lw["down"], residual)
+        else:
+            qbuf = torch.empty((T, qd), dtype=self.dtype, device=self.device)
+            ops.decode_persist(residual, tab, qbuf, attn, act, *meta, 0, L, ops.PERSIST_STAGES,
+                               self.hq, self.hkv, F, self.kv_k.shape[3], S, self.scale, eps,
+                               PERSIST_FLAGS)
+        x = ops.rms_norm(residual, w["final_norm"], eps)
+        xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
+        return ops.linear(xs, w["lm_head"])
 
     def _fold_step(self, m: "ForwardMeta", T: int) -> bool:
         """Run this step through _forward_fold: folded weights, a small step whose
@@ -247,6 +349,8 @@ class DecoderLM:
 
         if self.tp.enabled and 0 < self.sp_min_tokens <= T:
             return self._forward_sp(m)
+        if self._persist_step(m, T):
+            return self._forward_persist(m)
         if self._fold_step(m, T):
             return self._forward_fold(m)
         h = ops.embed(m.input_ids[:T], w["embed"])

@@ -25,7 +25,7 @@ __all__ = [
     "register_tiled", "tiled_of", "tiled_only", "clear_tiled", "SPLITK_TILED", "SPLITK_NT", "SPLITK_PERSIST",
     "ROWS_BIT", "ROWS_MAX_M", "ROWS_CFGS", "ROWS_CFGS_PAIRED", "rows_ok",
     "set_rows_best", "rows_rope_normx", "rows_swiglu_normx", "rows_residual_add", "fold_ok",
-    "kernel_errors",
+    "kernel_errors", "decode_persist", "decode_persist_info", "PERSIST_STAGES",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -45,6 +45,32 @@ def kernel_errors() -> list[int]:
     if not _native.available():
         return [0, 0, 0]
     return list(torch.ops.rfq_amd.kernel_errors())
+
+
+# Persistent decode layers (csrc/kernels/decode_persist.hip): stage bits
+PERSIST_QKV, PERSIST_ATTN, PERSIST_O, PERSIST_GU, PERSIST_DOWN = 1, 2, 4, 8, 16
+PERSIST_STAGES = 31
+
+
+def decode_persist_info(M: int, d: int, Kx: int, nst: int) -> tuple[int, int, int]:
+    """(counter words, LDS bytes, grid) of a persistent launch of ``nst`` stages."""
+    return tuple(_native.ops().decode_persist_info(M, d, Kx, nst))
+
+
+def decode_persist(residual, layers, qbuf, attn, act, positions, cos_sin, slots, block_tables,
+                   q_start, q_len, kv_len, work_seq, work_ct, part_o, part_ml, tickets, counters,
+                   l0, l1, stages, Hq, Hkv, F, BS, splits, scale, eps, flags=0) -> None:
+    """Layers [l0, l1) of a small decode step in one launch (GPU only): qkv + RoPE + KV
+    append -> attention + split merge -> o (+= residual) -> gate|up + SwiGLU -> down
+    (+= residual), each stage present in the ``stages`` mask.  ``layers`` is the int64
+    [L, 8] device table of (qkv, o, gate_up, down, k_cache, v_cache, 0, 0) pointers; the
+    norms are folded into qkv / gate|up (DecoderLM.fold_norms).  ``residual`` [M, d] is
+    updated in place; ``counters`` (int32 zeros, decode_persist_info words) are left
+    zeroed by the launch."""
+    _native.ops().decode_persist(residual, layers, qbuf, attn, act, positions, cos_sin, slots,
+                                 block_tables, q_start, q_len, kv_len, work_seq, work_ct,
+                                 part_o, part_ml, tickets, counters, l0, l1, stages, Hq, Hkv, F,
+                                 BS, splits, scale, eps, flags)
 
 
 def _gpu(t: torch.Tensor) -> bool:

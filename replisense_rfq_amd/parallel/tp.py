@@ -27,6 +27,7 @@ class TPContext:
     group: object = None
     car: object = None            # CustomAllReduce (RFQ_CUSTOM_AR, on by default)
     car_status: str = ""          # why the custom all-reduce is (not) in use
+    emulated = False              # EmulatedTP: every collective is a local no-op
 
     @property
     def enabled(self) -> bool:
@@ -167,6 +168,8 @@ class EmulatedTP(TPContext):
     its local work (residual add + RMSNorm); the all-reduce itself, whose xGMI cost
     is priced separately, is skipped, and the sampler's partial all-gather copies this
     rank's partials into every slot."""
+
+    emulated = True
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         return t

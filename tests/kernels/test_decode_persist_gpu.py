@@ -1,0 +1,135 @@
+"""Persistent decode layers (csrc/kernels/decode_persist.hip) against the multi-launch
+small-step path they replace (DecoderLM._forward_fold / the plain forward), on one GPU.
+
+The GEMV stages accumulate in gemv_rows.hip's per-lane order, so the KV entries the qkv
+stage appends are compared bit for bit; the attention splits its keys per (kv head,
+split) unit like attn_decode.hip, so logits are compared with a relative tolerance.
+Shapes: tiny-llama, the 8B layer shape and the 70B TP=8 rank shape (2 layers each, small
+vocab), decode batches of 1-4 sequences and 1-4-token extends of one sequence, 1 / 4 / 16
+splits, the whole step in one launch ("all") and attention + o per layer ("ao").
+Repeated launches must give identical results (the seam counters are re-zeroed by every
+launch), also when replayed from a captured hipGraph."""
+import copy
+from dataclasses import replace
+
+import pytest
+import torch
+
+from replisense_rfq_amd import ops
+from replisense_rfq_amd.models.config import LLAMA3_8B, ModelConfig, get_config
+from replisense_rfq_amd.models.llama import DecoderLM, ForwardMeta
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {
+    "tiny": get_config("tiny-llama"),
+    "8b": replace(LLAMA3_8B, name="8b-2l", n_layers=2, vocab_size=4096),
+    "70b-tp8-rank": ModelConfig("70b-rank-2l", vocab_size=4096, hidden=8192, n_layers=2,
+                                n_heads=8, n_kv_heads=1, ffn=3584),
+}
+CTX = 70
+
+
+def _models(cfg, device, nblocks, mode):
+    torch.manual_seed(0)
+    a = DecoderLM(cfg, device, seed=5)
+    for lw in a.w["layers"]:
+        lw["attn_norm"].copy_((1 + 0.2 * torch.randn_like(lw["attn_norm"].float())).to(torch.bfloat16))
+        lw["mlp_norm"].copy_((1 + 0.2 * torch.randn_like(lw["mlp_norm"].float())).to(torch.bfloat16))
+    w = dict(a.w)
+    w["layers"] = [{k: t.clone() for k, t in lw.items()} for lw in a.w["layers"]]
+    b = DecoderLM(cfg, device, weights=w)
+    shape = (cfg.n_layers, nblocks, a.hkv, 32, 128)
+    g = torch.Generator(device=device).manual_seed(7)
+    kk = torch.randn(shape, generator=g, device=device).to(torch.bfloat16)
+    vv = torch.randn(shape, generator=g, device=device).to(torch.bfloat16)
+    a.attach_kv_cache(kk.clone(), vv.clone())
+    b.attach_kv_cache(kk.clone(), vv.clone())
+    assert a.fold_norms() and b.fold_norms()
+    a.persist, b.persist = "0", mode
+    return a, b
+
+
+def _meta(cfg, hq, hkv, T, batch, splits, device):
+    """T decode rows: `batch` = True -> T sequences of one query each, False -> one sequence
+    extending by T tokens.  Every sequence has CTX cached tokens before the step."""
+    nb = (CTX + T + 31) // 32
+    G = hq // hkv
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32, device=device)  # noqa: E731
+    g = torch.Generator().manual_seed(T * 10 + batch)
+    ids = torch.randint(0, cfg.vocab_size, (T,), generator=g, dtype=torch.int32).to(device)
+    if batch:
+        pos = [CTX] * T
+        slots = [(i * nb + CTX // 32) * 32 + CTX % 32 for i in range(T)]
+        bt = [[i * nb + j for j in range(nb)] for i in range(T)]
+        qs, ql, kvl = list(range(T)), [1] * T, [CTX + 1] * T
+        ws, wct = list(range(T)), [0] * T
+    else:
+        pos = [CTX + t for t in range(T)]
+        slots = [(p // 32) * 32 + p % 32 for p in pos]
+        bt = [list(range(nb))]
+        qs, ql, kvl = [0], [T], [CTX + T]
+        tiles = (T * G + 15) // 16
+        ws, wct = [0] * tiles, list(range(tiles))
+    return ForwardMeta(
+        input_ids=ids, positions=i32(pos), slot_mapping=i32(slots), num_decode=T,
+        dec_block_tables=i32(bt), dec_q_start=i32(qs), dec_q_len=i32(ql), dec_kv_len=i32(kvl),
+        dec_work_seq=i32(ws), dec_work_ct=i32(wct),
+        logits_idx=torch.arange(T, dtype=torch.int64, device=device), decode_splits=splits)
+
+
+def _rel(x, y):
+    return float((x.float() - y.float()).norm() / y.float().norm().clamp_min(1e-6))
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("mode", ["all", "ao"])
+def test_persist_matches_multi_launch(gpu, shape, mode):
+    ops.reset_plans()
+    cfg = SHAPES[shape]
+    errs0 = ops.kernel_errors()
+    for batch in (True, False):
+        for T in (1, 2, 3, 4):
+            nblocks = T * ((CTX + T + 31) // 32) + 1
+            a, b = _models(cfg, gpu, nblocks, mode)
+            for splits in (1, 4, 16):
+                m = _meta(cfg, a.hq, a.hkv, T, batch, splits, gpu)
+                assert b._persist_step(m, T), (shape, T)
+                la = a.forward(m)
+                lb = b.forward(m)
+                torch.cuda.synchronize()
+                # the qkv stage appends the same k / v as the row-streaming launch (bit for
+                # bit where the reference step runs it: T <= FOLD_MAX_M)
+                if T <= ops.FOLD_MAX_M:
+                    assert torch.equal(a.kv_k, b.kv_k) and torch.equal(a.kv_v, b.kv_v), \
+                        (shape, mode, batch, T, splits)
+                else:
+                    assert _rel(b.kv_k, a.kv_k) < 1e-2 and _rel(b.kv_v, a.kv_v) < 1e-2
+                assert _rel(lb, la) < 1e-2, (shape, mode, batch, T, splits, _rel(lb, la))
+                # a second launch over the same state gives the same logits (counters reset)
+                lb2 = b.forward(m)
+                torch.cuda.synchronize()
+                assert torch.equal(lb, lb2), (shape, mode, batch, T, splits)
+    assert ops.kernel_errors()[:2] == errs0[:2]
+
+
+def test_persist_graph_replay(gpu):
+    """A captured persistent step replays with the same result many times over."""
+    ops.reset_plans()
+    cfg = SHAPES["8b"]
+    a, b = _models(cfg, gpu, 8, "all")
+    m = _meta(cfg, a.hq, a.hkv, 1, True, 16, gpu)
+    ref = b.forward(m).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.forward(m)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = b.forward(m)
+    for _ in range(20):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert ops.kernel_errors()[1] == 0
