@@ -20,8 +20,8 @@
 // MI355X_MICROARCH.md 'prefetch-credit').
 //
 // Geometry: one workgroup of 4 waves per CU (grid = CUs, all resident), one wave per SIMD
-// with the whole 512-register file: two 16 KB weight groups in flight per wave (128 KB per
-// CU) and the attention body without spills.
+// with the whole 512-register file: three 16 KB weight groups in flight per wave (192 KB
+// per CU) and the attention body without spills.
 // Work of a stage is dealt to the 4 x CUs waves with consecutive units on different CUs:
 // wave slot gw = wave * CUs + workgroup; unit U goes to slot U % slots.
 //
@@ -31,7 +31,7 @@
 // of every 1 KB chunk of the row (non-temporal), the stage's input rows come from LDS
 // (staged once per workgroup per stage), v_dot2c_f32_bf16 accumulates, a DPP wave sum
 // reduces.  A wave streams its (unit, chunk) items in groups of 16 loads (16 KB),
-// double-buffered; the first two groups of a stage are the ones prefetched across the seam.
+// three groups in flight; the first three groups of a stage are prefetched across the seam.
 // Per-lane accumulation order = gemv_rows.hip's, so each projection is bit-identical to
 // its row-streaming launch.
 //
@@ -46,7 +46,7 @@
 // its stores (vmcnt(0)), the workgroup meets at a barrier, one lane adds 1 to its shard
 // (workgroup % 8) of the seam's counter; wave 0 polls the 8 shards with sc1 loads until
 // they sum to the grid, then a barrier releases the workgroup; every load of handed-off
-// bytes is an sc1 load.  Waves issue the next stage's first two weight groups before they
+// bytes is an sc1 load.  Waves issue the next stage's first three weight groups before they
 // wait, so the stream keeps going through the seam; wave 0 polls first, except behind the
 // attention (its poll would wait behind its own prefetch: loads retire in order, and only
 // the attention seam is long enough to hide that).
@@ -113,7 +113,9 @@ struct DpArgs {
   uint32_t* cnt;                 // seam counters (see dp_cnt), abort and exit words
   uint32_t* err;                 // kernel_error_words (may be null)
   float eps;
-  int flags;                     // bit 0: wave 0 prefetches too (A/B)
+  int flags;                     // A/B and timing bits: 1 wave 0 prefetches too, 2 no
+                                 // cross-seam prefetch, 4 attention units skipped (timing),
+                                 // 8 rotated chunk start per wave
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(const void* p, int bytes) {
@@ -122,6 +124,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(const void* p, int byt
 __device__ __forceinline__ u32x4 dp_ld16(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
 }
+// a pointer the compiler must treat as wave-uniform (buffer descriptors need SGPRs; a
+// VGPR-held base would make every buffer access a waterfall loop)
+template <typename T>
+__device__ __forceinline__ T* dp_uni(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ uint32_t* dp_cnt(uint32_t* cnt, int seam, int shard) {
   return cnt + (seam * kDpShards + shard) * kDpShardWords;
 }
@@ -129,7 +140,7 @@ __device__ __forceinline__ uint32_t* dp_cnt(uint32_t* cnt, int seam, int shard) 
 // ------------------------------------------------------------------ GEMV stages
 struct DpStage {
   const bf16_t* W;
-  int K, nunits, rstride;
+  int K, nunits, rstride, bytes;      // bytes: the whole weight (buffer range)
 };
 
 template <int EPI>
@@ -139,36 +150,37 @@ __device__ __forceinline__ int dp_row0(int U) {
 }
 
 // A wave's items are (unit i, chunk c), units U = gw + i * nwt, walked in order by two
-// cursors (issue, consume).  A group is exactly 16 loads: past the last item the issue
-// cursor stays on it (harmless re-loads), so the compiler's wait counts stay static.
+// cursors (issue, consume).  Weight loads are buffer loads over the whole weight (uniform
+// descriptor and byte offset, lane * 16 in the VGPR): a group is always 16 load
+// instructions -- past the wave's last item the offset leaves the buffer's range, the
+// load returns zeros and moves no bytes -- so the compiler's wait counts stay static.
 struct DpCur {
   int i, c;
 };
 
-template <int EPI>
-__device__ __forceinline__ const bf16_t* dp_rowp(const DpStage& s, int U, int lane) {
-  return s.W + (int64_t)dp_row0<EPI>(U) * s.K + lane * 8;
-}
+constexpr int kDpOob = 0x7ffffff0;      // byte offset past every weight's range
 
 template <int EPI>
 __device__ __forceinline__ void dp_issue(u32x4 (&b)[kDpLoads], const DpStage& s, int gw, int nwt,
-                                         DpCur& cur, int nu, int nch, int lane) {
+                                         DpCur& cur, int nu, int nch, int rot, int lane) {
   constexpr int NR = EPI == kEpRes ? 1 : 2;
   constexpr int CU = kDpLoads / NR;
-  const bf16_t* p = dp_rowp<EPI>(s, gw + cur.i * nwt, lane);
-  const int64_t rs = (int64_t)s.rstride * s.K;
+  const __amdgpu_buffer_rsrc_t wr = dp_rsrc(dp_uni(s.W), s.bytes);
+  const int rsb = s.rstride * s.K * 2;
 #pragma unroll
   for (int t = 0; t < CU; ++t) {
+    const bool live = cur.i < nu;
+    const int row = dp_row0<EPI>(gw + cur.i * nwt);
+    const int ch = cur.c + rot < nch ? cur.c + rot : cur.c + rot - nch;
+    // the item's offset rides in the VGPR offset (no per-load SGPR), past the end out of range
+    const int off = live ? row * s.K * 2 + ch * 1024 + lane * 16 : kDpOob;
 #pragma unroll
     for (int r = 0; r < NR; ++r)
-      b[t * NR + r] = __builtin_nontemporal_load(
-          reinterpret_cast<const u32x4*>(p + r * rs + cur.c * 512));
-    if (cur.c + 1 < nch) {
-      ++cur.c;
-    } else if (cur.i + 1 < nu) {
+      b[t * NR + r] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, live ? off + r * rsb : kDpOob, 0, kNt));
+    if (++cur.c == nch) {
       cur.c = 0;
       ++cur.i;
-      p = dp_rowp<EPI>(s, gw + cur.i * nwt, lane);
     }
   }
 }
@@ -230,11 +242,14 @@ __device__ __forceinline__ void dp_epilogue(float (&acc)[2][MM], const float (&r
     } else if (e.my_slot >= 0) {
       const bool is_k = h < a.Hq + a.Hkv;
       const int kvh = is_k ? h - a.Hq : h - a.Hq - a.Hkv;
+      // the row differs per lane (token): global sc1 stores with a per-lane address.  A
+      // buffer store would need a per-lane descriptor, i.e. a waterfall loop -- and hipcc
+      // (ROCm 7.2) reloads the loop's address registers from AGPR spill slots inside it
+      // and overwrote the address after the first lane group (illegal access at M >= 2)
       bf16_t* dst = (is_k ? e.kc : e.vc) +
                     (((int64_t)(e.my_slot / a.BS) * a.Hkv + kvh) * a.BS + e.my_slot % a.BS) * 128;
-      const __amdgpu_buffer_rsrc_t cr = dp_rsrc(dst, 256);
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(o1), cr, dd * 2, 0, kSc1);
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(o2), cr, (64 + dd) * 2, 0, kSc1);
+      __hip_atomic_store(dst + dd, f2bf(o1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + 64 + dd, f2bf(o2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -245,7 +260,7 @@ template <int MM, int EPI>
 __device__ __forceinline__ void dp_consume(const u32x4 (&b)[kDpLoads], float (&acc)[2][MM],
                                            const float (&rs)[MM], const bf16_t* x_l, int K,
                                            int gw, int nwt, DpCur& cur, int& left, int nch,
-                                           const DpEpi& e, int lane) {
+                                           int rot, const DpEpi& e, int lane) {
   constexpr int NR = EPI == kEpRes ? 1 : 2;
   constexpr int CU = kDpLoads / NR;
 #pragma unroll
@@ -253,9 +268,10 @@ __device__ __forceinline__ void dp_consume(const u32x4 (&b)[kDpLoads], float (&a
     if (left <= 0) break;                         // wave-uniform
     --left;
     u32x4 x[MM];
+    const int ch = cur.c + rot < nch ? cur.c + rot : cur.c + rot - nch;
 #pragma unroll
     for (int m = 0; m < MM; ++m)
-      x[m] = *reinterpret_cast<const u32x4*>(x_l + m * K + cur.c * 512 + lane * 8);
+      x[m] = *reinterpret_cast<const u32x4*>(x_l + m * K + ch * 512 + lane * 8);
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -279,13 +295,19 @@ __device__ __forceinline__ int dp_units(int nunits, int gw, int nwt) {
   return gw < nunits ? (nunits - gw + nwt - 1) / nwt : 0;
 }
 
-// The body of one GEMV stage for this wave, after its input rows are in LDS: bA holds
-// group 0 when `prefetched` (issue cursor `ic` then points past it).  normx: scale by
+// The body of one GEMV stage for this wave, after its input rows are in LDS.  Groups
+// rotate through a ring of three 16 KB register buffers: every consume has the two
+// younger groups in flight (48 KB per wave, 192 KB per CU), and the consumed buffer is
+// refilled with the group three ahead right away.  Every group is 16 loads (out-of-range
+// past the end), so the loop is one static body and the compiler's wait counts are exact.
+// With `prefetched` the first three groups are already in flight (issued across the
+// seam; the issue cursor `ic` then points past them).  normx: scale by
 // rsqrt(mean(x^2) + eps) per token (folded RMSNorm, gemv_rows.hip kRwNormX).
 template <int MM, int EPI>
-__device__ __forceinline__ void dp_gemv(u32x4 (&bA)[kDpLoads], u32x4 (&bB)[kDpLoads], int npre,
-                                        DpCur ic, const DpStage& s, const bf16_t* x_l,
-                                        bool normx, float eps, int gw, int nwt, const DpEpi& e,
+__device__ __forceinline__ void dp_gemv(u32x4 (&bA)[kDpLoads], u32x4 (&bB)[kDpLoads],
+                                        u32x4 (&bC)[kDpLoads], bool prefetched, DpCur ic,
+                                        const DpStage& s, const bf16_t* x_l, bool normx,
+                                        float eps, int gw, int nwt, int rot, const DpEpi& e,
                                         int lane) {
   const int nu = dp_units(s.nunits, gw, nwt);
   if (nu == 0) return;
@@ -294,9 +316,11 @@ __device__ __forceinline__ void dp_gemv(u32x4 (&bA)[kDpLoads], u32x4 (&bB)[kDpLo
   constexpr int CU = kDpLoads / NR;
   const int nitems = nu * nch;
   const int ngroups = (nitems + CU - 1) / CU;
-  if (npre == 0) {
+  if (!prefetched) {
     ic = DpCur{0, 0};
-    dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, lane);
+    dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_issue<EPI>(bB, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_issue<EPI>(bC, s, gw, nwt, ic, nu, nch, rot, lane);
   }
   float rs[MM];
 #pragma unroll
@@ -321,38 +345,52 @@ __device__ __forceinline__ void dp_gemv(u32x4 (&bA)[kDpLoads], u32x4 (&bB)[kDpLo
     for (int m = 0; m < MM; ++m) acc[r][m] = 0.f;
   DpCur cc{0, 0};
   int left = nitems;
-  for (int g = 0; g < ngroups; g += 2) {
-    if (g + 1 < ngroups && (g > 0 || npre < 2)) dp_issue<EPI>(bB, s, gw, nwt, ic, nu, nch, lane);
-    dp_consume<MM, EPI>(bA, acc, rs, x_l, K, gw, nwt, cc, left, nch, e, lane);
-    if (g + 1 >= ngroups) break;
-    if (g + 2 < ngroups) dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, lane);
-    dp_consume<MM, EPI>(bB, acc, rs, x_l, K, gw, nwt, cc, left, nch, e, lane);
+  for (int g = 0; g < ngroups; g += 3) {
+    dp_consume<MM, EPI>(bA, acc, rs, x_l, K, gw, nwt, cc, left, nch, rot, e, lane);
+    dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_consume<MM, EPI>(bB, acc, rs, x_l, K, gw, nwt, cc, left, nch, rot, e, lane);
+    dp_issue<EPI>(bB, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_consume<MM, EPI>(bC, acc, rs, x_l, K, gw, nwt, cc, left, nch, rot, e, lane);
+    dp_issue<EPI>(bC, s, gw, nwt, ic, nu, nch, rot, lane);
   }
 }
 
-// stage the step's rows of `src` ([M, n] bf16, row stride ld) into LDS [MM][n] with sc1
-// loads (bytes of this launch), rows past M zero
+// stage the step's rows of up to two sources ([M, n] bf16, row stride ld) into LDS
+// [MM][n] with sc1 loads (bytes of this launch), rows past M zero: every load of both is
+// issued before the LDS stores, so the staging costs one memory round trip
 template <int MM>
-__device__ __forceinline__ void dp_stage_rows(bf16_t* dst, const bf16_t* src, int ld, int n,
+__device__ __forceinline__ void dp_stage_rows(bf16_t* dst0, const bf16_t* src0, int ld0, int n0,
+                                              bf16_t* dst1, const bf16_t* src1, int ld1, int n1,
                                               int M) {
   constexpr int U = 8;                  // loads in flight per thread before the LDS stores
-  const int per = n >> 3, total = MM * per;
-  const __amdgpu_buffer_rsrc_t r = dp_rsrc(src, M * ld * 2);
+  const int per0 = n0 >> 3, tot0 = MM * per0;
+  const int per1 = n1 >> 3, total = tot0 + MM * per1;
+  const __amdgpu_buffer_rsrc_t r0 = dp_rsrc(src0, M * ld0 * 2);
+  const __amdgpu_buffer_rsrc_t r1 = dp_rsrc(src1 != nullptr ? src1 : src0,
+                                            src1 != nullptr ? M * ld1 * 2 : 0);
   for (int base = threadIdx.x; base < total; base += U * kDpThreads) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = base + u * kDpThreads;
-      const int m = i / per, c = i - m * per;
       v[u] = (u32x4){0u, 0u, 0u, 0u};
-      if (i < total && m < M) v[u] = dp_ld16(r, (m * ld + c * 8) * 2);
+      if (i < tot0) {
+        const int m = i / per0, c = i - m * per0;
+        if (m < M) v[u] = dp_ld16(r0, (m * ld0 + c * 8) * 2);
+      } else if (i < total) {
+        const int j = i - tot0, m = j / per1, c = j - m * per1;
+        if (m < M) v[u] = dp_ld16(r1, (m * ld1 + c * 8) * 2);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = base + u * kDpThreads;
-      if (i < total) {
-        const int m = i / per, c = i - m * per;
-        *reinterpret_cast<u32x4*>(dst + m * n + c * 8) = v[u];
+      if (i < tot0) {
+        const int m = i / per0, c = i - m * per0;
+        *reinterpret_cast<u32x4*>(dst0 + m * n0 + c * 8) = v[u];
+      } else if (i < total) {
+        const int j = i - tot0, m = j / per1, c = j - m * per1;
+        *reinterpret_cast<u32x4*>(dst1 + m * n1 + c * 8) = v[u];
       }
     }
   }
@@ -405,11 +443,13 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
     const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
     const int np = pg_last - pg0 + 1;
     int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
+    bf16_t* const kc = dp_uni(L.kc);
+    bf16_t* const vc = dp_uni(L.vc);
     auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
-      const int64_t page = pg_next;
+      const int64_t page = __builtin_amdgcn_readfirstlane(pg_next);
       pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
-      const __amdgpu_buffer_rsrc_t kr = dp_rsrc(L.kc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
-      const __amdgpu_buffer_rsrc_t vr_ = dp_rsrc(L.vc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
+      const __amdgpu_buffer_rsrc_t kr = dp_rsrc(kc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
+      const __amdgpu_buffer_rsrc_t vr_ = dp_rsrc(vc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -602,11 +642,12 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
 
 // ------------------------------------------------------------------ the kernel
 __device__ __forceinline__ DpStage dp_desc(const DpArgs& a, const DpLayer& L, int st) {
+  const int nq = (a.Hq + 2 * a.Hkv) * 128;
   switch (st) {
-    case kDpQkv: return DpStage{L.wqkv, a.d, (a.Hq + 2 * a.Hkv) * 64, 64};
-    case kDpO: return DpStage{L.wo, a.Hq * kD, a.d, 0};
-    case kDpGu: return DpStage{L.wgu, a.d, a.F, a.F};
-    default: return DpStage{L.wd, a.F, a.d, 0};
+    case kDpQkv: return DpStage{L.wqkv, a.d, nq / 2, 64, nq * a.d * 2};
+    case kDpO: return DpStage{L.wo, a.Hq * kD, a.d, 0, a.d * a.Hq * kD * 2};
+    case kDpGu: return DpStage{L.wgu, a.d, a.F, a.F, 2 * a.F * a.d * 2};
+    default: return DpStage{L.wd, a.F, a.d, 0, a.d * a.F * 2};
   }
 }
 
@@ -677,31 +718,34 @@ __device__ __forceinline__ bool dp_gemv_stage(const DpArgs& a, const DpLayer& L,
                                               bf16_t* res_l, bf16_t* x_l, const DpEpi& e,
                                               int wave, int gw, int nwt, int lane) {
   const DpStage s = dp_desc(a, L, st);
-  u32x4 bA[kDpLoads], bB[kDpLoads];
-  int npre = 0;
+  u32x4 bA[kDpLoads], bB[kDpLoads], bC[kDpLoads];
+  bool pre = false;
   DpCur ic{0, 0};
   const int nu = dp_units(s.nunits, gw, nwt);
-  // the first two groups' weight loads go out before the seam settles (wave 0 polls
+  // flags bit 3: each wave starts its rows at chunk gw % nch (rotating), so the waves of a
+  // stage do not all read the same 1 KB column of their rows at once after a seam
+  const int rot = (a.flags & 8) ? gw % (s.K >> 9) : 0;
+  // the first three groups' weight loads go out before the seam settles (wave 0 polls
   // first, except behind the attention or with flags bit 0)
-  if (!aborted && nu > 0 && (wave != 0 || after_attn || (a.flags & 1))) {
-    constexpr int CU = kDpLoads / (EPI == kEpRes ? 1 : 2);
+  if (!aborted && nu > 0 && !(a.flags & 2) && (wave != 0 || after_attn || (a.flags & 1))) {
     const int nch = s.K >> 9;
-    dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, lane);
-    npre = 1;
-    if (nu * nch > CU) {
-      dp_issue<EPI>(bB, s, gw, nwt, ic, nu, nch, lane);
-      npre = 2;
-    }
+    dp_issue<EPI>(bA, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_issue<EPI>(bB, s, gw, nwt, ic, nu, nch, rot, lane);
+    dp_issue<EPI>(bC, s, gw, nwt, ic, nu, nch, rot, lane);
+    pre = true;
   }
   if (k > 0) aborted = dp_wait(a, k - 1, l, st, ctl, abort_w, wave, lane);
   if (aborted) return true;
   // the input rows (and, for o / down, the residual the epilogue adds to) into LDS
-  dp_stage_rows<MM>(res_l, a.residual, a.d, a.d, a.M);
-  if (st == kDpO) dp_stage_rows<MM>(x_l, a.attn, a.Hq * kD, a.Hq * kD, a.M);
-  if (st == kDpDown) dp_stage_rows<MM>(x_l, a.act, a.F, a.F, a.M);
+  if (st == kDpO)
+    dp_stage_rows<MM>(res_l, a.residual, a.d, a.d, x_l, a.attn, a.Hq * kD, a.Hq * kD, a.M);
+  else if (st == kDpDown)
+    dp_stage_rows<MM>(res_l, a.residual, a.d, a.d, x_l, a.act, a.F, a.F, a.M);
+  else
+    dp_stage_rows<MM>(res_l, a.residual, a.d, a.d, nullptr, nullptr, 0, 0, a.M);
   __syncthreads();
   const bool nx = EPI != kEpRes;
-  dp_gemv<MM, EPI>(bA, bB, npre, ic, s, nx ? res_l : x_l, nx, a.eps, gw, nwt, e, lane);
+  dp_gemv<MM, EPI>(bA, bB, bC, pre, ic, s, nx ? res_l : x_l, nx, a.eps, gw, nwt, rot, e, lane);
   return false;
 }
 
@@ -740,7 +784,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_persist_kernel(DpArgs a)
       if (!((a.stages >> st) & 1)) continue;
       if (st == kDpAttn) {
         if (k > 0) aborted = dp_wait(a, k - 1, l, st, ctl, abort_w, wave, lane);
-        if (!aborted) {
+        if (!aborted && !(a.flags & 4)) {
           // units (w, kvh, split) on wave slots; the V tiles reuse the LDS rows
           const int nu = a.W * a.Hkv * a.splits;
           bf16_t* v_lds = res_l + wave * (kDpVTile / 2);

@@ -105,7 +105,11 @@ def test_persist_matches_multi_launch(gpu, shape, mode):
                         (shape, mode, batch, T, splits)
                 else:
                     assert _rel(b.kv_k, a.kv_k) < 1e-2 and _rel(b.kv_v, a.kv_v) < 1e-2
-                assert _rel(lb, la) < 1e-2, (shape, mode, batch, T, splits, _rel(lb, la))
+                # T <= FOLD_MAX_M: the reference runs the same row-streaming GEMVs (only the
+                # attention differs); above it, the plain forward's GEMMs (the fold test's
+                # 3e-2 bound for that path)
+                tol = 1e-2 if T <= ops.FOLD_MAX_M else 3e-2
+                assert _rel(lb, la) < tol, (shape, mode, batch, T, splits, _rel(lb, la))
                 # a second launch over the same state gives the same logits (counters reset)
                 lb2 = b.forward(m)
                 torch.cuda.synchronize()

@@ -77,6 +77,9 @@ def main():
             decode_splits=a.splits)
         ref = None
         for mode in a.modes.split(","):
+            if mode.startswith(("raw:", "rows:")):
+                bench_parts(model, m, mode, a, cfg, ctx)
+                continue
             model.persist = mode
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -107,6 +110,75 @@ def main():
                               "rel_vs_first": round(rel, 5),
                               "kernel_errors": ops.kernel_errors()}), flush=True)
             del graph
+
+
+def bench_parts(model, m, mode, a, cfg, ctx):
+    """Timing pieces: ``raw:<mask>`` = one persistent launch of every layer with only the
+    stages in <mask> (1 qkv, 2 attention, 4 o, 8 gate|up, 16 down; no embed / LM head);
+    ``rows:<qkv|o|gu|down|attn>`` = the same projection on its multi-launch kernel for every
+    layer (the fold path's row-streaming GEMVs / decode attention)."""
+    import torch
+
+    from replisense_rfq_amd import ops
+
+    T = m.num_tokens
+    w = model.w
+    eps = cfg.rms_eps
+    qd, F = model.hq * cfg.head_dim, model.ffn_local
+    res = torch.randn((T, cfg.hidden), device=model.device).to(torch.bfloat16)
+    attn = torch.randn((T, qd), device=model.device).to(torch.bfloat16) * 0.1
+    act = torch.randn((T, F), device=model.device).to(torch.bfloat16) * 0.1
+    qbuf = torch.randn((T, qd), device=model.device).to(torch.bfloat16)
+    tab, tk, cnt = model._persist_state()
+    S = m.decode_splits
+    po = torch.empty(T * model.hq * S * 128, device=model.device)
+    pm = torch.empty(T * model.hq * S * 2, device=model.device)
+    kind, arg = mode.split(":")
+
+    def body():
+        if kind == "raw":
+            ops.decode_persist(res, tab, qbuf, attn, act, m.positions, model.cos_sin,
+                               m.slot_mapping, m.dec_block_tables, m.dec_q_start, m.dec_q_len,
+                               m.dec_kv_len, m.dec_work_seq, m.dec_work_ct, po, pm, tk, cnt, 0,
+                               cfg.n_layers, int(arg), model.hq, model.hkv, F,
+                               model.kv_k.shape[3], S, model.scale, eps, a.flags)
+            return
+        for li in range(cfg.n_layers):
+            lw = w["layers"][li]
+            if arg == "qkv":
+                ops.rows_rope_normx(res, lw["qkv"], m.positions, model.cos_sin, m.slot_mapping,
+                                    model.kv_k[li], model.kv_v[li], model.hq, model.hkv, eps)
+            elif arg == "o":
+                ops.rows_residual_add(attn, lw["o"], res)
+            elif arg == "gu":
+                ops.rows_swiglu_normx(res, lw["gate_up"], eps)
+            elif arg == "down":
+                ops.rows_residual_add(act, lw["down"], res)
+            elif arg == "attn":
+                model._attend(li, None, attn, m, (po, pm), None, qkv=qbuf)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        body()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        graph.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(json.dumps({"shape": a.shape, "layers": cfg.n_layers, "ctx": ctx, "T": T,
+                      "splits": S, "mode": mode, "flags": a.flags, "ms": round(ms, 4),
+                      "us_per_layer": round(1000 * ms / cfg.n_layers, 2),
+                      "kernel_errors": ops.kernel_errors()}), flush=True)
 
 
 if __name__ == "__main__":
