@@ -113,6 +113,9 @@ def parse():
                     help="70B phase: single requests over the reference's 14 recorded prompts "
                          "(a fixed set; fewer if the phase budget runs out)")
     ap.add_argument("--tp-latency-runs", type=int, default=14)
+    ap.add_argument("--pdf-set", type=int, default=12,
+                    help="multi-page PDF RFQs past the 8,000-char cap run one at a time in "
+                         "the 70B phase (BASELINE config 4, prefill-heavy); 0 = off")
     ap.add_argument("--tp-docs", type=int, default=256,
                     help="TP phase: documents timed in a continuous stream (0 = skip)")
     ap.add_argument("--tp-in-flight", type=int, default=128,
@@ -611,7 +614,7 @@ def main():
             mark("phase:70b")
             out["phases"]["llama3_70b"] = ph.model_phase(
                 args.big_model, seed=args.seed, latency_runs=args.big_latency_runs,
-                budget_s=left(), in_flight=8, reference_set=True,
+                budget_s=left(), in_flight=8, reference_set=True, pdf_set=args.pdf_set,
                 # one request at a time: decode graphs / start-up plans for one sequence
                 # (M = 1..8 with jump-forward extends) -- the 64-row plans took 86 s
                 graph_buckets=(1,),

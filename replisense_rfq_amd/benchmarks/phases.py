@@ -30,8 +30,8 @@ import statistics
 import threading
 import time
 
-from .stream import (DocStream, latency, latency_reference, loaded_latency, pcts, single_stream,
-                     validate)
+from .stream import (DocStream, latency, latency_pdf_set, latency_reference, loaded_latency, pcts,
+                     single_stream, validate)
 
 BASELINE_P50_S = 0.883            # Groq llama3-70b p50 server time per request
 # uvicorn closes an idle keep-alive connection after 5 s by default; the open-loop
@@ -621,7 +621,7 @@ def depth_phase(engine, in_flight: int, warm_docs: int, docs: int, budget_s: flo
 def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 0,
                 docs: int = 0, latency_runs: int = 0, formats: tuple | None = None,
                 budget_s: float = 120.0, parse_procs: int = 4, reference_set: bool = False,
-                **cfg_over) -> dict:
+                pdf_set: int = 0, **cfg_over) -> dict:
     """Build ``model`` on this GPU, then (a) ``latency_runs`` idle single requests and
     (b) a closed-loop stream of ``docs`` documents at ``in_flight`` after
     ``warm_docs`` of warm-up; free everything before returning."""
@@ -666,6 +666,10 @@ def model_phase(model: str, seed: int = 0, in_flight: int = 0, warm_docs: int = 
                         + REFERENCE_SAMPLED_STEPS_P50 / ss["sampled_steps_per_s_p50"], 4)
                 res["per_row"] = [{"row": a, "sampled": b, "tokens": c, "prompt": d,
                                    "s": round(t, 3)} for (a, b, c, d), t in zip(rows, lat)]
+            if pdf_set and time.perf_counter() < deadline - 30.0:
+                # BASELINE config 4's prefill-heavy documents
+                res["pdf_set"] = latency_pdf_set(eng, pdf_set,
+                                                 deadline=deadline - 10.0 if docs else deadline)
         elif latency_runs:
             lat, detail = latency(eng, 0, latency_runs)
             res["p50_parse_text_latency_s"] = round(statistics.median(lat), 4)

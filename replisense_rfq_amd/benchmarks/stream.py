@@ -506,6 +506,73 @@ def latency_reference(engine, runs: int = 14, deadline: float | None = None):
     return out, detail, rows
 
 
+PDF_SET_SEEDS = tuple(range(9000, 9012))
+
+
+def pdf_set_requests(n: int = 12) -> list[dict]:
+    """BASELINE config 4's prefill-heavy workload: a FIXED set of
+    multi-page PDF RFQs (utils/synth.make_long_rfq, rendered by utils/docgen) whose
+    parsed text (service/parser.py, the reference's file_parser.py contract) runs past the
+    8,000-character cap of rfq_agent.py:147-149.  Returns the chat messages, the parsed
+    text length, the page count and the item hint per document."""
+    import os
+    import tempfile
+    from pathlib import Path
+
+    from ..service.hints import estimate_line_items
+    from ..service.parser import FileParser
+    from ..service.prompt import build_messages, truncate
+    from ..utils import docgen, synth
+
+    out = []
+    for seed in PDF_SET_SEEDS[:n]:
+        d = synth.make_long_rfq(seed)
+        p = Path(tempfile.gettempdir()) / f"rfq_pdfset_{os.getpid()}_{seed}.pdf"
+        p.write_bytes(docgen.rfq_attachment(d, "pdf"))
+        try:
+            text = FileParser().parse_file(str(p))["raw_text"]
+        finally:
+            p.unlink(missing_ok=True)
+        out.append({"seed": seed, "messages": build_messages(text), "chars": len(text),
+                    "pages": text.count("=== Page "),
+                    "min_items": estimate_line_items(truncate(text))})
+    return out
+
+
+def latency_pdf_set(engine, n: int = 12, deadline: float | None = None) -> dict | None:
+    """Single-request latency over the fixed PDF set (one request at a time, bench hints
+    as for the reference set): TTFT (prefill of ~2.3-2.6 K new tokens after the shared
+    prefix) and end-to-end seconds per document."""
+    from ..engine.grammar import PROFILE_SYNTHETIC
+    from ..service.extract import parse_and_validate_response
+
+    tok = engine.tokenizer
+    rows = []
+    for r in pdf_set_requests(n):
+        if deadline is not None and time.perf_counter() > deadline:
+            break
+        t0 = time.perf_counter()
+        ids = tok.chat_ids(r["messages"])
+        params = engine.default_params(min_items=r["min_items"], profile=PROFILE_SYNTHETIC)
+        s, = engine.generate([ids], params)
+        res = parse_and_validate_response(engine.decode_text(s), "upload.pdf")
+        dt = time.perf_counter() - t0
+        rows.append({"seed": r["seed"], "pages": r["pages"], "chars": r["chars"],
+                     "prompt_tokens": len(ids), "prefix_hit": s.span().get("prefix_hit"),
+                     "ttft_ms": round(s.span().get("ttft_ms") or 0.0, 1),
+                     "sampled": s.num_sampled, "tokens": s.num_generated, "s": round(dt, 3),
+                     "valid": bool(res.get("success"))})
+    if not rows:
+        return None
+    med = lambda k: statistics.median(x[k] for x in rows)  # noqa: E731
+    return {"set": "multi-page PDF RFQs past the 8,000-char cap (synth.make_long_rfq seeds "
+                   f"{PDF_SET_SEEDS[0]}-{PDF_SET_SEEDS[-1]}), parsed by service/parser.py",
+            "docs": len(rows), "pages_p50": med("pages"), "chars_p50": med("chars"),
+            "prompt_tokens_p50": med("prompt_tokens"), "ttft_ms_p50": med("ttft_ms"),
+            "e2e_s_p50": round(med("s"), 4), "sampled_steps_p50": med("sampled"),
+            "valid": round(sum(x["valid"] for x in rows) / len(rows), 3), "per_doc": rows}
+
+
 def single_stream(detail):
     """Single-request decode rates (Groq 350 tok/s per stream): output
     tokens/s after the first token, and the sampled (non-jump-forward) step rate."""

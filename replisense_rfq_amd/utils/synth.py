@@ -158,6 +158,69 @@ def make_rfq(seed: int, n_items: int | None = None, style: str | None = None) ->
     return RFQDoc("\n".join(lines), company, email, contact, phone, supplier, city, items)
 
 
+TERMS = [
+    "Prices shall be quoted firm and fixed for the validity period stated in the offer and "
+    "shall include packing suitable for sea and road freight.",
+    "All goods shall be supplied new, of current manufacture, and traceable to the original "
+    "component manufacturer by lot and date code.",
+    "Partial shipments are acceptable only with prior written approval of the purchasing "
+    "department; each shipment shall carry the purchase order number on every package.",
+    "The supplier shall state the country of origin and the HS tariff code of every line "
+    "item together with the unit net weight.",
+    "Lead times shall be given in calendar days from receipt of the purchase order; "
+    "deviations from the requested delivery schedule shall be highlighted.",
+    "Alternative or equivalent parts may be offered only if clearly marked as alternates "
+    "with the full manufacturer part number and a datasheet link.",
+    "Quality documentation, including certificates of conformity and test reports, shall "
+    "accompany each delivery or be sent electronically before dispatch.",
+    "Warranty shall cover a minimum period of twenty-four months from the date of delivery "
+    "against defects in material and workmanship.",
+    "Invoices shall reference the purchase order and line numbers; payment terms are sixty "
+    "days net from receipt of a correct invoice.",
+    "The buyer reserves the right to award the order in whole or in part, or to reject any "
+    "offer without stating reasons.",
+]
+
+
+def make_long_rfq(seed: int, min_chars: int = 9000) -> RFQDoc:
+    """A multi-page formal RFQ whose text runs past the reference's 8,000-character
+    input cap (rfq_agent.py:147-149): letterhead, a long numbered item list and the
+    buyer's terms and conditions -- BASELINE config 4's "multi-page PDF RFQs
+    (prefill-heavy)".  Rendered as a PDF (docgen.rfq_attachment) it spans 4-5 pages;
+    the parsed text is truncated to 8,000 characters by the prompt builder, i.e. a
+    prompt of ~2.9 K tokens on the in-tree tokenizer (~2.4 K after the shared prefix)."""
+    base = make_rfq(seed, n_items=0, style="formal")
+    r = random.Random(seed * 7 + 1)
+    head = base.text.splitlines()[:7]
+    tail = base.text.splitlines()[7:]
+    items, lines = [], list(head)
+    lines.append("Section 1 - Items to be quoted")
+    i = 0
+    while True:
+        desc, pn = r.choice(ITEMS)
+        pn = f"{pn}-{r.randint(10, 99)}" if r.random() < 0.6 else pn
+        qty = r.choice([10, 25, 50, 100, 250, 500, 1000, 2500])
+        price = None if r.random() < 0.3 else round(r.uniform(0.05, 900), 2)
+        cur = r.choice(CURRENCIES) if price is not None else None
+        items.append(LineItem(pn, desc, qty, price, cur[0] if cur else None))
+        i += 1
+        tp = (" | Target price: " + dict(CURRENCIES)[cur[0]].format(price)) if price is not None else ""
+        lines.append(f"{i}. {desc} | P/N {pn} | Quantity: {qty} pcs | Delivery: "
+                     f"{_date(r)}{tp}")
+        if i >= 40 or len("\n".join(lines)) > min_chars * 0.6:
+            break
+    lines.append("Section 2 - Terms and conditions")
+    for k, t in enumerate(TERMS * 3, 1):
+        lines.append(f"2.{k} {t}")
+        if len("\n".join(lines + tail)) > min_chars:
+            break
+    lines.append("Section 3 - Required documents")
+    lines.append("; ".join(r.sample(DOCS, 4)) + ".")
+    lines += tail
+    return RFQDoc("\n".join(lines), base.client_name, base.client_email, base.client_contact,
+                  base.client_phone, base.rfq_to, base.delivery_location, items)
+
+
 def corpus(n: int, seed: int = 0) -> list[RFQDoc]:
     return [make_rfq(seed * 1_000_003 + i) for i in range(n)]
 

@@ -91,3 +91,17 @@ def test_pathological_grid_is_bounded():
     t = extract_tables(seg, glyphs, h)
     assert time.perf_counter() - t0 < 30.0
     assert len(t) == 1 and len(t[0]) == n - 1 and all(c == "x" for c in t[0][0])
+
+
+def test_pdf_set_is_multi_page_and_past_the_cap():
+    """the 70B phase's fixed PDF set (BASELINE config 4, prefill-heavy)
+    parses, through the service parser, to multi-page text past the 8,000-char cap of
+    rfq_agent.py:147-149, so every prompt carries the full truncated document."""
+    from replisense_rfq_amd.benchmarks.stream import pdf_set_requests
+    from replisense_rfq_amd.service.prompt import MAX_INPUT_CHARS
+
+    rs = pdf_set_requests(12)
+    assert len(rs) == 12 and len({r["seed"] for r in rs}) == 12
+    for r in rs:
+        assert r["chars"] > MAX_INPUT_CHARS and r["pages"] >= 3
+        assert r["messages"][1]["content"].endswith('... [truncated]\n"""')

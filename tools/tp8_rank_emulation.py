@@ -59,6 +59,9 @@ def main():
                     help="effective two-shot all-reduce bandwidth for prefill messages")
     ap.add_argument("--norm-us", type=float, default=4.9,
                     help="the emulated step's fused_add_rms_norm launch (rocprof window)")
+    ap.add_argument("--pdf-set", type=int, default=0,
+                    help="also prefill N multi-page PDF RFQs past the 8,000-char cap "
+                         "(benchmarks/stream.pdf_set_requests) and report their TTFT")
     ap.add_argument("--md", default="")
     ap.add_argument("--reproject", default="",
                     help="recompute the projection of an earlier run's JSON (no GPU)")
@@ -119,6 +122,21 @@ def main():
         res_runs.append({"prompt_tokens": s.prompt_len, "prefix_hit": s.prefix_hit_tokens,
                          "generated": n, "ttft_ms": round(1e3 * ttft, 2),
                          "step_ms": round(1e3 * (e2e - ttft) / max(1, n - 1), 3)})
+    pdf_rows = []
+    if a.pdf_set:
+        # BASELINE config 4's prefill-heavy documents: TTFT of ~2.4 K
+        # new tokens after the shared prefix, one request at a time
+        from replisense_rfq_amd.benchmarks.stream import pdf_set_requests
+
+        for j, r in enumerate(pdf_set_requests(a.pdf_set)):
+            ids = tok.chat_ids(r["messages"])
+            sp = SamplingParams(temperature=0.1, max_tokens=4, seed=j, grammar=False)
+            s, = eng.generate([ids], sp)
+            if gpu:
+                torch.cuda.synchronize()
+            pdf_rows.append({"seed": r["seed"], "pages": r["pages"], "prompt_tokens": s.prompt_len,
+                             "prefix_hit": s.prefix_hit_tokens,
+                             "ttft_ms": round(1e3 * (s.t_first_token - s.t_arrival), 2)})
     step = statistics.median(r["step_ms"] for r in res_runs)
     ttft = statistics.median(r["ttft_ms"] for r in res_runs)
     prefill_tokens = statistics.median(r["prompt_tokens"] - r["prefix_hit"] for r in res_runs)
@@ -135,6 +153,12 @@ def main():
            "hbm_floor_ms": round(w_bytes / 6.3e12 * 1e3, 3),
            "graph_steps": eng.stats().get("graph_steps"),
            "all_reduces_per_step": 2 * L, "steps_p50": a.steps_p50, "projection": proj}
+    if pdf_rows:
+        pf = statistics.median(r["prompt_tokens"] - r["prefix_hit"] for r in pdf_rows)
+        pttft = statistics.median(r["ttft_ms"] for r in pdf_rows)
+        out["pdf_set"] = {"docs": len(pdf_rows), "new_tokens_p50": pf, "rank0_ttft_ms_p50": pttft,
+                          "projection": project(step, pttft, pf, L, msg_decode, a),
+                          "per_doc": pdf_rows}
     print(json.dumps(out), flush=True)
     if a.md:
         write_md(a.md, proj)
