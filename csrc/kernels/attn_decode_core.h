@@ -87,10 +87,19 @@ __device__ __forceinline__ void attn_decode_body(
     }
   }
 
+  // MODE 0: split s takes the pages s, s + S, s + 2S, ... (interleaved): its first block-
+  // table entry does not depend on kv_len, so that scalar load goes out together with the
+  // kv_len / q_len loads and the first K / V page waits on one round trip fewer.  The
+  // cascade modes keep contiguous key ranges (their prefix boundary is a page count).
+  constexpr bool ILV = MODE == 0;
+  const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
+  int pg_next = 0;
+  if constexpr (ILV) pg_next = bt[__builtin_amdgcn_readfirstlane(min(split, bt_stride - 1))];
   int tps = (kvl - base + num_splits - 1) / num_splits;
   tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = base + split * tps;
-  const int end = min(kvl, start + tps);
+  const int npg_all = (kvl + kPage - 1) / kPage;
+  const int start = ILV ? split * kPage : base + split * tps;
+  const int end = ILV ? kvl : min(kvl, start + tps);
 
   float m_run[NT], l_run[NT];
   f32x4 o[NT][8];
@@ -114,18 +123,21 @@ __device__ __forceinline__ void attn_decode_body(
         if (!cvalid[t]) qf[t][ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
-    const int32_t* bt = block_tables + (int64_t)seq * bt_stride;
-    const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
-    const int np = pg_last - pg0 + 1;
+    // pages of this split: contiguous [pg0, pg_last], or interleaved pg0 + j * S
+    const int pstep = ILV ? num_splits : 1;
+    const int pg0 = start / kPage;
+    const int np = ILV ? (npg_all - split + num_splits - 1) / num_splits
+                       : (end - 1) / kPage - pg0 + 1;
+    const int pg_last = pg0 + (np - 1) * pstep;
     // block-table entries by wave-uniform (scalar, lgkmcnt-counted) loads, one page
     // ahead: a vector load here would make every page's K / V issue wait on vmcnt(0),
     // i.e. drain the page loads already in flight
-    int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
+    if constexpr (!ILV) pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
     // issue page j's K fragments (A operand: row = key, k = dh) and V rows (g + 4i,
     // chunk c) into registers; must be called with j = 0, 1, 2, ...
     auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
       const int64_t page = pg_next;
-      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
+      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + (j + 1) * pstep, pg_last))];
       const bf16_t* kb = k_cache + ((page * Hkv + kvh) * kPage) * kD;
       const bf16_t* vb = v_cache + ((page * Hkv + kvh) * kPage) * kD;
       if (NTK && pg0 + j >= kNtFromPage) {
@@ -147,8 +159,8 @@ __device__ __forceinline__ void attn_decode_body(
       }
     };
     auto process = [&](int j, const s16x8 (&kf)[2][4], const s16x8 (&vr)[8]) {
-      const int kt = start + j * kPage;
-      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1)
+      const int kt = start + j * pstep * kPage;
+      const int nvalid = end - kt;  // keys of this tile inside the split (>= 1; > 32 = all)
       // ---- V tile -> LDS (swizzled), rows past the split/context zeroed ----
 #pragma unroll
       for (int i = 0; i < 8; ++i) {

@@ -420,10 +420,12 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
   const int h = kvh * G + (cvalid ? col % G : 0);
   const int qrow = a.q_start[seq] + qi;
   const int lim = kvl - ql + qi + 1;                 // keys [0, lim) visible
-  int tps = (kvl + S - 1) / S;
-  tps = (tps + kPage - 1) / kPage * kPage;
-  const int start = split * tps;
-  const int end = min(kvl, start + tps);
+  // pages split, split + S, ... (interleaved, as attn_decode_core.h MODE 0)
+  const int32_t* bt = a.block_tables + (int64_t)seq * a.bt_stride;
+  int pg_next = bt[__builtin_amdgcn_readfirstlane(min(split, a.bt_stride - 1))];
+  const int npg_all = (kvl + kPage - 1) / kPage;
+  const int start = split * kPage;
+  const int end = kvl;
 
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[8];
@@ -439,15 +441,14 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
           s16x8, dp_ld16(qr, (qrow * a.ldq + h * kD + 32 * ks + 8 * g) * 2));
       if (!cvalid) qf[ks] = (s16x8){0, 0, 0, 0, 0, 0, 0, 0};
     }
-    const int32_t* bt = a.block_tables + (int64_t)seq * a.bt_stride;
-    const int pg0 = start / kPage, pg_last = (end - 1) / kPage;
-    const int np = pg_last - pg0 + 1;
-    int pg_next = bt[__builtin_amdgcn_readfirstlane(pg0)];
+    const int pg0 = split;
+    const int np = (npg_all - split + S - 1) / S;
+    const int pg_last = pg0 + (np - 1) * S;
     bf16_t* const kc = dp_uni(L.kc);
     bf16_t* const vc = dp_uni(L.vc);
     auto fetch = [&](int j, s16x8 (&kf)[2][4], s16x8 (&vr)[8]) {
       const int64_t page = __builtin_amdgcn_readfirstlane(pg_next);
-      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + j + 1, pg_last))];
+      pg_next = bt[__builtin_amdgcn_readfirstlane(min(pg0 + (j + 1) * S, pg_last))];
       const __amdgpu_buffer_rsrc_t kr = dp_rsrc(kc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
       const __amdgpu_buffer_rsrc_t vr_ = dp_rsrc(vc + ((page * Hkv + kvh) * kPage) * kD, kDpVTile);
 #pragma unroll
@@ -461,7 +462,7 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
         vr[i] = __builtin_bit_cast(s16x8, dp_ld16(vr_, ((g + 4 * i) * kD + 8 * c) * 2));
     };
     auto process = [&](int j, const s16x8 (&kf)[2][4], const s16x8 (&vr)[8]) {
-      const int kt = start + j * kPage;
+      const int kt = start + j * S * kPage;
       const int nvalid = end - kt;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {

@@ -387,10 +387,20 @@ def token_shape(seqs) -> dict:
     ``sampled_tokens_p50`` compare with the recorded rows' 341.5 / 160."""
     import statistics
 
+    from ..engine.grammar import PROFILE_SYNTHETIC, Limits
+
     n = max(1, len(seqs))
     gen = sum(s.num_generated for s in seqs)
     samp = sum(s.num_sampled for s in seqs)
+    # ADVICE r5: documents whose part-count hint exceeds the SYNTHETIC item cap decode
+    # fewer line items than they mention -- report how many
+    cap = Limits.from_env().max_items
+    synth = [s for s in seqs if s.params.profile == PROFILE_SYNTHETIC]
+    trunc = sum(1 for s in synth if s.params.min_items > cap)
     return dict(
+        items_hint_cap=cap,
+        items_hint_truncated_share=trunc / max(1, len(synth)),
+        items_hint_p50=statistics.median([s.params.min_items for s in synth]) if synth else 0,
         prompt_tokens=sum(s.prompt_len for s in seqs) / n,
         completion_tokens=gen / n,
         sampled_tokens=samp / n,

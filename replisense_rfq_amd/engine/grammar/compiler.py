@@ -125,29 +125,47 @@ class Op:
 class Limits:
     """Caps of the SYNTHETIC profile (0 = none).  The REFERENCE profile has none.
 
-    Calibrated to the reference's decode shape (VERDICT r4 item 3,
-    tests/engine/test_decode_shape.py): the 14 recorded completions
-    (cache_rows.json, rows 1-14) replayed through this grammar and tokenizer need 52.4 %
-    of their tokens SAMPLED (one engine step each), p50 160 sampled steps and 341.5
-    completion tokens.  A random-init model picks near-uniformly among the tokens a
-    state allows, and those are long code-like tokens (~7-8 characters), and it never
-    closes a string on its own -- so the character caps below are ~4x the recorded
-    field lengths (title ~36, names ~20, descriptions ~45 characters), which yields the
-    recorded token counts per field; the item array takes exactly the document's part
-    count (min_items) up to ``max_items`` = 3 (the recorded p50 is 3.5, one 23-item
-    outlier).  Random walks over the bench's documents then give ~0.49-0.50 sampled
-    share, p50 ~345-360 completion tokens and ~165-180 sampled steps."""
-    title: int = 144
-    field: int = 80
-    description: int = 176
-    part_number: int = 64
-    item_description: int = 112
+    Calibrated to the reference's decode shape: the 14
+    recorded completions (cache_rows.json, rows 1-14) replayed through this grammar and
+    tokenizer take p50 160 sampled steps (one engine step each) and p50 341.5 completion
+    tokens.  The caps are measured against the ENGINE itself -- the 8B bench's own
+    documents decoded by the random-init Llama-3-8B under Gumbel sampling at T = 0.1 on
+    one MI355X (profiles/r6_decode_shape.md, tests/assets/decode_shape_calibration.json):
+    a uniform random walk over the same grammar under-reads the engine's sampled steps by
+    ~20 % (163.5 vs 200 at the r5 caps), because a random-init model's picks follow its
+    context, not a uniform draw.  With the r5 caps x 0.72 below the engine decodes p50
+    ~158 sampled steps and ~345 completion tokens per document.  The item array takes
+    exactly the document's part count (min_items) up to ``max_items`` = 3 (the recorded
+    p50 is 3.5; the bench reports how many documents' hints exceed the cap:
+    per_doc.items_hint_truncated_share)."""
+    title: int = 104
+    field: int = 58
+    description: int = 127
+    part_number: int = 46
+    item_description: int = 81
     currency: int = 6
     max_items: int = 3
     max_docs: int = 2
-    doc: int = 80
+    doc: int = 58
     max_missing: int = 5
-    missing: int = 64
+    missing: int = 46
+
+    @classmethod
+    def from_env(cls) -> "Limits":
+        """Defaults, with the bench calibration knobs RFQ_SYNTH_CAP_SCALE (multiplies the
+        string caps) and RFQ_SYNTH_MAX_ITEMS (the line-item cap) when set."""
+        import os
+
+        lim = cls()
+        scale = float(os.environ.get("RFQ_SYNTH_CAP_SCALE", "1") or 1)
+        if scale != 1.0:
+            for f in ("title", "field", "description", "part_number", "item_description", "doc",
+                      "missing"):
+                setattr(lim, f, max(8, int(round(getattr(lim, f) * scale))))
+        items = os.environ.get("RFQ_SYNTH_MAX_ITEMS")
+        if items:
+            lim.max_items = int(items)
+        return lim
 
     def caps(self) -> list[int]:
         c = [0] * NCAP
@@ -389,7 +407,7 @@ class _Prog:
 
 def compile_rfq_grammar(tok, limits: Limits | None = None) -> CompiledGrammar:
     """Compile the RFQResponse schema (field order = rfq_agent.py:41-59) for `tok`."""
-    L = limits or Limits()
+    L = limits or Limits.from_env()
     P = _Prog(tok)
     quote = P.single('"')
     comma, rbrack, lbrace, lbrack = P.single(","), P.single("]"), P.single("{"), P.single("[")

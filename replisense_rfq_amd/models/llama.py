@@ -150,7 +150,11 @@ class DecoderLM:
         reduction left in a decode layer (2 launches fewer per layer).  Dense models at
         TP = 1 only (RFQ_NORM_FOLD=0 turns it off); the final norm before the LM head
         stays.  Returns whether the weights were folded."""
-        if (self.norms_folded or self.cfg.is_moe or (self.tp.enabled and not self.tp.emulated)
+        # TP > 1: only the one-GPU rank emulation with the persistent path folds (a real
+        # group's row-parallel epilogue is the all-reduce + add + RMSNorm kernel, so the
+        # emulation keeps that structure unless it runs the persistent layers)
+        tp_ok = not self.tp.enabled or (self.tp.emulated and self.persist != "0")
+        if (self.norms_folded or self.cfg.is_moe or not tp_ok
                 or os.environ.get("RFQ_NORM_FOLD", "1") == "0"):
             return self.norms_folded
         with torch.no_grad():

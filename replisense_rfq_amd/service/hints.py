@@ -39,7 +39,7 @@ def synthetic_item_limit() -> int:
     """The SYNTHETIC profile's line-item cap (engine/grammar/compiler.py Limits)."""
     from ..engine.grammar import Limits
 
-    return Limits().max_items
+    return Limits.from_env().max_items
 
 
 def estimate_line_items(text: str, limit: int = 8) -> int:

@@ -29,6 +29,8 @@ def test_persist_gate_cpu():
 def test_fold_allowed_for_emulated_tp_only():
     cfg = get_config("tiny-llama-tp")
     emu = DecoderLM(cfg, "cpu", tp=EmulatedTP(rank=0, world=2), seed=1)
-    assert emu.tp.emulated and emu.fold_norms()
+    assert emu.tp.emulated and not emu.fold_norms()      # multi-launch emulation: unfolded
+    emu.persist = "all"
+    assert emu.fold_norms()                              # persistent emulation: folded
     real = DecoderLM(cfg, "cpu", tp=TPContext(rank=0, world=2), seed=1)
     assert not real.tp.emulated and not real.fold_norms()
