@@ -32,9 +32,12 @@ class EngineConfig:
     kv_fraction: float = 0.85            # of free HBM for the paged KV pool (bench.py default)
     max_kv_blocks: int = 0               # 0 = from kv_fraction
     block_size: int = 32                 # tokens per KV page (kernel tile)
-    # sequences in flight per replica: the deepest the bench shows servable inside the
-    # 30 s request deadline on one MI355X (profiles/r3_depth_sweep.md; bench.py default)
-    max_num_seqs: int = 1536
+    # sequences in flight per replica.  The service default bounds latency: 160 in flight
+    # serves 58-60 docs/s at loaded p50 2.6 s / p99 3.8 s on one MI355X (the bench's
+    # latency_bounded_depth phase), where the throughput headline's 1,536 (bench.py
+    # --max-num-seqs, RFQ_MAX_BATCH=1536) gives ~109 docs/s but makes a saturated server
+    # hold every request ~14 s (profiles/r3_depth_sweep.md)
+    max_num_seqs: int = 160
     max_batched_tokens: int = 16384      # prefill chunk budget per step
     max_model_len: int = 8192            # llama3-70b-8192 context
     graph_buckets: tuple = (1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384,
