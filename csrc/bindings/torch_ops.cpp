@@ -88,7 +88,10 @@ void launch_gemm_dense(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, 
 void launch_gemm_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
                          int, int64_t, bool, hipStream_t);
 void launch_gemm_w4_grouped(const bf16_t*, const bf16_t*, bf16_t*, const int32_t*, int, int, int,
-                            int, int64_t, bool, hipStream_t);
+                            int, int64_t, bool, hipStream_t, float*, int, int);
+void launch_moe_combine_w2(const bf16_t*, const float*, int64_t, const int32_t*, int, int, int,
+                           const int32_t*, const float*, int, int, int, bf16_t*, int64_t,
+                           hipStream_t);
 int64_t car_signal_bytes();
 uint32_t* kernel_error_words(hipStream_t);
 int decode_persist_counter_words(int);
@@ -1040,10 +1043,47 @@ void moe_gemm_dense(const Tensor& x, const Tensor& w, const Tensor& out,
   TORCH_CHECK(!(cfg & 8) || K % 128 == 0, "moe_gemm_dense: the gemm_w4 form needs K % 128");
   if (cfg & 8)
     rfq::launch_gemm_w4_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
-                                x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
+                                x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream(), nullptr, 0, 0);
   else
     rfq::launch_gemm_grouped(bp(x), bp(w), bpm(out), expert_offsets.data_ptr<int32_t>(),
                              x.size(0) / 128, n_out, K, E, N, swiglu, cur_stream());
+}
+
+// Throughput-path w2 + top-k combine (gemm_w4.hip GROUPED KS = 2, moe.hip
+// moe_combine_w2_kernel): both kernels decide on the device, from the expert offsets and
+// `cus`, whether the GEMM runs two K slices into yf (fp32 [2, >= rows, N]) or one into y
+// (bf16 [rows, N]); the combine reads whichever was written.  cus <= 0: never split.
+void moe_w2_combine(const Tensor& x, const Tensor& w, const Tensor& y, const Tensor& yf,
+                    const Tensor& expert_offsets, const Tensor& inv_pos, const Tensor& weights,
+                    int64_t topk, const Tensor& out, int64_t cus) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_I32(expert_offsets);
+  CHECK_I32(inv_pos); CHECK_BF16(out); CHECK_ROWMAJOR(out);
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && y.is_contiguous() && yf.is_contiguous(),
+              "contiguous");
+  TORCH_CHECK(w.dim() == 3, "w must be [E, N, K]");
+  const int E = w.size(0), N = w.size(1), K = w.size(2);
+  TORCH_CHECK(x.size(1) == K && x.size(0) % 128 == 0, "moe_w2_combine: x [rows % 128, K]");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == N, "moe_w2_combine: y [rows, N]");
+  TORCH_CHECK(yf.scalar_type() == at::kFloat && yf.dim() == 3 && yf.size(0) == 2 &&
+                  yf.size(1) >= x.size(0) && yf.size(2) == N,
+              "moe_w2_combine: yf must be fp32 [2, >= rows, N]");
+  TORCH_CHECK(N % 256 == 0 && K % 256 == 0 && K >= 512,
+              "moe_w2_combine: N % 256, K % 256 (each K slice % 128), K >= 512");
+  TORCH_CHECK(out.size(1) == N && weights.scalar_type() == at::kFloat &&
+                  weights.size(0) == out.size(0) && weights.size(1) == topk &&
+                  inv_pos.numel() >= out.size(0) * topk,
+              "moe_w2_combine: out [T, N], weights fp32 [T, topk], inv_pos [T * topk]");
+  TORCH_CHECK(expert_offsets.numel() >= E + 1, "expert_offsets too short");
+  TORCH_CHECK((int64_t)x.size(0) * K < (int64_t)INT32_MAX && (int64_t)N * K < (int64_t)INT32_MAX,
+              "moe_w2_combine: offsets exceed int32");
+  const int tiles_n = N / 256;
+  rfq::launch_gemm_w4_grouped(bp(x), bp(w), bpm(y), expert_offsets.data_ptr<int32_t>(),
+                              x.size(0) / 128, N, K, E, N, false, cur_stream(),
+                              yf.data_ptr<float>(), (int)yf.size(1), (int)cus);
+  rfq::launch_moe_combine_w2(bp(y), yf.data_ptr<float>(), yf.stride(0),
+                             expert_offsets.data_ptr<int32_t>(), E, tiles_n, (int)cus,
+                             inv_pos.data_ptr<int32_t>(), weights.data_ptr<float>(),
+                             out.size(0), (int)topk, N, bpm(out), out.stride(0), cur_stream());
 }
 
 // out[t] = sum_k weights[t,k] * y[pos of (t,k)]
@@ -1145,6 +1185,8 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("gemm_dense(Tensor x, Tensor w, Tensor(a!) out, bool swiglu=False, int cfg=0) -> ()");
   m.def("moe_gemm_dense(Tensor x, Tensor w, Tensor(a!) out, Tensor expert_offsets, "
         "bool swiglu, int cfg=0) -> ()");
+  m.def("moe_w2_combine(Tensor x, Tensor w, Tensor(a!) y, Tensor(b!) yf, Tensor expert_offsets, "
+        "Tensor inv_pos, Tensor weights, int topk, Tensor(c!) out, int cus) -> ()");
   m.def("moe_skinny_splitk(Tensor x, Tensor sorted_ids, int topk, Tensor expert_offsets, Tensor w, "
         "Tensor(a!) yf, int max_rows, int splits) -> ()");
   m.def("moe_combine_splitk(Tensor yf, int splits, Tensor inv_pos, Tensor weights, int topk, "
@@ -1189,6 +1231,7 @@ TORCH_LIBRARY_IMPL(rfq_amd, CUDA, m) {
   m.impl("moe_combine", &moe_combine);
   m.impl("gemm_dense", &gemm_dense);
   m.impl("moe_gemm_dense", &moe_gemm_dense);
+  m.impl("moe_w2_combine", &moe_w2_combine);
   m.impl("moe_skinny_splitk", &moe_skinny_splitk);
   m.impl("moe_combine_splitk", &moe_combine_splitk);
 }

@@ -117,6 +117,24 @@ __device__ __forceinline__ void report_error(uint32_t* words, int slot) {
     __hip_atomic_fetch_add(words + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// MoE grouped GEMM enumeration (gemm_w4.hip GROUPED): 256-row chunks over the experts'
+// 128-row-padded segments.
+__device__ __forceinline__ int moe_live_chunks(const int32_t* offs, int E) {
+  int n = 0;
+  for (int e = 0; e < E; ++e) n += ((offs[e + 1] - offs[e]) / 128 + 1) >> 1;
+  return n;
+}
+
+// Split-K rule of the grouped w2 (gemm_w4.hip KS = 2, moe.hip moe_combine_w2_kernel):
+// two K slices when `tiles` 256x256 tiles leave the last round on `cus` CUs at most half
+// full within the first three rounds (measured: profiles/r6_mixtral_window.md).  Both
+// kernels evaluate it on the same offsets, so the combine reads what the GEMM wrote.
+__device__ __forceinline__ int moe_w2_ksplit(int tiles, int cus) {
+  if (cus <= 0) return 1;
+  const int full = tiles / cus, part = tiles - full * cus;
+  return (part > 0 && 2 * part <= cus && full <= 2) ? 2 : 1;
+}
+
 // Counter-based RNG (splitmix/murmur style finaliser) — deterministic per
 // (seed, row, column), identical on every TP rank for the same global column.
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint32_t a, uint32_t b) {

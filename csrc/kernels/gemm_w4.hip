@@ -78,29 +78,43 @@ typedef __attribute__((address_space(3))) char w4_lds_c;
 // live tiles are enumerated expert-major -> weight tile -> 256-row chunk from the
 // offsets, so no host sync and a grid fixed by the capacity (blocks past the live
 // tiles leave before any barrier).
+// KS = 2 (grouped store form only): split-K decided on the device.  From the live tile
+// count (expert offsets) every workgroup evaluates moe_w2_ksplit (common.h); with two
+// slices each tile's K range is cut in half, run by two adjacent workgroups, and slice s
+// writes its fp32 partial to slab s of outf ([2][M][ldo], M = the slab's rows); with one,
+// the bf16 store to `out` as KS = 1.  The top-k combine evaluates the same rule and reads
+// whichever was written (moe.hip moe_combine_w2_kernel).  For Mixtral's w2 at ~2,600-token
+// steps the grouped store has 1.5 rounds of 256x256 tiles on 256 CUs, a half-empty second
+// round; two K slices make it 3 half-length rounds (profiles/r6_mixtral_window.md).
 template <int EPI, int ABL = 0, bool SPREAD = false, bool EARLY = false, int MF = 16,
-          bool W3 = false, bool GROUPED = false>
+          bool W3 = false, bool GROUPED = false, int KS = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ w,
                     int64_t ldw, bf16_t* __restrict__ out, int64_t ldo, int M, int K, int up_off,
                     int tiles_m, int tiles_n, int group_m,
                     const int32_t* __restrict__ expert_offsets = nullptr, int E = 0,
-                    int64_t w_estride = 0) {
+                    int64_t w_estride = 0, float* __restrict__ outf = nullptr, int split_cus = 0) {
+  static_assert(KS == 1 || (KS == 2 && GROUPED && EPI == kW4Store && MF == 16),
+                "split-K: grouped fp32-partial store form only");
   extern __shared__ __attribute__((aligned(16))) char smem_w4[];
   w4_lds_c* const lds = (w4_lds_c*)smem_w4;
 
   // ---- block -> (row tile, weight tile): bijective XCD remap, then L2 groups
   int row0, tn, m_valid, m_store;         // first row, weight tile, rows readable / stored
+  int kslice = 0, nslice = 1;             // KS > 1: this workgroup's K slice, slices
   if constexpr (GROUPED) {
     constexpr int kB = 128;
-    int nchunks = 0;
-    for (int e = 0; e < E; ++e)
-      nchunks += ((expert_offsets[e + 1] - expert_offsets[e]) / kB + 1) >> 1;
-    const int nlive = nchunks * tiles_n;
+    const int nchunks = moe_live_chunks(expert_offsets, E);
+    if constexpr (KS > 1) nslice = moe_w2_ksplit(nchunks * tiles_n, split_cus);
+    const int nlive = nchunks * tiles_n * nslice;
     const int bid = blockIdx.x;
     if (bid >= nlive) return;               // before any barrier: the whole block leaves
     const int q8 = nlive >> 3, r8 = nlive & 7, xg = bid & 7;
-    const int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    int wg = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + (bid >> 3);
+    if (KS > 1 && nslice > 1) {
+      kslice = wg & 1;
+      wg >>= 1;
+    }
     int e = 0, p0 = 0, s0 = 0, nbe = 0, che = 0;
     for (; e < E; ++e) {
       s0 = expert_offsets[e] / kB;
@@ -117,6 +131,11 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     m_store = 2 * chunk + 1 < nbe ? 256 : 128;
     m_valid = min(expert_offsets[E] - row0, kW4M);
     w += (int64_t)e * w_estride;
+    if (KS > 1 && nslice > 1) {
+      K >>= 1;                              // rows keep their full strides ldx / ldw
+      x += (int64_t)kslice * K;
+      w += (int64_t)kslice * K;
+    }
   } else {
     const int nwg = tiles_m * tiles_n;
     const int bid = blockIdx.x;
@@ -435,7 +454,18 @@ void gemm_w4_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __r
     const int trow = 128 * wm + 16 * j + rr;
     if (trow >= m_store) continue;
     bf16_t* orow = out + (int64_t)(row0 + trow) * ldo;
-    if constexpr (EPI == kW4Swiglu) {
+    if (KS > 1 && nslice > 1) {
+      float* frow = outf + ((int64_t)kslice * M + row0 + trow) * ldo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float4 v;
+        v.x = acc[i][j][0];
+        v.y = acc[i][j][1];
+        v.z = acc[i][j][2];
+        v.w = acc[i][j][3];
+        *reinterpret_cast<float4*>(frow + tn * kW4N + 128 * wn + 16 * i + 4 * kq) = v;
+      }
+    } else if constexpr (EPI == kW4Swiglu) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float o[4];
@@ -962,14 +992,19 @@ void gemm_w4p_kernel(const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __
 // gemm_dense.hip launch_gemm_grouped.  K % 128 == 0.
 void launch_gemm_w4_grouped(const bf16_t* x, const bf16_t* w, bf16_t* out,
                             const int32_t* expert_offsets, int max_blocks, int n_out, int K,
-                            int E, int64_t w_rows, bool swiglu, hipStream_t s) {
+                            int E, int64_t w_rows, bool swiglu, hipStream_t s, float* outf,
+                            int slab_rows, int split_cus) {
   if (max_blocks <= 0) return;
   const int tiles_n = swiglu ? n_out / 128 : n_out / kW4N;
   const int chunks = (max_blocks + E) / 2 + 1;    // live 256-row tiles <= this
   const int grid = chunks * tiles_n;
   const int64_t estride = w_rows * K;
   constexpr int lds3 = 5 * kW4Img * 2;            // 160 KB
-  if (swiglu)
+  if (outf != nullptr && !swiglu)                 // outf: float [2][slab_rows][n_out]
+    gemm_w4_kernel<kW4Store, 0, true, true, 16, true, true, 2><<<2 * grid, 256, lds3, s>>>(
+        x, K, w, K, out, n_out, slab_rows, K, n_out, 0, tiles_n, 4, expert_offsets, E,
+        estride, outf, split_cus);
+  else if (swiglu)
     gemm_w4_kernel<kW4Swiglu, 0, true, true, 16, true, true><<<grid, 256, lds3, s>>>(
         x, K, w, K, out, n_out, max_blocks * 128, K, n_out, 0, tiles_n, 4, expert_offsets, E,
         estride);

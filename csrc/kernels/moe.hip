@@ -461,6 +461,45 @@ __global__ __launch_bounds__(256) void moe_combine_splitk_kernel(
   }
 }
 
+// Combine after the throughput-path w2 (gemm_w4.hip GROUPED KS = 2): the same split rule
+// on the same offsets tells which the GEMM wrote -- two fp32 K-slice slabs (yf, slab
+// stride in floats) or the bf16 rows y.
+__global__ __launch_bounds__(256) void moe_combine_w2_kernel(
+    const bf16_t* __restrict__ y, const float* __restrict__ yf, int64_t slab,
+    const int32_t* __restrict__ offs, int E, int tiles_n, int cus,
+    const int32_t* __restrict__ inv_pos, const float* __restrict__ wts, int T, int k, int d,
+    bf16_t* __restrict__ out, int64_t out_stride) {
+  const bool split = moe_w2_ksplit(moe_live_chunks(offs, E) * tiles_n, cus) == 2;
+  const int cpr = d >> 3;
+  const int64_t total = (int64_t)T * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / cpr;
+    const int c = (int)(i - t * cpr);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = wts[t * k + j];
+      if (wj == 0.f) continue;        // pair routed to another rank's expert (EP)
+      const int p = inv_pos[t * k + j];
+      if (split) {
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const float4* src = reinterpret_cast<const float4*>(yf + sl * slab + (int64_t)p * d) + 2 * c;
+          const float4 a = src[0], b = src[1];
+          acc[0] += wj * a.x; acc[1] += wj * a.y; acc[2] += wj * a.z; acc[3] += wj * a.w;
+          acc[4] += wj * b.x; acc[5] += wj * b.y; acc[6] += wj * b.z; acc[7] += wj * b.w;
+        }
+      } else {
+        float v[8];
+        unpack8(reinterpret_cast<const s16x8*>(y + (int64_t)p * d)[c], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += wj * v[q];
+      }
+    }
+    reinterpret_cast<s16x8*>(out + t * out_stride)[c] = pack8(acc);
+  }
+}
+
 static inline int moe_stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
@@ -894,6 +933,14 @@ void launch_moe_combine_splitk(const float* yf, int splits, int64_t slab, const 
   if (T == 0) return;
   moe_combine_splitk_kernel<<<moe_stream_grid((int64_t)T * (d >> 3)), 256, 0, s>>>(
       yf, splits, slab, inv_pos, w, T, k, d, out, out_stride);
+}
+
+void launch_moe_combine_w2(const bf16_t* y, const float* yf, int64_t slab, const int32_t* offs,
+                           int E, int tiles_n, int cus, const int32_t* inv_pos, const float* w,
+                           int T, int k, int d, bf16_t* out, int64_t out_stride, hipStream_t s) {
+  if (T == 0) return;
+  moe_combine_w2_kernel<<<moe_stream_grid((int64_t)T * (d >> 3)), 256, 0, s>>>(
+      y, yf, slab, offs, E, tiles_n, cus, inv_pos, w, T, k, d, out, out_stride);
 }
 
 void launch_moe_combine(const bf16_t* y, const int32_t* inv_pos, const float* w, int T, int k,

@@ -24,7 +24,10 @@ BLOCK_S = 16            # expert segment padding on the small-batch path
 SKINNY_MAX_TOKENS = 64  # T <= this: per-expert weight-streaming kernels
 # K slices of the latency-path w2 (gemm_skinny.hip moe_skinny_kernel SPLIT): 0/1 = off
 W2_SPLITS = int(os.environ.get("RFQ_MOE_W2_SPLITS", "2"))
-
+# Throughput-path grouped w2 split-K (gemm_w4.hip GROUPED KS = 2): "auto" lets the GEMM
+# and the combine decide on the device from the live tile count (common.h moe_w2_ksplit);
+# "0" never splits
+W2_KSPLIT = os.environ.get("RFQ_MOE_W2_KSPLIT", "auto")
 
 
 @dataclass
@@ -44,6 +47,7 @@ class MoEBuffers:
     act: torch.Tensor
     y: torch.Tensor
     yf: torch.Tensor | None = None     # [W2_SPLITS, rows, d] fp32 split-K w2 partials
+    yf2: torch.Tensor | None = None    # [2, cap, d] fp32 throughput-path split-K w2 partials
 
     @classmethod
     def allocate(cls, max_tokens: int, topk: int, E: int, d: int, F: int, device,
@@ -69,6 +73,8 @@ class MoEBuffers:
             yf=(torch.empty(W2_SPLITS, n + (E + 2) * BLOCK_S, d, dtype=torch.float32,
                             device=device)
                 if max_tokens <= SKINNY_MAX_TOKENS and W2_SPLITS > 1 else None),
+            yf2=(torch.empty(2, cap, d, dtype=torch.float32, device=device)
+                 if max_tokens > SKINNY_MAX_TOKENS and W2_KSPLIT != "0" else None),
         )
 
 
@@ -138,6 +144,12 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         # than one hipBLASLt GEMM per expert at every step size from 512 to 16K tokens,
         # so no step reads the offsets back to the host
         ops.moe_gemm_dense(xs, w13, act, bufs.expert_offsets, True)
+        if bufs.yf2 is not None and ops.MOE_W4 and w2_split_ok(w2):
+            # w2 + combine with the split-K decision taken on the device (the live tile
+            # count depends on the routing): fp32 K-slice slabs in yf2 or bf16 rows in y
+            ops.moe_w2_combine(act, w2, y, bufs.yf2, bufs.expert_offsets, bufs.inv_pos[:n], w,
+                               topk, out, _cus(x.device))
+            return out
         ops.moe_gemm_dense(act, w2, y, bufs.expert_offsets, False)
     elif ops.moe_gemm8_ok(w13, True) and ops.moe_gemm8_ok(w2, False):
         w2_tile = 256 if n >= 320 * w13.shape[0] else 128
@@ -149,6 +161,21 @@ def moe_mlp(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torc
         ops.moe_grouped_gemm(act, w2, y, eob, bufs.num_blocks)
     ops.moe_combine(y, bufs.inv_pos[:n], w, topk, out)
     return out
+
+
+def w2_split_ok(w2: torch.Tensor) -> bool:
+    """Shapes the split-K grouped w2 takes (w2 [E, d, F]: d % 256, F % 256, F >= 512)."""
+    d, F = w2.shape[1], w2.shape[2]
+    return d % 256 == 0 and F % 256 == 0 and F >= 512
+
+
+_CUS: dict = {}
+
+
+def _cus(device) -> int:
+    if device not in _CUS:
+        _CUS[device] = torch.cuda.get_device_properties(device).multi_processor_count
+    return _CUS[device]
 
 
 def _localize(ids: torch.Tensor, w: torch.Tensor, e0: int, e_local: int) -> None:

@@ -940,6 +940,14 @@ def moe_gemm_dense(x, w, out, expert_offsets, swiglu: bool = False, cfg: int | N
     _native.ops().moe_gemm_dense(x, w, out, expert_offsets, swiglu, cfg)
 
 
+def moe_w2_combine(x, w, y, yf, expert_offsets, inv_pos, weights, topk, out, cus: int):
+    """Throughput-path w2 + weighted top-k combine in two launches (gemm_w4.hip GROUPED
+    KS = 2 and moe.hip moe_combine_w2_kernel).  Both decide on the device from the expert
+    offsets whether the grouped GEMM cuts each tile's K range in two (fp32 partial slabs
+    in yf [2, >= rows, N]) or stores bf16 rows in y; cus <= 0 never splits."""
+    _native.ops().moe_w2_combine(x, w, y, yf, expert_offsets, inv_pos, weights, topk, out, cus)
+
+
 def moe_gemm_dense_ok(w, swiglu: bool) -> bool:
     N, K = w.shape[1], w.shape[2]
     return K % 64 == 0 and ((N // 2) % 128 == 0 if swiglu else N % 256 == 0)

@@ -947,6 +947,50 @@ def test_moe_gemm_dense(gpu, T, swiglu, cfg, d, F):
         assert bool((out[off[E]:].float() == 7.0).all())
 
 
+@pytest.mark.parametrize("T", [65, 300, 1000])
+@pytest.mark.parametrize("mode", ["never", "split", "full_rounds"])
+def test_moe_w2_combine_split_rule(gpu, T, mode):
+    """Throughput-path w2 + top-k combine (ops.moe_w2_combine): the grouped GEMM and the
+    combine take the split-K decision on the device from the expert offsets and the CU
+    count.  `cus` is chosen per case so each branch runs: 0 = never split; twice the live
+    tile count = the last round at most half full -> two fp32 K slices; exactly the tile
+    count = whole rounds -> one bf16 store.  Every branch must equal the fp32 oracle of
+    act . w2^T combined with the top-k weights (empty expert, odd block counts)."""
+    from replisense_rfq_amd.models.moe import BLOCK_M, MoEBuffers
+
+    E, k, d, F = 8, 2, 512, 1024
+    g = torch.Generator(device="cuda").manual_seed(T + 11)
+    w2 = ((torch.rand(E, d, F, device="cuda", generator=g) * 2 - 1) / math.sqrt(F)).to(BF)
+    bufs = MoEBuffers.allocate(T, k, E, d, F, "cuda")
+    logits = torch.randn(T, E, device="cuda", generator=g).to(BF)
+    logits[:, 5] = -30.0                                  # expert 5 gets no rows
+    n = T * k
+    cap = (n + E * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+    wts, ids = bufs.weights[:T], bufs.ids[:T]
+    ops.moe_topk(logits, k, True, wts, ids)
+    ops.moe_align(ids, E, BLOCK_M, bufs.sorted_ids[:cap], bufs.inv_pos[:n],
+                  bufs.expert_of_block[:cap // BLOCK_M], bufs.expert_offsets, bufs.num_blocks)
+    act = (torch.rand(cap, F, device="cuda", generator=g) * 2 - 1).to(BF)
+    off = bufs.expert_offsets.tolist()
+    tiles = sum(((off[e + 1] - off[e]) // BLOCK_M + 1) // 2 for e in range(E)) * (d // 256)
+    cus = {"never": 0, "split": 2 * tiles, "full_rounds": tiles}[mode]
+    y = torch.full((cap, d), 7.0, device="cuda", dtype=BF)
+    yf = torch.full((2, cap + 128, d), 7.0, device="cuda", dtype=torch.float32)
+    out = torch.empty(T, d, device="cuda", dtype=BF)
+    ops.moe_w2_combine(act, w2, y, yf, bufs.expert_offsets, bufs.inv_pos[:n], wts, k, out, cus)
+    yr = torch.zeros(cap, d, device="cuda")
+    for e in range(E):
+        a, b = off[e], off[e + 1]
+        if b > a:
+            yr[a:b] = act[a:b].float() @ w2[e].float().t()
+    pos = bufs.inv_pos[:n].long().view(T, k)
+    ref = (yr[pos] * wts.float().unsqueeze(-1)).sum(1)
+    _close(out, ref, atol=2e-2, rtol=2e-2, what=f"w2 combine {mode}")
+    wrote_slabs = bool((yf[:, :off[E]] != 7.0).any())
+    assert wrote_slabs == (mode == "split"), (mode, wrote_slabs)
+    assert bool((y[:off[E]] != 7.0).any()) == (mode != "split")
+
+
 ROWS_CFGS_PLAIN = (0 | 4, 0 | 8, 0 | 12, 1 | 4, 1 | 8, 2 | 0, 2 | 4, 3 | 0)   # (RW, CU) pairs
 
 

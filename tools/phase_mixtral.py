@@ -6,9 +6,10 @@ rocprofv3 step window.  Prints one JSON line.
 """
 import json
 import logging
+import os
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from replisense_rfq_amd.benchmarks.phases import model_phase  # noqa: E402
 
 if __name__ == "__main__":
