@@ -97,6 +97,7 @@ uint32_t* kernel_error_words(hipStream_t);
 int decode_persist_counter_words(int);
 int decode_persist_lds_bytes(int, int, int);
 int decode_persist_grid();
+int decode_engine_layout(int, int, int, int, int, int, int*, int*, int*, int*);
 void launch_decode_persist_op(const int64_t*, int, int, int, int, int, int, int, int, bf16_t*,
                               bf16_t*, int, bf16_t*, bf16_t*, const int32_t*, const float*,
                               const int32_t*, int, const int32_t*, int, const int32_t*,
@@ -789,6 +790,15 @@ std::vector<int64_t> decode_persist_info(int64_t M, int64_t d, int64_t Kx, int64
           (int64_t)rfq::decode_persist_grid()};
 }
 
+// Engine form's LDS bytes and ring slots for (M, d, Hq, Hkv, F) on this device: [bytes, slots]
+// (bytes 0: does not fit)
+std::vector<int64_t> decode_engine_info(int64_t M, int64_t d, int64_t Hq, int64_t Hkv, int64_t F) {
+  int r = 0, p, a, o;
+  const int b = rfq::decode_engine_layout((int)M, (int)d, (int)Hq, (int)Hkv, (int)F,
+                                          rfq::decode_persist_grid(), &r, &p, &a, &o);
+  return {(int64_t)b, (int64_t)r};
+}
+
 void decode_persist(const Tensor& residual, const Tensor& layers, const Tensor& qbuf,
                     const Tensor& attn, const Tensor& act, const Tensor& positions,
                     const Tensor& cos_sin, const Tensor& slots, const Tensor& block_tables,
@@ -834,6 +844,15 @@ void decode_persist(const Tensor& residual, const Tensor& layers, const Tensor& 
   TORCH_CHECK(counters.numel() >= rfq::decode_persist_counter_words((int)nst),
               "decode_persist: counter buffer too small");
   const int64_t Kx = std::max<int64_t>(Hq * 128, F);
+  if (flags & 16) {
+    // engine form: M <= 2, a row spans at most 3 ring slots, >= 5 slots fit next to the rows
+    int r, p, a, o;
+    TORCH_CHECK(M <= 2, "decode_persist engine: M <= 2 tokens");
+    TORCH_CHECK(std::max<int64_t>(d, Kx) / 512 <= 33, "decode_persist engine: K / 512 <= 33");
+    TORCH_CHECK(rfq::decode_engine_layout((int)M, (int)d, (int)Hq, (int)Hkv, (int)F,
+                                          rfq::decode_persist_grid(), &r, &p, &a, &o) > 0,
+                "decode_persist engine: the rows leave fewer than 5 ring slots in LDS");
+  }
   TORCH_CHECK(rfq::decode_persist_lds_bytes((int)M, (int)d, (int)Kx) <= 160 * 1024,
               "decode_persist: the step's rows do not fit in LDS (M * (d + max(Hq*128, F)))");
   rfq::launch_decode_persist_op(
@@ -1138,6 +1157,7 @@ TORCH_LIBRARY(rfq_amd, m) {
   m.def("car_data_offset() -> int", &car_data_offset);
   m.def("kernel_errors() -> int[]", &kernel_errors);
   m.def("decode_persist_info(int M, int d, int Kx, int nst) -> int[]", &decode_persist_info);
+  m.def("decode_engine_info(int M, int d, int Hq, int Hkv, int F) -> int[]", &decode_engine_info);
   m.def("decode_persist(Tensor(a!) residual, Tensor layers, Tensor(b!) qbuf, Tensor(c!) attn, "
         "Tensor(d!) act, Tensor positions, Tensor cos_sin, Tensor slots, Tensor block_tables, "
         "Tensor q_start, Tensor q_len, Tensor kv_len, Tensor work_seq, Tensor work_ct, "

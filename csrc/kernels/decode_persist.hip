@@ -115,7 +115,10 @@ struct DpArgs {
   float eps;
   int flags;                     // A/B and timing bits: 1 wave 0 prefetches too, 2 no
                                  // cross-seam prefetch, 4 attention units skipped (timing),
-                                 // 8 rotated chunk start per wave
+                                 // 8 rotated chunk start per wave, 16 the engine form;
+                                 // engine timing bits (WRONG results): 32 slots released
+                                 // unread, 64 no weight stream
+  int eg_ring, eg_parts, eg_area, eg_ring_off;   // engine form: ring slots, LDS offsets
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dp_rsrc(const void* p, int bytes) {
@@ -830,6 +833,551 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_persist_kernel(DpArgs a)
   }
 }
 
+// ================================================================== engine form
+// flags bit 4 (RFQ_PERSIST=engine), M <= 2.  The same chain and seams, with the weight
+// stream moved off the computing waves (MI355X_MICROARCH.md 'engine-vs-launches',
+// 'ldsdma-fill', 'prefetch-credit'): per CU wave 0 is a LOADER that only issues LDS-DMA
+// (buffer_load ... lds, nt) of the CU's weight pieces into a ring of 16 KB slots, and
+// waves 1-3 are CONSUMERS that take the slots round-robin, run the attention units and
+// the stage epilogues.  The loader never waits on a seam: it walks the launch's weight
+// sequence (every layer's qkv, o, gate|up, down rows of this CU, in stage order) and
+// stalls only on a full ring, so during every seam and during the attention the ring
+// fills with the next stage's weights (o's whole 33.5 MB at 8B fits the chip's rings).
+//
+// Stream of a stage: the CU's units U = cu + i * CUs (qkv: a rotate-half row pair, gate|up:
+// gate row U and up row F + U, o / down: row U), each row as K / 512 pieces of 1 KB
+// (64 lanes x 16 B, a piece never straddles rows since K % 512 == 0); slot j holds pieces
+// 16 j .. 16 j + 15 of the CU's stage stream.  Hand-offs inside the CU are LDS words:
+// FULL[slot] = sequence number (loader, after the counted vmcnt that lands it; at most
+// kEgDepth slots in flight), DONE[slot] = sequence number (consumer, once the slot is in
+// its registers).  A consumer reduces each row segment of a slot (DPP wave sum) into
+// parts[row][segment] (deterministic: no float atomics); the consumer that takes the
+// stage's last slot (an LDS count) sums the segments in order, runs the epilogue (RoPE +
+// q / KV stores, SwiGLU, residual add) for all of the CU's units and arrives at the seam.
+// Seams: consumer 1 polls the global shards (the GEMV form's protocol) and releases the
+// others through an LDS word; the loader is not part of any barrier.
+constexpr int kEgFlag = 16;
+constexpr int kEgCons = 3;                // consumer waves (1..3); wave 0 loads
+constexpr int kEgSlot = 16384;            // ring slot: 16 pieces of 1 KB
+constexpr int kEgDepth = 4;               // slots in flight per loader
+constexpr int kEgSegs = 3;                // ring slots one row can span (K <= 16.5 K)
+constexpr int kEgCtlBytes = 256;
+enum { kEgFull = 0, kEgDone = 8, kEgRel = 16, kEgAb = 17, kEgCons_ = 18, kEgStg = 19,
+       kEgAtt = 20, kEgExit = 21 };
+
+typedef __attribute__((address_space(3))) char eg_lds_c;
+typedef volatile __attribute__((address_space(3))) int eg_ctl_t;   // LDS control words
+typedef const __attribute__((address_space(3))) u32x4 eg_lds_v4;
+
+struct EgStage {
+  const bf16_t* W;
+  int K, ppr, rpu, n_cu, P, S, bytes, Kin;
+};
+
+__device__ __forceinline__ EgStage eg_stage(const DpArgs& a, const DpLayer& L, int st, int cu,
+                                            int nwg) {
+  EgStage s;
+  const int nq = (a.Hq + 2 * a.Hkv) * 128;
+  int nunits;
+  switch (st) {
+    case kDpQkv: s.W = L.wqkv; s.K = a.d; nunits = nq / 2; s.rpu = 2; s.bytes = nq * a.d * 2; break;
+    case kDpO: s.W = L.wo; s.K = a.Hq * kD; nunits = a.d; s.rpu = 1; s.bytes = a.d * s.K * 2; break;
+    case kDpGu: s.W = L.wgu; s.K = a.d; nunits = a.F; s.rpu = 2; s.bytes = 2 * a.F * a.d * 2; break;
+    default: s.W = L.wd; s.K = a.F; nunits = a.d; s.rpu = 1; s.bytes = a.d * a.F * 2; break;
+  }
+  s.Kin = s.K;
+  s.n_cu = cu < nunits ? (nunits - cu + nwg - 1) / nwg : 0;
+  s.ppr = s.K >> 9;
+  s.P = s.n_cu * s.rpu * s.ppr;
+  s.S = (s.P + 15) >> 4;
+  return s;
+}
+
+// weight row of the CU's unit U, row r of the unit
+__device__ __forceinline__ int eg_row(const DpArgs& a, int st, int U, int r) {
+  if (st == kDpQkv) return (U >> 6) * 128 + (U & 63) + r * 64;
+  if (st == kDpGu) return U + r * a.F;
+  return U;
+}
+
+__device__ __forceinline__ eg_ctl_t* eg_ctl(char* smem) {
+  return (eg_ctl_t*)(smem + kDpCsBytes);
+}
+__device__ __forceinline__ int eg_lds_add(eg_ctl_t* ctl, int i) {
+  return __atomic_fetch_add((__attribute__((address_space(3))) int*)(ctl + i), 1,
+                            __ATOMIC_RELAXED);
+}
+
+// bounded LDS spin: true once `ok()` holds, false on the abort word or after 1 s (which
+// raises the abort word and counts kErrPersist).  A tight LDS poll: the clock (an SMEM
+// round trip) and the abort word are read every 256 polls only -- a sleep or a clock read
+// per poll made every ring hand-off cost ~0.3 µs.
+template <typename F>
+__device__ __forceinline__ bool eg_spin(const DpArgs& a, eg_ctl_t* ctl, F ok) {
+  if (ok()) return true;
+  uint64_t t0 = 0;
+  for (int it = 1;; ++it) {
+    if (ok()) return true;
+    if ((it & 255) == 0) {
+      if (ctl[kEgAb]) return false;
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      if (t0 == 0) {
+        t0 = t;
+      } else if (t - t0 > kSpinTicks) {
+        report_error(a.err, kErrPersist);
+        ctl[kEgAb] = 1;
+        return false;
+      }
+    }
+  }
+}
+
+// flags bit 8 (diagnostic): CU 0 writes s_memrealtime stamps (100 MHz) into part_ml viewed
+// as uint64 [512]: 0-3 wave start, 4-7 wave end, 8-10 consumer after staging, 12-14 after
+// rs, 16 epilogue start, 17 epilogue end, 64 + n loader slot n issued (n < 64), 128 + n
+// loader slot n published, 192 + n consumer saw slot n full (n < 64)
+__device__ __forceinline__ void eg_stamp(const DpArgs& a, int i, int lane) {
+  if ((a.flags & 256) && blockIdx.x == 0 && lane == 0 && i < 512)
+    reinterpret_cast<uint64_t*>(a.part_ml)[i] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---- loaders (waves 0 .. NL-1): loader li issues the slots n with n % NL == li and
+// publishes them; every loader walks the whole piece sequence to keep its cursor
+template <int NL>
+__device__ void eg_loader(const DpArgs& a, char* smem, int li, int lane) {
+  eg_ctl_t* ctl = eg_ctl(smem);
+  eg_lds_c* const ring = (eg_lds_c*)(smem + a.eg_ring_off);
+  const int R = a.eg_ring, cu = blockIdx.x, nwg = gridDim.x;
+  int n = 0, idx = 0;                   // global slot sequence, n % R
+  int pub = li, last = li - NL;         // next own slot to publish, last own slot issued
+  auto publish_upto = [&](int upto) {
+    for (; pub <= upto; pub += NL) {
+      ctl[kEgFull + pub % R] = pub;
+      if (pub < 64) eg_stamp(a, 128 + pub, lane);
+    }
+  };
+  for (int l = a.l0; l < a.l1; ++l) {
+    const DpLayer L = a.layers[l];
+    for (int st = 0; st < kDpStages; ++st) {
+      if (!((a.stages >> st) & 1) || st == kDpAttn) continue;
+      const EgStage s = eg_stage(a, L, st, cu, nwg);
+      const __amdgpu_buffer_rsrc_t wr = dp_rsrc(dp_uni(s.W), s.bytes);
+      const int nrows = s.n_cu * s.rpu, rsb = s.K * 2;
+      int ri = 0, kp = 0;               // piece cursor: row ordinal, piece in row
+      int rowoff = nrows > 0 ? eg_row(a, st, cu, 0) * rsb : 0;
+      for (int j = 0; j < s.S; ++j) {
+        const bool own = NL == 1 || (n % NL) == li;
+        if (own && n >= R && ctl[kEgDone + idx] < n - R) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          publish_upto(last);           // consumers may be waiting on landed slots
+          const int need = n - R, ix = idx;
+          if (!eg_spin(a, ctl, [&]() { return ctl[kEgDone + ix] >= need; })) return;
+        }
+        eg_lds_c* const dst = ring + idx * kEgSlot;
+        const bool load = own && !(a.flags & 64);   // 64: timing, no weight stream
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+          if (load) {
+            // pieces past the stage's stream re-read the weight's first KB (never consumed)
+            const int off = ri < nrows ? __builtin_amdgcn_readfirstlane(rowoff + kp * 1024) : 0;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(dst + p * 1024), 16,
+                                                     lane * 16, off, 0, kNt);
+          }
+          if (ri < nrows && ++kp == s.ppr) {
+            kp = 0;
+            if (++ri < nrows)
+              rowoff = (s.rpu == 2 ? eg_row(a, st, cu + (ri >> 1) * nwg, ri & 1)
+                                   : eg_row(a, st, cu + ri * nwg, 0)) * rsb;
+          }
+        }
+        if (own) {
+          if (n < 64) eg_stamp(a, 64 + n, lane);
+          last = n;
+          if (last - pub >= (kEgDepth - 1) * NL) {
+            // all but this loader's youngest kEgDepth - 1 slots (16 loads each) have landed
+            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            publish_upto(last - (kEgDepth - 1) * NL);
+          }
+        }
+        ++n;
+        if (++idx == R) idx = 0;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  publish_upto(last);
+}
+
+// ---- consumers (waves 1..3): seam wait.  Consumer 0 polls the global shards (bounded, as
+// dp_wait) and releases the others through ctl[kEgRel]; returns the abort state.
+__device__ bool eg_wait(const DpArgs& a, int k, int l, int st, eg_ctl_t* ctl,
+                        uint32_t* abort_w, int c, int lane) {
+  if (c == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t nwg = gridDim.x;
+    for (;;) {
+      uint32_t v = 0;
+      if (lane < kDpShards)
+        v = __hip_atomic_load(dp_cnt(a.cnt, k, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (lane == kDpShards)
+        v = __hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t ab = __shfl(v, kDpShards, 64);
+      uint32_t tot = lane < kDpShards ? v : 0u;
+#pragma unroll
+      for (int o2 = 1; o2 < kDpShards; o2 <<= 1) tot += __shfl_xor(tot, o2, 64);
+      tot = __shfl(tot, 0, 64);
+      if (ab != 0 || ctl[kEgAb]) {
+        if (lane == 0) ctl[kEgAb] = 1;
+        break;
+      }
+      if (tot >= nwg) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+        if (lane == 0) {
+          report_error(a.err, kErrPersist);
+          uint32_t zero = 0;
+          if (a.err != nullptr)
+            __hip_atomic_compare_exchange_strong(a.err + kErrPersistInfo, &zero,
+                                                 (uint32_t)((l << 8) | st) + 1u, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ctl[kEgAb] = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) ctl[kEgRel] = k + 1;
+    return ctl[kEgAb] != 0;
+  }
+  eg_spin(a, ctl, [&]() { return ctl[kEgRel] >= k + 1; });
+  return ctl[kEgAb] != 0;
+}
+
+// the arriving wave's stores are drained (vmcnt(0)) before its add: Guideline 16
+__device__ __forceinline__ void eg_arrive_global(const DpArgs& a, int k, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    __hip_atomic_fetch_add(dp_cnt(a.cnt, k, blockIdx.x & (kDpShards - 1)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the stage's input rows (and the residual the o / down epilogue adds to) into LDS by the
+// three consumers (every load of a thread in flight before its LDS stores), then an LDS
+// count over the consumers (monotonic: stage ordinal sn)
+template <int MM, int NC>
+__device__ void eg_stage_inputs(const DpArgs& a, int st, bf16_t* res_l, bf16_t* x_l, int c,
+                                int lane, eg_ctl_t* ctl, int sn) {
+  const bf16_t* src1 = st == kDpO ? a.attn : st == kDpDown ? a.act : nullptr;
+  const int n1 = st == kDpO ? a.Hq * kD : a.F;
+  const int per0 = a.d >> 3, tot0 = MM * per0;
+  const int per1 = n1 >> 3, total = tot0 + (src1 != nullptr ? MM * per1 : 0);
+  const __amdgpu_buffer_rsrc_t r0 = dp_rsrc(a.residual, a.M * a.d * 2);
+  const __amdgpu_buffer_rsrc_t r1 = dp_rsrc(src1 != nullptr ? src1 : a.residual,
+                                            src1 != nullptr ? a.M * n1 * 2 : 0);
+  constexpr int U = 8, NT = NC * 64;
+  for (int base = c * 64 + lane; base < total; base += U * NT) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * NT;
+      v[u] = (u32x4){0u, 0u, 0u, 0u};
+      if (i < tot0) {
+        const int m = i / per0, cc = i - m * per0;
+        if (m < a.M) v[u] = dp_ld16(r0, (m * a.d + cc * 8) * 2);
+      } else if (i < total) {
+        const int jj = i - tot0, m = jj / per1, cc = jj - m * per1;
+        if (m < a.M) v[u] = dp_ld16(r1, (m * n1 + cc * 8) * 2);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * NT;
+      if (i < tot0) {
+        const int m = i / per0, cc = i - m * per0;
+        *reinterpret_cast<u32x4*>(res_l + m * a.d + cc * 8) = v[u];
+      } else if (i < total) {
+        const int jj = i - tot0, m = jj / per1, cc = jj - m * per1;
+        *reinterpret_cast<u32x4*>(x_l + m * n1 + cc * 8) = v[u];
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) eg_lds_add(ctl, kEgStg);
+  eg_spin(a, ctl, [&]() { return ctl[kEgStg] >= NC * (sn + 1); });
+}
+
+// epilogue of the CU's units of a GEMV stage (one consumer wave; lanes over (unit, token))
+template <int MM>
+__device__ void eg_epilogue(const DpArgs& a, const DpLayer& L, int st, const EgStage& s,
+                            const float* parts_l, const bf16_t* res_l, const float* cs_l,
+                            const float (&rs)[MM], int lane) {
+  const int cu = blockIdx.x, nwg = gridDim.x;
+  for (int t = lane; t < s.n_cu * MM; t += 64) {
+    const int i = t / MM, m = t - i * MM;
+    if (m >= a.M) continue;
+    float v[2] = {0.f, 0.f};
+    for (int r = 0; r < s.rpu; ++r) {
+      const int ri = i * s.rpu + r;
+      const int f = (ri * s.ppr) >> 4, e = (ri * s.ppr + s.ppr - 1) >> 4;
+      float sum = 0.f;
+      for (int sg = 0; sg <= e - f; ++sg) sum += parts_l[(ri * kEgSegs + sg) * MM + m];
+      v[r] = sum;
+    }
+    float rsm = 1.f;
+#pragma unroll
+    for (int q = 0; q < MM; ++q)
+      if (q == m) rsm = rs[q];
+    const int U = cu + i * nwg;
+    if (st == kDpO || st == kDpDown) {
+      // residual <- bf16(bf16(x . w) + residual)  (gemv_rows.hip kRwResAdd)
+      const float old = bf2f(res_l[m * a.d + U]);
+      const bf16_t nv = f2bf(bf2f(f2bf(v[0])) + old);
+      __builtin_amdgcn_raw_buffer_store_b16(nv, dp_rsrc(a.residual, a.M * a.d * 2),
+                                            (m * a.d + U) * 2, 0, kSc1);
+    } else if (st == kDpGu) {
+      const float gf = bf2f(f2bf(v[0] * rsm));
+      const float sg = gf / (1.f + __expf(-gf));
+      const bf16_t o = f2bf(bf2f(f2bf(sg)) * bf2f(f2bf(v[1] * rsm)));
+      __builtin_amdgcn_raw_buffer_store_b16(o, dp_rsrc(a.act, a.M * a.F * 2), (m * a.F + U) * 2, 0,
+                                            kSc1);
+    } else {
+      const float va = v[0] * rsm, vb = v[1] * rsm;
+      const int h = U >> 6, dd = U & 63;
+      float o1 = va, o2 = vb;
+      if (h < a.Hq + a.Hkv) {
+        const float cc = cs_l[m * 128 + dd], ss = cs_l[m * 128 + 64 + dd];
+        o1 = va * cc - vb * ss;
+        o2 = vb * cc + va * ss;
+      }
+      if (h < a.Hq) {
+        const __amdgpu_buffer_rsrc_t qr = dp_rsrc(a.qbuf, a.M * a.ldq * 2);
+        const int off = (m * a.ldq + h * 128 + dd) * 2;
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(o1), qr, off, 0, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(o2), qr, off + 128, 0, kSc1);
+      } else {
+        const int slot = a.slots[m];
+        if (slot >= 0) {
+          const bool is_k = h < a.Hq + a.Hkv;
+          const int kvh = is_k ? h - a.Hq : h - a.Hq - a.Hkv;
+          // per-lane global sc1 stores (see dp_epilogue: no per-lane buffer descriptor)
+          bf16_t* dst = (is_k ? L.kc : L.vc) +
+                        (((int64_t)(slot / a.BS) * a.Hkv + kvh) * a.BS + slot % a.BS) * 128;
+          __hip_atomic_store(dst + dd, f2bf(o1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dst + 64 + dd, f2bf(o2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+}
+
+// one slot: 16 pieces, partial dot products per row segment into parts_l
+template <int MM>
+__device__ __forceinline__ void eg_consume_slot(const eg_lds_c* sl, const EgStage& s, int j,
+                                                const bf16_t* x_in, float* parts_l,
+                                                eg_ctl_t* ctl, int idx, int seq, int lane) {
+  u32x4 w[16];
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+    w[p] = *(eg_lds_v4*)(sl + p * 1024 + lane * 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) ctl[kEgDone + idx] = seq;       // the slot's bytes are in registers
+  const int q0 = j * 16;
+  int row = q0 / s.ppr, kp = q0 - row * s.ppr;
+  int seg = j - ((row * s.ppr) >> 4);
+  float acc[MM];
+#pragma unroll
+  for (int m = 0; m < MM; ++m) acc[m] = 0.f;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    if (q0 + p < s.P) {                          // wave-uniform
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        const u32x4 x = *reinterpret_cast<const u32x4*>(x_in + m * s.Kin + kp * 512 + lane * 8);
+        acc[m] = dot8(w[p], x, acc[m]);
+      }
+      const bool row_end = kp == s.ppr - 1;
+      if (row_end || p == 15 || q0 + p + 1 == s.P) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+          const float t = wave_sum_dpp(acc[m]);
+          if (lane == 0) parts_l[(row * kEgSegs + seg) * MM + m] = t;
+          acc[m] = 0.f;
+        }
+      }
+      if (row_end) {
+        kp = 0;
+        ++row;
+        seg = j - ((row * s.ppr) >> 4);
+      } else {
+        ++kp;
+      }
+    }
+  }
+}
+
+template <int MM, int NL>
+__global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) {
+  constexpr int NC = kDpWaves - NL;       // consumer waves
+  extern __shared__ __attribute__((aligned(1024))) char eg_smem[];
+  float* cs_l = reinterpret_cast<float*>(eg_smem);
+  eg_ctl_t* ctl = eg_ctl(eg_smem);
+  float* parts_l = reinterpret_cast<float*>(eg_smem + a.eg_parts);
+  bf16_t* res_l = reinterpret_cast<bf16_t*>(eg_smem + a.eg_area);
+  bf16_t* x_l = res_l + MM * a.d;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = gridDim.x, cu = blockIdx.x;
+
+  for (int i = tid; i < MM * 128; i += kDpThreads) {
+    const int m = i >> 7;
+    cs_l[i] = m < a.M ? a.cos_sin[(int64_t)a.positions[m] * 128 + (i & 127)] : 0.f;
+  }
+  for (int i = tid; i < kEgCtlBytes / 4; i += kDpThreads) ctl[i] = i < 16 ? -1 : 0;
+  int nper = 0;
+  for (int st = 0; st < kDpStages; ++st) nper += (a.stages >> st) & 1;
+  const int nst = (a.l1 - a.l0) * nper;
+  uint32_t* abort_w = a.cnt + (nst > 1 ? nst - 1 : 0) * kDpShards * kDpShardWords;
+  uint32_t* exit_w = abort_w + kDpShardWords;
+  __syncthreads();
+
+  if (wave < NL) {
+    eg_stamp(a, wave, lane);
+    eg_loader<NL>(a, eg_smem, wave, lane);
+    eg_stamp(a, 4 + wave, lane);
+  } else {
+    const int c = wave - NL;
+    eg_stamp(a, wave, lane);
+    const int gw = c * nwg + cu, nwt = NC * nwg;
+    const eg_lds_c* const ring = (const eg_lds_c*)(eg_smem + a.eg_ring_off);
+    const int R = a.eg_ring;
+    bool aborted = false;
+    int n = 0, cbase = 0, sn = 0, an = 0, k = 0;
+    for (int l = a.l0; l < a.l1 && !aborted; ++l) {
+      const DpLayer L = a.layers[l];
+      for (int st = 0; st < kDpStages && !aborted; ++st) {
+        if (!((a.stages >> st) & 1)) continue;
+        if (k > 0) aborted = eg_wait(a, k - 1, l, st, ctl, abort_w, c, lane);
+        if (aborted) break;
+        if (st == kDpAttn) {
+          if (!(a.flags & 4)) {
+            const int nu = a.W * a.Hkv * a.splits;
+            bf16_t* v_lds = res_l + c * (kDpVTile / 2);
+            for (int u = gw; u < nu; u += nwt) {
+              const int split = u % a.splits, rest = u / a.splits;
+              dp_attn_unit(a, L, rest / a.Hkv, rest % a.Hkv, split, v_lds, lane);
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          int prev = 0;
+          if (lane == 0) prev = eg_lds_add(ctl, kEgAtt);
+          prev = __shfl(prev, 0, 64);
+          if (prev == NC * an + NC - 1 && k + 1 < nst) eg_arrive_global(a, k, lane);
+          ++an;
+        } else {
+          const EgStage s = eg_stage(a, L, st, cu, nwg);
+          eg_stage_inputs<MM, NC>(a, st, res_l, x_l, c, lane, ctl, sn);
+          if (sn == 0) eg_stamp(a, 8 + c, lane);
+          const bool normx = st == kDpQkv || st == kDpGu;
+          const bf16_t* x_in = normx ? res_l : x_l;
+          float rs[MM];
+#pragma unroll
+          for (int m = 0; m < MM; ++m) rs[m] = 1.f;
+          if (normx) {
+            float ssq[MM];
+#pragma unroll
+            for (int m = 0; m < MM; ++m) ssq[m] = 0.f;
+            for (int ch = 0; ch < (a.d >> 9); ++ch)
+#pragma unroll
+              for (int m = 0; m < MM; ++m) {
+                const u32x4 x = *reinterpret_cast<const u32x4*>(res_l + m * a.d + ch * 512 + lane * 8);
+                ssq[m] = dot8(x, x, ssq[m]);
+              }
+#pragma unroll
+            for (int m = 0; m < MM; ++m) rs[m] = rsqrtf(wave_sum_dpp(ssq[m]) / (float)a.d + a.eps);
+          }
+          if (sn == 0) eg_stamp(a, 12 + c, lane);
+          int idx = (n + c) % R;
+          for (int j = c; j < s.S; j += NC, idx = idx + NC >= R ? idx + NC - R : idx + NC) {
+            const int seq = n + j;
+            if (!eg_spin(a, ctl, [&]() { return ctl[kEgFull + idx] >= seq; })) {
+              aborted = true;
+              break;
+            }
+            if (seq < 64) eg_stamp(a, 192 + seq, lane);
+            if (a.flags & 32) {         // timing: slots released unread (WRONG results)
+              if (lane == 0) ctl[kEgDone + idx] = seq;
+            } else {
+              eg_consume_slot<MM>(ring + idx * kEgSlot, s, j, x_in, parts_l, ctl, idx, seq, lane);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            int prev = 0;
+            if (lane == 0) prev = eg_lds_add(ctl, kEgCons_);
+            prev = __shfl(prev, 0, 64);
+            if (prev == cbase + s.S - 1) {            // the stage's last slot: epilogue
+              if (sn == 0) eg_stamp(a, 16, lane);
+              eg_epilogue<MM>(a, L, st, s, parts_l, res_l, cs_l, rs, lane);
+              if (sn == 0) eg_stamp(a, 17, lane);
+              if (k + 1 < nst) eg_arrive_global(a, k, lane);
+            }
+          }
+          if (s.S == 0 && c == 0 && k + 1 < nst) eg_arrive_global(a, k, lane);
+          n += s.S;
+          cbase += s.S;
+          ++sn;
+        }
+        ++k;
+      }
+    }
+    if (aborted && lane == 0) ctl[kEgAb] = 1;
+    eg_stamp(a, 4 + wave, lane);
+  }
+
+  // ---- exit (as decode_persist_kernel)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev =
+        __hip_atomic_fetch_add(exit_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl[kEgExit] = prev == (unsigned)nwg - 1;
+  }
+  __syncthreads();
+  if (ctl[kEgExit]) {
+    const int nseam = nst > 1 ? nst - 1 : 0;
+    for (int i = tid; i < nseam * kDpShards; i += kDpThreads)
+      __hip_atomic_store(a.cnt + i * kDpShardWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(abort_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exit_w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// engine LDS layout for (M, d, Hq, Hkv, F) on `grid` CUs: cs | ctl | parts | area | ring;
+// returns the total bytes (0 when fewer than 5 ring slots fit in 160 KB)
+int decode_engine_layout(int M, int d, int Hq, int Hkv, int F, int grid, int* ring, int* parts,
+                         int* area, int* ring_off) {
+  const int mm = M <= 1 ? 1 : 2;
+  const int nq = (Hq + 2 * Hkv) * 128, qd = Hq * kD;
+  auto cdiv = [](int x, int y) { return (x + y - 1) / y; };
+  int rows = cdiv(nq / 2, grid) * 2;
+  rows = rows > cdiv(d, grid) ? rows : cdiv(d, grid);
+  rows = rows > cdiv(F, grid) * 2 ? rows : cdiv(F, grid) * 2;
+  const int kx = qd > F ? qd : F;
+  int ar = mm * (d + kx) * 2;
+  if (ar < kEgCons * kDpVTile) ar = kEgCons * kDpVTile;
+  const int p0 = kDpCsBytes + kEgCtlBytes;
+  const int a0 = (p0 + rows * kEgSegs * mm * 4 + 15) & ~15;
+  const int r0 = (a0 + ar + 1023) & ~1023;
+  int R = (160 * 1024 - r0) / kEgSlot;
+  if (R > 8) R = 8;
+  if (R < 5) return 0;
+  *ring = R;
+  *parts = p0;
+  *area = a0;
+  *ring_off = r0;
+  return r0 + R * kEgSlot;
+}
+
 // counter words a launch of `nst` stages needs: (nst - 1) seams x 8 shards x 32 words,
 // then the abort and exit words (32 words apart)
 int decode_persist_counter_words(int nst) {
@@ -859,6 +1407,23 @@ void launch_decode_persist(const DpArgs& a, hipStream_t s) {
   const int grid = decode_persist_grid();
   DpArgs b = a;
   b.err = kernel_error_words(s);
+  if (a.flags & kEgFlag) {
+    // shapes (M <= 2, K / 512 <= 33, the layout fits) are checked by the binding
+    const int bytes = decode_engine_layout(a.M, a.d, a.Hq, a.Hkv, a.F, grid, &b.eg_ring,
+                                           &b.eg_parts, &b.eg_area, &b.eg_ring_off);
+    // flags bit 7: two loader waves (two consumers)
+    if (a.flags & 128) {
+      if (a.M <= 1)
+        decode_engine_kernel<1, 2><<<grid, kDpThreads, bytes, s>>>(b);
+      else
+        decode_engine_kernel<2, 2><<<grid, kDpThreads, bytes, s>>>(b);
+    } else if (a.M <= 1) {
+      decode_engine_kernel<1, 1><<<grid, kDpThreads, bytes, s>>>(b);
+    } else {
+      decode_engine_kernel<2, 1><<<grid, kDpThreads, bytes, s>>>(b);
+    }
+    return;
+  }
   if (a.M <= 1)
     decode_persist_kernel<1><<<grid, kDpThreads, lds, s>>>(b);
   else if (a.M <= 2)

@@ -124,7 +124,7 @@ class DecoderLM:
         self.norms_folded = False       # fold_norms: attn / mlp RMSNorm weights in qkv / gate|up
         self.single_pass = (SINGLE_PASS_DECODE in ("1", "on", "true")
                             or (SINGLE_PASS_DECODE == "auto" and self.hq // self.hkv <= 4))
-        self.persist = PERSIST if PERSIST in ("0", "1", "all", "ao") else "0"
+        self.persist = PERSIST if PERSIST in ("0", "1", "all", "ao", "engine") else "0"
         self._persist_tab = None        # int64 [L, 8] device table of layer pointers
         self._persist_key = None
         self._persist_tk = None         # split-merge tickets of the persistent attention
@@ -187,6 +187,10 @@ class DecoderLM:
         d, qd, F = self.cfg.hidden, self.hq * self.cfg.head_dim, self.ffn_local
         if d % 512 or qd % 512 or F % 512:
             return False
+        if self.persist == "engine":
+            # loader / consumer form: M <= 2, a row within 3 ring slots, >= 5 slots in LDS
+            return (T <= 2 and max(d, qd, F) // 512 <= 33
+                    and ops.decode_engine_info(T, d, self.hq, self.hkv, F)[0] > 0)
         mm = 1 if T <= 1 else 2 if T <= 2 else 4
         return 2112 + mm * (d + max(qd, F)) * 2 <= 160 * 1024
 
@@ -212,7 +216,8 @@ class DecoderLM:
 
     def _forward_persist(self, m: ForwardMeta) -> torch.Tensor:
         """Small decode step on the persistent kernel (csrc/kernels/decode_persist.hip):
-        "all" runs every layer in one launch, "ao" keeps qkv / MLP on the row-streaming
+        "all" runs every layer in one launch, "engine" the same on the loader / consumer
+        form (LDS-DMA weight ring, M <= 2), "ao" keeps qkv / MLP on the row-streaming
         launches and fuses attention + o per layer.  Same numerics as _forward_fold except
         the attention's split boundaries (one wave per (kv head, split), in-kernel merge)."""
         cfg, w = self.cfg, self.w
@@ -244,9 +249,10 @@ class DecoderLM:
                 ops.rows_residual_add(a, lw["down"], residual)
         else:
             qbuf = torch.empty((T, qd), dtype=self.dtype, device=self.device)
+            flags = PERSIST_FLAGS | (ops.PERSIST_ENGINE if self.persist == "engine" else 0)
             ops.decode_persist(residual, tab, qbuf, attn, act, *meta, 0, L, ops.PERSIST_STAGES,
                                self.hq, self.hkv, F, self.kv_k.shape[3], S, self.scale, eps,
-                               PERSIST_FLAGS)
+                               flags)
         x = ops.rms_norm(residual, w["final_norm"], eps)
         xs = x if m.logits_idx is None else x.index_select(0, m.logits_idx)
         return ops.linear(xs, w["lm_head"])

@@ -26,6 +26,7 @@ __all__ = [
     "ROWS_BIT", "ROWS_MAX_M", "ROWS_CFGS", "ROWS_CFGS_PAIRED", "rows_ok",
     "set_rows_best", "rows_rope_normx", "rows_swiglu_normx", "rows_residual_add", "fold_ok",
     "kernel_errors", "decode_persist", "decode_persist_info", "PERSIST_STAGES",
+    "PERSIST_ENGINE", "decode_engine_info",
 ]
 
 # Tokens per step up to which projections use the skinny weight-streaming GEMM
@@ -50,6 +51,12 @@ def kernel_errors() -> list[int]:
 # Persistent decode layers (csrc/kernels/decode_persist.hip): stage bits
 PERSIST_QKV, PERSIST_ATTN, PERSIST_O, PERSIST_GU, PERSIST_DOWN = 1, 2, 4, 8, 16
 PERSIST_STAGES = 31
+PERSIST_ENGINE = 16      # flags bit: the loader / consumer (LDS-DMA ring) form, M <= 2
+
+
+def decode_engine_info(M: int, d: int, Hq: int, Hkv: int, F: int) -> tuple[int, int]:
+    """(LDS bytes, ring slots) of the engine form on this device; bytes 0 = does not fit."""
+    return tuple(_native.ops().decode_engine_info(M, d, Hq, Hkv, F))
 
 
 def decode_persist_info(M: int, d: int, Kx: int, nst: int) -> tuple[int, int, int]:

@@ -34,3 +34,15 @@ def test_fold_allowed_for_emulated_tp_only():
     assert emu.fold_norms()                              # persistent emulation: folded
     real = DecoderLM(cfg, "cpu", tp=TPContext(rank=0, world=2), seed=1)
     assert not real.tp.emulated and not real.fold_norms()
+
+
+def test_engine_mode_gate_cpu(monkeypatch):
+    """RFQ_PERSIST=engine is a known mode (the loader / consumer form) and, like the other
+    persistent modes, never runs on CPU tensors."""
+    import replisense_rfq_amd.models.llama as llama
+
+    monkeypatch.setattr(llama, "PERSIST", "engine")
+    m = llama.DecoderLM(get_config("tiny-llama"), "cpu", seed=1)
+    assert m.persist == "engine"
+    m.fold_norms()
+    assert not m._persist_step(_decode_meta(1), 1)

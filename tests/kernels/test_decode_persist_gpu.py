@@ -137,3 +137,53 @@ def test_persist_graph_replay(gpu):
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     assert ops.kernel_errors()[1] == 0
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_engine_matches_multi_launch(gpu, shape):
+    """The loader / consumer form (RFQ_PERSIST=engine: LDS-DMA weight ring, M <= 2) against
+    the multi-launch path.  Its row sums are reduced per ring-slot segment, so the appended
+    K / V and the logits are compared with a relative tolerance, not bit for bit; a
+    repeated launch must still be bit-identical (no float atomics)."""
+    ops.reset_plans()
+    cfg = SHAPES[shape]
+    errs0 = ops.kernel_errors()
+    for batch in (True, False):
+        for T in (1, 2):
+            nblocks = T * ((CTX + T + 31) // 32) + 1
+            a, b = _models(cfg, gpu, nblocks, "engine")
+            for splits in (1, 4, 16):
+                m = _meta(cfg, a.hq, a.hkv, T, batch, splits, gpu)
+                assert b._persist_step(m, T), (shape, T)
+                la = a.forward(m)
+                lb = b.forward(m)
+                torch.cuda.synchronize()
+                assert _rel(b.kv_k, a.kv_k) < 1e-2 and _rel(b.kv_v, a.kv_v) < 1e-2, \
+                    (shape, batch, T, splits)
+                assert _rel(lb, la) < 1e-2, (shape, batch, T, splits, _rel(lb, la))
+                lb2 = b.forward(m)
+                torch.cuda.synchronize()
+                assert torch.equal(lb, lb2), (shape, batch, T, splits)
+    assert ops.kernel_errors()[:2] == errs0[:2]
+
+
+def test_engine_graph_replay(gpu):
+    """A captured engine-form step replays with the same result many times over."""
+    ops.reset_plans()
+    cfg = SHAPES["8b"]
+    a, b = _models(cfg, gpu, 8, "engine")
+    m = _meta(cfg, a.hq, a.hkv, 1, True, 16, gpu)
+    ref = b.forward(m).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        b.forward(m)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = b.forward(m)
+    for _ in range(20):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert ops.kernel_errors()[1] == 0

@@ -1,0 +1,14 @@
+#!/bin/bash
+# engine form timing pieces (8B, ctx 1024): gate|up alone (1 and 32 layers) and the whole
+# layer, one or two loader waves, consumers' compute or the loader's stream switched off
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-.}
+mkdir -p gpurun_out
+O=gpurun_out/eng_parts2.jsonl
+: > $O
+for f in 16 112 144; do
+  timeout -k 10 120 python -u tools/bench_persist.py --shape 8b --ctx 1024 --layers 1 --modes raw:8 --flags $f --iters 200 >> $O 2>&1 || { tail -20 $O; exit 1; }
+  timeout -k 10 120 python -u tools/bench_persist.py --shape 8b --ctx 1024 --modes raw:8,raw:31 --flags $f --iters 20 >> $O 2>&1 || { tail -20 $O; exit 1; }
+done
+timeout -k 10 120 python -u tools/bench_persist.py --shape 8b --ctx 1024 --modes 0,engine --iters 20 >> $O 2>&1 || { tail -20 $O; exit 1; }
+grep '^{' $O
