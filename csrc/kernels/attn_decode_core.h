@@ -338,7 +338,7 @@ __device__ __forceinline__ void attn_decode_body(
   gu32* tk = (gu32*)(tickets + (int64_t)w * Hkv + kvh);
   unsigned prev = 0;
   if (lane == 0) prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
+  prev = __builtin_amdgcn_readfirstlane(prev);   // uniform: the merge branch stays scalar
   if (prev != (unsigned)num_splits - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
   if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

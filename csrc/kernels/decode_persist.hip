@@ -577,7 +577,7 @@ __device__ __forceinline__ void dp_attn_unit(const DpArgs& a, const DpLayer& L, 
   gu32* tk = (gu32*)(a.tickets + (int64_t)w * Hkv + kvh);
   unsigned prev = 0;
   if (lane == 0) prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
+  prev = __builtin_amdgcn_readfirstlane(prev);   // uniform: the merge branch is scalar
   if (prev != (unsigned)S - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // every handed-off load is sc1
   if (lane == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -685,11 +685,11 @@ __device__ __forceinline__ bool dp_wait(const DpArgs& a, int k, int l, int st, i
         v = __hip_atomic_load(dp_cnt(a.cnt, k, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == kDpShards)
         v = __hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t ab = __shfl(v, kDpShards, 64);
+      const uint32_t ab = __builtin_amdgcn_readfirstlane(__shfl(v, kDpShards, 64));
       uint32_t tot = lane < kDpShards ? v : 0u;
 #pragma unroll
       for (int o2 = 1; o2 < kDpShards; o2 <<= 1) tot += __shfl_xor(tot, o2, 64);
-      tot = __shfl(tot, 0, 64);
+      tot = __builtin_amdgcn_readfirstlane(tot);
       if (ab != 0) {
         if (lane == 0) ctl[0] = 1;
         break;
@@ -712,7 +712,7 @@ __device__ __forceinline__ bool dp_wait(const DpArgs& a, int k, int l, int st, i
     }
   }
   __syncthreads();
-  return ctl[0] != 0;
+  return __builtin_amdgcn_readfirstlane(ctl[0]) != 0;
 }
 
 template <int MM, int EPI>
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_persist_kernel(DpArgs a)
     ctl[1] = prev == (unsigned)nwg - 1;
   }
   __syncthreads();
-  if (ctl[1]) {
+  if (__builtin_amdgcn_readfirstlane(ctl[1])) {
     const int nseam = nst > 1 ? nst - 1 : 0;
     for (int i = tid; i < nseam * kDpShards; i += kDpThreads)
       __hip_atomic_store(a.cnt + i * kDpShardWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -871,7 +871,7 @@ typedef const __attribute__((address_space(3))) u32x4 eg_lds_v4;
 
 struct EgStage {
   const bf16_t* W;
-  int K, ppr, rpu, n_cu, P, S, bytes, Kin;
+  int K, ppr, rpu, n_cu, u0, P, S, bytes, Kin;
 };
 
 __device__ __forceinline__ EgStage eg_stage(const DpArgs& a, const DpLayer& L, int st, int cu,
@@ -886,7 +886,12 @@ __device__ __forceinline__ EgStage eg_stage(const DpArgs& a, const DpLayer& L, i
     default: s.W = L.wd; s.K = a.F; nunits = a.d; s.rpu = 1; s.bytes = a.d * a.F * 2; break;
   }
   s.Kin = s.K;
-  s.n_cu = cu < nunits ? (nunits - cu + nwg - 1) / nwg : 0;
+  // a contiguous block of units per CU (units u0 .. u0 + n_cu - 1): the CU's rows share
+  // pages, where a unit stride of CUs put every row of a CU 2 MB from the last (one TLB
+  // walk per row; the stream measured ~18 GB/s per CU)
+  const int base = nunits / nwg, rem = nunits - base * nwg;
+  s.n_cu = base + (cu < rem ? 1 : 0);
+  s.u0 = cu * base + (cu < rem ? cu : rem);
   s.ppr = s.K >> 9;
   s.P = s.n_cu * s.rpu * s.ppr;
   s.S = (s.P + 15) >> 4;
@@ -903,6 +908,13 @@ __device__ __forceinline__ int eg_row(const DpArgs& a, int st, int U, int r) {
 __device__ __forceinline__ eg_ctl_t* eg_ctl(char* smem) {
   return (eg_ctl_t*)(smem + kDpCsBytes);
 }
+// a control word read as a wave-uniform value: without the readfirstlane the compiler
+// treats every branch on an LDS-loaded word as divergent, and everything after it (loop
+// cursors, slot indices, the LDS-DMA destination in M0) moves to VGPRs with exec-masked
+// control flow -- the loader then took ~1 µs per slot with no loads at all
+__device__ __forceinline__ int eg_ld(eg_ctl_t* ctl, int i) {
+  return __builtin_amdgcn_readfirstlane(ctl[i]);
+}
 __device__ __forceinline__ int eg_lds_add(eg_ctl_t* ctl, int i) {
   return __atomic_fetch_add((__attribute__((address_space(3))) int*)(ctl + i), 1,
                             __ATOMIC_RELAXED);
@@ -918,8 +930,9 @@ __device__ __forceinline__ bool eg_spin(const DpArgs& a, eg_ctl_t* ctl, F ok) {
   uint64_t t0 = 0;
   for (int it = 1;; ++it) {
     if (ok()) return true;
+    if (a.flags & 512) __builtin_amdgcn_s_sleep(1);   // A/B: sleeping pollers
     if ((it & 255) == 0) {
-      if (ctl[kEgAb]) return false;
+      if (eg_ld(ctl, kEgAb)) return false;
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       if (t0 == 0) {
         t0 = t;
@@ -934,11 +947,18 @@ __device__ __forceinline__ bool eg_spin(const DpArgs& a, eg_ctl_t* ctl, F ok) {
 
 // flags bit 8 (diagnostic): CU 0 writes s_memrealtime stamps (100 MHz) into part_ml viewed
 // as uint64 [512]: 0-3 wave start, 4-7 wave end, 8-10 consumer after staging, 12-14 after
-// rs, 16 epilogue start, 17 epilogue end, 64 + n loader slot n issued (n < 64), 128 + n
-// loader slot n published, 192 + n consumer saw slot n full (n < 64)
+// rs, 16 epilogue start, 17 epilogue end, 64 + n loader starts issuing slot n (n < 64),
+// 256 + n its 16 loads issued, 128 + n slot n published, 192 + n consumer saw it full
 __device__ __forceinline__ void eg_stamp(const DpArgs& a, int i, int lane) {
   if ((a.flags & 256) && blockIdx.x == 0 && lane == 0 && i < 512)
     reinterpret_cast<uint64_t*>(a.part_ml)[i] = __builtin_amdgcn_s_memrealtime();
+}
+// the shader clock counter next to the real-time one (clock = d memtime / d realtime)
+__device__ __forceinline__ void eg_stamp_clk(const DpArgs& a, int i, int lane) {
+  if ((a.flags & 256) && blockIdx.x == 0 && lane == 0) {
+    reinterpret_cast<uint64_t*>(a.part_ml)[i] = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<uint64_t*>(a.part_ml)[i + 1] = __builtin_amdgcn_s_memtime();
+  }
 }
 
 // ---- loaders (waves 0 .. NL-1): loader li issues the slots n with n % NL == li and
@@ -948,12 +968,15 @@ __device__ void eg_loader(const DpArgs& a, char* smem, int li, int lane) {
   eg_ctl_t* ctl = eg_ctl(smem);
   eg_lds_c* const ring = (eg_lds_c*)(smem + a.eg_ring_off);
   const int R = a.eg_ring, cu = blockIdx.x, nwg = gridDim.x;
+  const int vl = lane * 16;
   int n = 0, idx = 0;                   // global slot sequence, n % R
-  int pub = li, last = li - NL;         // next own slot to publish, last own slot issued
+  int pub = li, pidx = li, last = li - NL;   // next own slot to publish (and % R), last issued
   auto publish_upto = [&](int upto) {
     for (; pub <= upto; pub += NL) {
-      ctl[kEgFull + pub % R] = pub;
+      ctl[kEgFull + pidx] = pub;
       if (pub < 64) eg_stamp(a, 128 + pub, lane);
+      pidx += NL;
+      if (pidx >= R) pidx -= R;
     }
   };
   for (int l = a.l0; l < a.l1; ++l) {
@@ -963,35 +986,56 @@ __device__ void eg_loader(const DpArgs& a, char* smem, int li, int lane) {
       const EgStage s = eg_stage(a, L, st, cu, nwg);
       const __amdgpu_buffer_rsrc_t wr = dp_rsrc(dp_uni(s.W), s.bytes);
       const int nrows = s.n_cu * s.rpu, rsb = s.K * 2;
-      int ri = 0, kp = 0;               // piece cursor: row ordinal, piece in row
-      int rowoff = nrows > 0 ? eg_row(a, st, cu, 0) * rsb : 0;
+      // piece cursor: byte offset of the next piece and pieces left in its row; past the
+      // stage's rows the offset is 0 (the weight's first KB, loaded and never consumed)
+      int ri = 0;
+      int so = nrows > 0 ? eg_row(a, st, s.u0, 0) * rsb : 0;
+      int left = nrows > 0 ? s.ppr : 1 << 30;
+      auto next_row = [&]() {
+        ++ri;
+        if (ri < nrows) {
+          so = (s.rpu == 2 ? eg_row(a, st, s.u0 + (ri >> 1), ri & 1)
+                           : eg_row(a, st, s.u0 + ri, 0)) * rsb;
+          left = s.ppr;
+        } else {
+          so = 0;
+          left = 1 << 30;
+        }
+      };
       for (int j = 0; j < s.S; ++j) {
         const bool own = NL == 1 || (n % NL) == li;
-        if (own && n >= R && ctl[kEgDone + idx] < n - R) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          publish_upto(last);           // consumers may be waiting on landed slots
-          const int need = n - R, ix = idx;
-          if (!eg_spin(a, ctl, [&]() { return ctl[kEgDone + ix] >= need; })) return;
-        }
-        eg_lds_c* const dst = ring + idx * kEgSlot;
-        const bool load = own && !(a.flags & 64);   // 64: timing, no weight stream
-#pragma unroll
-        for (int p = 0; p < 16; ++p) {
-          if (load) {
-            // pieces past the stage's stream re-read the weight's first KB (never consumed)
-            const int off = ri < nrows ? __builtin_amdgcn_readfirstlane(rowoff + kp * 1024) : 0;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(dst + p * 1024), 16,
-                                                     lane * 16, off, 0, kNt);
+        if (own && !(a.flags & 64)) {   // 64: timing, no weight stream
+          if (n >= R && eg_ld(ctl, kEgDone + idx) < n - R) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            publish_upto(last);         // consumers may be waiting on landed slots
+            const int need = n - R, ix = idx;
+            if (!eg_spin(a, ctl, [&]() { return eg_ld(ctl, kEgDone + ix) >= need; })) return;
           }
-          if (ri < nrows && ++kp == s.ppr) {
-            kp = 0;
-            if (++ri < nrows)
-              rowoff = (s.rpu == 2 ? eg_row(a, st, cu + (ri >> 1) * nwg, ri & 1)
-                                   : eg_row(a, st, cu + ri * nwg, 0)) * rsb;
+          eg_lds_c* const dst = ring + idx * kEgSlot;
+          if (n < 64) eg_stamp(a, 64 + n, lane);
+#pragma unroll
+          for (int p = 0; p < 16; ++p) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void_t*)(dst + p * 1024), 16, vl,
+                                                     so, 0, kNt);
+            so += 1024;
+            if (--left == 0) next_row();
+          }
+          if (n < 64) eg_stamp(a, 256 + n, lane);
+        } else {
+          if (own && n >= R && eg_ld(ctl, kEgDone + idx) < n - R) {
+            publish_upto(last);
+            const int need = n - R, ix = idx;
+            if (!eg_spin(a, ctl, [&]() { return eg_ld(ctl, kEgDone + ix) >= need; })) return;
+          }
+          for (int adv = 16; adv > 0;) {     // another loader's slot: move the cursor only
+            const int t = adv < left ? adv : left;
+            so += t * 1024;
+            left -= t;
+            adv -= t;
+            if (left == 0) next_row();
           }
         }
         if (own) {
-          if (n < 64) eg_stamp(a, 64 + n, lane);
           last = n;
           if (last - pub >= (kEgDepth - 1) * NL) {
             // all but this loader's youngest kEgDepth - 1 slots (16 loads each) have landed
@@ -1021,12 +1065,12 @@ __device__ bool eg_wait(const DpArgs& a, int k, int l, int st, eg_ctl_t* ctl,
         v = __hip_atomic_load(dp_cnt(a.cnt, k, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else if (lane == kDpShards)
         v = __hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t ab = __shfl(v, kDpShards, 64);
+      const uint32_t ab = __builtin_amdgcn_readfirstlane(__shfl(v, kDpShards, 64));
       uint32_t tot = lane < kDpShards ? v : 0u;
 #pragma unroll
       for (int o2 = 1; o2 < kDpShards; o2 <<= 1) tot += __shfl_xor(tot, o2, 64);
-      tot = __shfl(tot, 0, 64);
-      if (ab != 0 || ctl[kEgAb]) {
+      tot = __builtin_amdgcn_readfirstlane(tot);
+      if (ab != 0 || eg_ld(ctl, kEgAb)) {
         if (lane == 0) ctl[kEgAb] = 1;
         break;
       }
@@ -1047,10 +1091,10 @@ __device__ bool eg_wait(const DpArgs& a, int k, int l, int st, eg_ctl_t* ctl,
       __builtin_amdgcn_s_sleep(1);
     }
     if (lane == 0) ctl[kEgRel] = k + 1;
-    return ctl[kEgAb] != 0;
+    return eg_ld(ctl, kEgAb) != 0;
   }
-  eg_spin(a, ctl, [&]() { return ctl[kEgRel] >= k + 1; });
-  return ctl[kEgAb] != 0;
+  eg_spin(a, ctl, [&]() { return eg_ld(ctl, kEgRel) >= k + 1; });
+  return eg_ld(ctl, kEgAb) != 0;
 }
 
 // the arriving wave's stores are drained (vmcnt(0)) before its add: Guideline 16
@@ -1103,7 +1147,7 @@ __device__ void eg_stage_inputs(const DpArgs& a, int st, bf16_t* res_l, bf16_t* 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (lane == 0) eg_lds_add(ctl, kEgStg);
-  eg_spin(a, ctl, [&]() { return ctl[kEgStg] >= NC * (sn + 1); });
+  eg_spin(a, ctl, [&]() { return eg_ld(ctl, kEgStg) >= NC * (sn + 1); });
 }
 
 // epilogue of the CU's units of a GEMV stage (one consumer wave; lanes over (unit, token))
@@ -1127,7 +1171,7 @@ __device__ void eg_epilogue(const DpArgs& a, const DpLayer& L, int st, const EgS
 #pragma unroll
     for (int q = 0; q < MM; ++q)
       if (q == m) rsm = rs[q];
-    const int U = cu + i * nwg;
+    const int U = s.u0 + i;
     if (st == kDpO || st == kDpDown) {
       // residual <- bf16(bf16(x . w) + residual)  (gemv_rows.hip kRwResAdd)
       const float old = bf2f(res_l[m * a.d + U]);
@@ -1242,7 +1286,9 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) 
 
   if (wave < NL) {
     eg_stamp(a, wave, lane);
+    if (wave == 0) eg_stamp_clk(a, 24, lane);
     eg_loader<NL>(a, eg_smem, wave, lane);
+    if (wave == 0) eg_stamp_clk(a, 26, lane);
     eg_stamp(a, 4 + wave, lane);
   } else {
     const int c = wave - NL;
@@ -1270,7 +1316,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) 
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           int prev = 0;
           if (lane == 0) prev = eg_lds_add(ctl, kEgAtt);
-          prev = __shfl(prev, 0, 64);
+          prev = __builtin_amdgcn_readfirstlane(prev);
           if (prev == NC * an + NC - 1 && k + 1 < nst) eg_arrive_global(a, k, lane);
           ++an;
         } else {
@@ -1299,7 +1345,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) 
           int idx = (n + c) % R;
           for (int j = c; j < s.S; j += NC, idx = idx + NC >= R ? idx + NC - R : idx + NC) {
             const int seq = n + j;
-            if (!eg_spin(a, ctl, [&]() { return ctl[kEgFull + idx] >= seq; })) {
+            if (!eg_spin(a, ctl, [&]() { return eg_ld(ctl, kEgFull + idx) >= seq; })) {
               aborted = true;
               break;
             }
@@ -1312,7 +1358,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) 
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             int prev = 0;
             if (lane == 0) prev = eg_lds_add(ctl, kEgCons_);
-            prev = __shfl(prev, 0, 64);
+            prev = __builtin_amdgcn_readfirstlane(prev);
             if (prev == cbase + s.S - 1) {            // the stage's last slot: epilogue
               if (sn == 0) eg_stamp(a, 16, lane);
               eg_epilogue<MM>(a, L, st, s, parts_l, res_l, cs_l, rs, lane);
@@ -1341,7 +1387,7 @@ __global__ __launch_bounds__(kDpThreads, 1) void decode_engine_kernel(DpArgs a) 
     ctl[kEgExit] = prev == (unsigned)nwg - 1;
   }
   __syncthreads();
-  if (ctl[kEgExit]) {
+  if (eg_ld(ctl, kEgExit)) {
     const int nseam = nst > 1 ? nst - 1 : 0;
     for (int i = tid; i < nseam * kDpShards; i += kDpThreads)
       __hip_atomic_store(a.cnt + i * kDpShardWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -105,7 +105,7 @@ def _default_plan(M: int, N: int, K: int) -> int:
 
 
 def linear_plan(M: int, N: int, K: int) -> int:
-    if M > SKINNY_MAX_M or K % 128 or N % 16:
+    if M < 1 or M > SKINNY_MAX_M or K % 128 or N % 16:
         return -1
     if _TUNED_MS:
         for m in _TUNED_MS:
@@ -618,6 +618,9 @@ def linear(x, w, out=None, plan: int | None = None):
     M-split plan measured that to be faster."""
     M, K = x.shape
     N = w.shape[0]
+    if M == 0:
+        # a chunked-prefill step whose chunk ends no prompt selects no logits rows
+        return out if out is not None else torch.empty((0, N), dtype=x.dtype, device=x.device)
     if _gpu(x) and tiled_only(w):
         return _gemv_tiled(x, w, out, plan)
     if _gpu(x) and x.stride(1) == 1 and x.stride(0) % 8 == 0:

@@ -1118,3 +1118,21 @@ def test_gemv_rows_folded_norm(gpu, M, cfg):
     torch.ops.rfq_amd.gemv_rows(a, wo, r2, ((cfg & 15) | 1) | 32)
     y = (a.float() @ wo.float().t()).to(BF)
     _close(r2, (y.float() + res.float()).to(BF), 2e-2, 1e-2, f"residual add M={M}")
+
+
+def test_linear_zero_rows_with_rows_plan(gpu):
+    """A chunked-prefill step whose chunk ends no prompt selects zero logits rows: the LM
+    head's linear must return an empty result even when the start-up plan put the M = 1
+    bucket on the row-streaming GEMV (which takes 1 <= M <= 4 only) -- the 70B phase's
+    multi-page PDF set failed there before."""
+    ops.reset_plans()
+    N, K = 1024, 512
+    w = (torch.randn(N, K, device="cuda") / 16).to(BF)
+    ops.set_linear_plan({(1, N, K): ops.ROWS_BIT | 9}, [1])
+    try:
+        x = torch.empty(0, K, device="cuda", dtype=BF)
+        assert ops.linear(x, w).shape == (0, N)
+        x1 = torch.randn(1, K, device="cuda").to(BF)
+        _close(ops.linear(x1, w), x1.float() @ w.float().t(), atol=2e-2, rtol=2e-2, what="M=1 rows")
+    finally:
+        ops.reset_plans()

@@ -41,7 +41,7 @@ def main():
     tab, tk, cnt = model._persist_state()
     S = 16
     po = torch.empty(T * model.hq * S * 128, device=dev)
-    pm = torch.zeros(1024, device=dev)
+    pm = torch.zeros(2048, device=dev)
 
     def run():
         ops.decode_persist(res, tab, qbuf, attn, act, m.positions, model.cos_sin, m.slot_mapping,
@@ -62,8 +62,10 @@ def main():
            "wave_start": [us(st[i]) for i in range(4)], "wave_end": [us(st[4 + i]) for i in range(4)],
            "after_staging": [us(st[8 + i]) for i in range(3)], "after_rs": [us(st[12 + i]) for i in range(3)],
            "epilogue": [us(st[16]), us(st[17])],
-           "issued": [us(st[64 + n]) for n in range(64)], "published": [us(st[128 + n]) for n in range(64)],
-           "consumed": [us(st[192 + n]) for n in range(64)], "kernel_errors": ops.kernel_errors()}
+           "issue_start": [us(st[64 + n]) for n in range(64)],
+           "issued": [us(st[256 + n]) for n in range(64)], "published": [us(st[128 + n]) for n in range(64)],
+           "consumed": [us(st[192 + n]) for n in range(64)], "clock_mhz": round((st[27] - st[25]) / max(1, st[26] - st[24]) * 100.0, 1),
+           "kernel_errors": ops.kernel_errors()}
     print(json.dumps(out), flush=True)
 
 
