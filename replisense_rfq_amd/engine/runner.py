@@ -23,6 +23,7 @@ A step's rows are laid out in two sections:
 """
 from __future__ import annotations
 
+import os
 import time
 import numpy as np
 import torch
@@ -40,6 +41,7 @@ SAMPLE_SPLITS = 8
 EXT_MAX = 32                 # extends up to this many tokens use the decode kernel
 TOKEN_MULTS = (1, 2, 3, 4, 6, 8)
 MAX_GRAPH_TOKENS = 4096
+_STEP_LOG = os.environ.get("RFQ_STEP_LOG", "")
 
 
 def _seed64(req_seed: int, pos: int) -> int:
@@ -261,6 +263,13 @@ class ModelRunner:
     def _run(self, header: np.ndarray, payload: np.ndarray) -> np.ndarray:
         t0 = time.perf_counter()
         key = (int(header[H_GNB]), int(header[H_GTB]))
+        if _STEP_LOG:
+            # debugging aid (RFQ_STEP_LOG=path): each step's shape, flushed before launch
+            with open(_STEP_LOG, "a") as f:
+                f.write(" ".join(f"{k}={int(header[i])}" for k, i in (
+                    ("T", H_T), ("TA", H_TA), ("NA", H_NA), ("NB", H_NB), ("S", H_S),
+                    ("maxb", H_MAXB), ("gnb", H_GNB), ("gtb", H_GTB), ("splits", H_SPLITS)))
+                        + "\n")
         if key[0]:
             g, gbuf, out = self.graphs[key]
             self._upload(payload, gbuf)
