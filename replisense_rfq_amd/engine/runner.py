@@ -287,6 +287,12 @@ class ModelRunner:
             except Exception as e:  # noqa: BLE001 - re-raised once the step has drained
                 hook_err = e
         t2 = time.perf_counter()
+        if out.is_cuda and out.numel() == 0:
+            # a step with no logits rows (a prefill chunk that ends no prompt): copying an
+            # empty tensor does not wait for the stream, and the next step is packed into
+            # the same pinned staging buffer this step's payload is still being uploaded
+            # from -- wait for the step, as the token readback does for every other step
+            torch.cuda.current_stream(self.device).synchronize()
         toks = out.cpu().numpy() if out.is_cuda else out.numpy()
         self.stats["launch_s"] += t1 - t0
         self.stats["overlap_s"] += t2 - t1

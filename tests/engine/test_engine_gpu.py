@@ -241,3 +241,40 @@ def test_mixed_tiled_plan_forward_matches_cpu_oracle(gpu, monkeypatch):
         lc = m_cpu.forward(_meta(T, "cpu", nb)).float()
         rel = (lg - lc).norm() / lc.norm()
         assert rel < 0.05, (T, rel)
+
+
+def test_chunked_prefill_steps_without_logits(gpu, monkeypatch):
+    """Long prompts split into prefill chunks whose steps select no logits rows (the
+    70B phase's multi-page PDF set, 1,024-token chunks): the LM head gets zero rows and
+    the runner must still wait for such a step before the next one is packed into the same
+    pinned staging buffer (an empty readback does not synchronise; without the wait the
+    previous step's upload could read the next payload).  Every step is checked to have
+    finished before the next upload, and the documents must decode to valid JSON twice
+    over with identical tokens."""
+    from replisense_rfq_amd.engine import runner as runner_mod
+
+    waits = []
+    orig = runner_mod.ModelRunner._run
+
+    def _run(self, header, payload):
+        out = orig(self, header, payload)
+        waits.append(torch.cuda.current_stream().query())   # the step has drained
+        return out
+
+    monkeypatch.setattr(runner_mod.ModelRunner, "_run", _run)
+    texts = []
+    for _ in range(2):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=4, max_kv_blocks=2048,
+                                     max_batched_tokens=96, graph_buckets=(1, 2, 4),
+                                     decode_hints=True))
+        tok = eng.tokenizer
+        prompts = [tok.chat_ids(build_messages(synth.make_long_rfq(i).text)) for i in range(2)]
+        assert all(len(p) > 3 * 96 for p in prompts)
+        seqs = eng.generate(prompts)
+        for s in seqs:
+            assert s.finish_reason == "stop"
+            RFQResponse(**json.loads(eng.decode_text(s)))
+        texts.append([eng.decode_text(s) for s in seqs])
+        del eng
+    assert texts[0] == texts[1]
+    assert waits and all(waits)

@@ -20,7 +20,11 @@ def main():
     cfg = EngineConfig.from_env(model="llama3-70b", seed=0, max_num_seqs=8, graph_buckets=(1,),
                                 max_batched_tokens=1024, gemm_split=False)
     eng = LLMEngine(cfg)
-    print("engine up", flush=True)
+    from replisense_rfq_amd import ops
+    plans = {name: {str(k): v for k, v in getattr(ops, name).items()}
+             for name in ("_LINEAR_PLAN", "_SILU_PLAN", "_NORM_PLAN", "_ROPE_PLAN", "_SWI_PLAN")
+             if isinstance(getattr(ops, name, None), dict)}
+    print("engine up; small-M plans", json.dumps(plans), "tuned", ops._TUNED_MS, flush=True)
     try:
         if nref:
             lat, _, _ = latency_reference(eng, nref)
