@@ -289,9 +289,9 @@ class DecoderLM:
         ``auto`` (RFQ_TILED_WEIGHTS, default) copies projections, smallest first, while
         the copies stay within 25 % of the device's memory (and 40 % of what is free;
         ranks sharing one GPU in a rehearsal set RFQ_TILED_WEIGHTS=0) and tiles the rest
-        in place: 8B and the 70B TP=8 shard copy all four, 70B at TP=1 copies qkv, o and
-        down and keeps only the tiled gate|up (whose 224-tile grid suits the dense GEMM
-        at prefill sizes).  ``copy`` / ``inplace`` force one mode for all.  Dense models
+        in place -- unless the norms are folded (the row-streaming decode path needs the
+        row-major weight; then the rest stays row-major): 8B and the 70B TP=8 shard copy
+        all four, 70B at TP=1 copies o and qkv and keeps gate|up and down row-major.  ``copy`` / ``inplace`` force one mode for all.  Dense models
         only.  The start-up plan (ops.autotune) times the tiled cfgs.  Returns the bytes
         of the extra copies."""
         mode = (mode or os.environ.get("RFQ_TILED_WEIGHTS", "auto")).lower()
@@ -312,6 +312,12 @@ class DecoderLM:
             for k in sorted(names, key=lambda n: size[n]):
                 if used + size[k] <= budget:
                     plan[k], used = "copy", used + size[k]
+                elif self.norms_folded:
+                    # the folded-norm decode path streams row-major weights (gemv_rows);
+                    # a tiled-only projection would send every small step to the split-K
+                    # GEMVs instead: 70B TP=1 single stream 44.4 vs 42.5 sampled steps/s
+                    # with gate|up row-major (profiles/r6/llama70b_tp1_tiling_ab.txt)
+                    plan[k] = "off"
                 else:
                     plan[k] = "inplace" if inplace_ok(k) else "off"
         elif mode == "inplace":
