@@ -41,8 +41,8 @@ import sys
 import threading
 import time
 
-from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, latency_reference,
-                                                  loaded_latency,
+from replisense_rfq_amd.benchmarks.stream import (DocStream, latency, latency_pdf_set,
+                                                  latency_reference, loaded_latency,
                                                   single_stream as _single_stream, token_shape,
                                                   validate)
 
@@ -287,6 +287,11 @@ def tp_latency_phase(model: str, args, wctx, rank: int, on_timeout) -> dict | No
                             / ss["sampled_steps_per_s_p50"], 4)
                     res["per_row"] = [{"row": a, "sampled": b, "tokens": c, "prompt": d,
                                        "s": round(t, 3)} for (a, b, c, d), t in zip(rows, lat)]
+                    if args.pdf_set and time.perf_counter() - t0 < args.tp_latency_budget - 90:
+                        # BASELINE config 4's prefill-heavy documents on the real TP group
+                        # (the one-GPU 70B phase runs the same fixed set at TP = 1)
+                        res["pdf_set"] = latency_pdf_set(
+                            eng, args.pdf_set, deadline=time.perf_counter() + 60.0)
                     if args.tp_docs > 0:
                         stream = DocStream(eng, 0, args.seed + 1, args.tp_in_flight)
                         warm = max(1, args.tp_in_flight // 2)

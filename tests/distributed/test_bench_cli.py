@@ -66,9 +66,12 @@ def test_bench_tp_latency_phase_gloo():
     the result rides in the same JSON line, the timed fields are untouched."""
     out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
                 "--model", "tiny-llama", "--tp-latency-model", "tiny-llama-tp",
-                "--tp-latency-runs", "2", "--tp-docs", "4", "--tp-in-flight", "2"] + SMALL)
+                "--tp-latency-runs", "2", "--tp-docs", "4", "--tp-in-flight", "2",
+                "--pdf-set", "1"] + SMALL)
     assert out["config"]["parallelism"] == "dp2"
     tpl = out["tp_latency"]
+    # BASELINE config 4's prefill-heavy documents on the TP group too
+    assert tpl["pdf_set"]["docs"] == 1 and tpl["pdf_set"]["valid"] == 1.0, tpl.get("pdf_set")
     assert tpl["status"] == "ok", tpl
     assert tpl["model"] == "tiny-llama-tp" and tpl["parallelism"] == "tp2"
     assert tpl["runs"] == 2 and tpl["p50_parse_text_latency_s"] > 0

@@ -182,7 +182,8 @@ def main():
     if os.environ.get("LAT_SP"):
         # one wave per split: the reduce launch vs the in-kernel merge by the last split wave
         # (tickets; whole-wave merge, every split's loads in flight at once)
-        for Hq, Hkv, L in ((8, 1, 80), (32, 8, 32)):
+        shapes = ((8, 1, 80), (32, 8, 32), (64, 8, 80))   # 70B TP=8 rank, 8B, 70B TP=1
+        for Hq, Hkv, L in shapes:
             for C in (512, 1024, 2048):
                 row = {"Hq": Hq, "Hkv": Hkv, "ctx": C}
                 for sp in (8, 16):
