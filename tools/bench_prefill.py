@@ -16,20 +16,22 @@ from replisense_rfq_amd.ops import _native  # noqa: E402
 _native.require()
 
 
-def run(B, S, Hq, Hkv, iters=10):
+def run(B, S, Hq, Hkv, iters=10, P=0):
+    """P > 0: the first P keys of each sequence are a cached prefix (q_len = S - P)."""
     qblk = int(os.environ.get("QBLK", 0)) or ops.prefill_qblk(Hq, Hkv)
     dev = torch.device("cuda")
     pages = (S + 31) // 32
     k = torch.randn(B * pages + 1, Hkv, 32, 128, device=dev, dtype=torch.bfloat16)
     v = torch.randn_like(k)
     bt = torch.arange(B * pages, dtype=torch.int32, device=dev).view(B, pages)
-    T = B * S
+    Q = S - P
+    T = B * Q
     q = torch.randn(T, Hq * 128, device=dev, dtype=torch.bfloat16)
     out = torch.empty_like(q)
-    qs = torch.arange(0, T, S, dtype=torch.int32, device=dev)
-    ql = torch.full((B,), S, dtype=torch.int32, device=dev)
+    qs = torch.arange(0, T, Q, dtype=torch.int32, device=dev)
+    ql = torch.full((B,), Q, dtype=torch.int32, device=dev)
     kvl = torch.full((B,), S, dtype=torch.int32, device=dev)
-    nqb = (S + qblk - 1) // qblk
+    nqb = (Q + qblk - 1) // qblk
     ws = torch.arange(B, dtype=torch.int32, device=dev).repeat_interleave(nqb)
     wq = torch.arange(nqb, dtype=torch.int32, device=dev).repeat(B)
     hs = int(os.environ["HSPLIT"]) if "HSPLIT" in os.environ else None
@@ -47,15 +49,16 @@ def run(B, S, Hq, Hkv, iters=10):
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / iters * 1e3
-    flops = B * 2.0 * S * S * 128 * Hq
+    # QK^T + PV over the visible keys: query i sees P + i + 1 of them
+    flops = B * 4.0 * 128 * Hq * (Q * P + Q * (Q + 1) / 2)
     # numerics spot check of the first sequence against an fp32 torch reference
     if B <= 4:
         from replisense_rfq_amd.ops import reference as ref
 
-        exp = torch.zeros(S, Hq * 128, dtype=torch.bfloat16)
-        ref.attn_prefill(q[:S].cpu(), k.cpu(), v.cpu(), bt[:1].cpu(), qs[:1].cpu(), ql[:1].cpu(),
+        exp = torch.zeros(Q, Hq * 128, dtype=torch.bfloat16)
+        ref.attn_prefill(q[:Q].cpu(), k.cpu(), v.cpu(), bt[:1].cpu(), qs[:1].cpu(), ql[:1].cpu(),
                          kvl[:1].cpu(), None, None, exp, Hq, Hkv, 1 / math.sqrt(128))
-        err = float((out[:S].float().cpu() - exp.float()).abs().max())
+        err = float((out[:Q].float().cpu() - exp.float()).abs().max())
         assert err < 0.05, ("prefill numerics", err)
     return us, flops / us / 1e6
 
@@ -66,13 +69,14 @@ SHAPES = [(1, 2048, 32, 8), (4, 2048, 32, 8), (1, 2048, 8, 1), (8, 2048, 8, 1),
 
 def main():
     # SHAPES=BxSxHqxHkv,...  (env) overrides the default list; HSPLIT / KVSPLIT / SMALL
-    # pick the small-grid forms (ops.attn_prefill)
+    # pick the small-grid forms (ops.attn_prefill); PREFIX=P: P cached keys per sequence
     shapes = SHAPES
     if os.environ.get("SHAPES"):
         shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["SHAPES"].split(",")]
+    P = int(os.environ.get("PREFIX", 0))
     for B, S, Hq, Hkv in shapes:
-        us, tf = run(B, S, Hq, Hkv)
-        print(json.dumps({"B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "us": round(us, 1),
+        us, tf = run(B, S, Hq, Hkv, P=P)
+        print(json.dumps({"B": B, "S": S, "prefix": P, "Hq": Hq, "Hkv": Hkv, "us": round(us, 1),
                           "TFLOPs": round(tf, 1), "pct_of_2.5PF": round(tf / 25.0, 1)}),
               flush=True)
 
