@@ -844,6 +844,9 @@ void decode_persist(const Tensor& residual, const Tensor& layers, const Tensor& 
   TORCH_CHECK(counters.numel() >= rfq::decode_persist_counter_words((int)nst),
               "decode_persist: counter buffer too small");
   const int64_t Kx = std::max<int64_t>(Hq * 128, F);
+  TORCH_CHECK(!(flags & 256) || ((flags & 16) && splits > 1 && part_ml.numel() >= 1024),
+              "decode_persist: the timeline stamps (flags bit 8) need the engine form and a "
+              "split partial buffer of >= 1024 floats (they are written there)");
   if (flags & 16) {
     // engine form: M <= 2, a row spans at most 3 ring slots, >= 5 slots fit next to the rows
     int r, p, a, o;
