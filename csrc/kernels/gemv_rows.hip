@@ -119,18 +119,26 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
         __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)(M * ldx * 2), 0x00020000);
     const int voff = lane * 16;
     constexpr int WAUX = NTL ? 2 : 0;
-    int c = 0;
-    for (; c + CU <= nch; c += CU) {
+    // CU chunks per iteration, all of an iteration's loads in flight at once; the last
+    // iteration's chunks past the row are loaded at an out-of-range offset (zeros, no
+    // bytes moved), so a K that is not a multiple of CU chunks costs one more round trip
+    // instead of one per remaining chunk (the serial tail loop it replaces made 8B down,
+    // 28 chunks, pay up to 12 dependent round trips).  Adding the zero products leaves
+    // every sum bit-identical.
+    constexpr int kOob = 0x7ffffff0;
+    for (int c = 0; c < nch; c += CU) {
       u32x4 w[RW][CU], x[MM][CU];
 #pragma unroll
       for (int r = 0; r < RW; ++r)
 #pragma unroll
         for (int u = 0; u < CU; ++u)
-          w[r][u] = bload<WAUX>(wr, voff, (r * rstride * K + (c + u) * 512) * 2);
+          w[r][u] = bload<WAUX>(wr, voff,
+                                c + u < nch ? (r * rstride * K + (c + u) * 512) * 2 : kOob);
 #pragma unroll
       for (int m = 0; m < MM; ++m)
 #pragma unroll
-        for (int u = 0; u < CU; ++u) x[m][u] = bload<0>(xr, voff, (int)(m * ldx + (c + u) * 512) * 2);
+        for (int u = 0; u < CU; ++u)
+          x[m][u] = bload<0>(xr, voff, c + u < nch ? (int)(m * ldx + (c + u) * 512) * 2 : kOob);
 #pragma unroll
       for (int u = 0; u < CU; ++u)
 #pragma unroll
@@ -142,21 +150,6 @@ __global__ __launch_bounds__(kRwWaves * 64) void gemv_rows_kernel(
         for (int u = 0; u < CU; ++u)
 #pragma unroll
           for (int m = 0; m < MM; ++m) ssq[m] = dot8(x[m][u], x[m][u], ssq[m]);
-      }
-    }
-    for (; c < nch; ++c) {                        // tail chunks (K / 512 not a multiple of CU)
-      u32x4 w[RW], x[MM];
-#pragma unroll
-      for (int r = 0; r < RW; ++r) w[r] = bload<WAUX>(wr, voff, (r * rstride * K + c * 512) * 2);
-#pragma unroll
-      for (int m = 0; m < MM; ++m) x[m] = bload<0>(xr, voff, (int)(m * ldx + c * 512) * 2);
-#pragma unroll
-      for (int r = 0; r < RW; ++r)
-#pragma unroll
-        for (int m = 0; m < MM; ++m) acc[r][m] = dot8(w[r], x[m], acc[r][m]);
-      if constexpr (NX) {
-#pragma unroll
-        for (int m = 0; m < MM; ++m) ssq[m] = dot8(x[m], x[m], ssq[m]);
       }
     }
   }

@@ -22,6 +22,7 @@ from replisense_rfq_amd.ops.autotune import _time  # noqa: E402
 SHAPES = {
     "tp8": {"hidden": 8192, "hq": 8, "hkv": 1, "ffn": 3584},
     "8b": {"hidden": 4096, "hq": 32, "hkv": 8, "ffn": 14336},
+    "70b": {"hidden": 8192, "hq": 64, "hkv": 8, "ffn": 28672},     # TP = 1
 }
 ROWS_PLAIN = (4, 8, 12, 5, 9, 2, 6, 3)
 ROWS_PAIRED = (4, 8, 12, 68, 72, 76)
