@@ -193,6 +193,17 @@ def main():
                             run_latency(C, Hq, Hkv, sp, t, L=L, single=True), 2)
                 print(json.dumps(row), flush=True)
         return
+    if os.environ.get("LAT_S32"):
+        # 32 splits (two-kernel merge; the in-kernel merge serves <= 16) vs 16, every shape
+        for Hq, Hkv, L in ((8, 1, 80), (32, 8, 32), (64, 8, 80)):
+            for C in (512, 1024, 2048, 4096):
+                print(json.dumps({"Hq": Hq, "Hkv": Hkv, "ctx": C,
+                                  "s16_t1_reduce_us": round(run_latency(C, Hq, Hkv, 16, 1, L=L), 2),
+                                  "s16_t1_single_us": round(run_latency(C, Hq, Hkv, 16, 1, L=L,
+                                                                        single=True), 2),
+                                  "s32_t1_reduce_us": round(run_latency(C, Hq, Hkv, 32, 1, L=L), 2)}),
+                      flush=True)
+        return
     if os.environ.get("LAT_TP8"):
         # Llama-3-70B TP=8 rank shape (Hq 8, Hkv 1): only splits x 1 kv head waves
         for C in (512, 1024, 2048, 4096):
