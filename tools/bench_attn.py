@@ -167,6 +167,32 @@ def run_latency(C, Hq, Hkv, splits, tiles=2, L=32, reps=20, single=False):
     return best
 
 
+def run_floor(Hq, L=32, reps=20):
+    """The graph's per-launch floor at this latency shape: L dependent one-row elementwise
+    kernels (an add into the [1, Hq*128] output) captured and replayed like run_latency."""
+    dev = torch.device("cuda")
+    out = torch.zeros(1, Hq * 128, device=dev, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        for _ in range(L):
+            out.add_(1)
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(3):
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / (reps * L))
+    return best
+
+
 def main():
     if os.environ.get("LAT"):
         # batch-1 latency path: split count vs context (8B 32/8 heads, 70B 64/8)
@@ -198,6 +224,7 @@ def main():
         for Hq, Hkv, L in ((8, 1, 80), (32, 8, 32), (64, 8, 80)):
             for C in (512, 1024, 2048, 4096):
                 print(json.dumps({"Hq": Hq, "Hkv": Hkv, "ctx": C,
+                                  "graph_floor_us": round(run_floor(Hq, L=L), 2),
                                   "s16_t1_reduce_us": round(run_latency(C, Hq, Hkv, 16, 1, L=L), 2),
                                   "s16_t1_single_us": round(run_latency(C, Hq, Hkv, 16, 1, L=L,
                                                                         single=True), 2),
