@@ -602,6 +602,7 @@ void attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
   const int64_t nw = qblk * (Hq / Hkv) / 32;
   TORCH_CHECK((qblk == 32 || qblk == 64) && (nw == 4 || nw == 8),
               "attn_prefill: qblk * (Hq / Hkv) must be 128 or 256 (4 or 8 waves)");
+  TORCH_CHECK(small_mode >= 0 && small_mode <= 3, "attn_prefill: small_mode must be 0-3");
   float* split_ws = nullptr;
   int32_t* split_tk = nullptr;
   if (ws.has_value() && tickets.has_value()) {

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const int32_t* __restrict__ seq_kv_len, const int32_t* __restrict__ work_seq,
     const int32_t* __restrict__ work_qblk, bf16_t* __restrict__ out, int64_t out_stride, int Hq,
     int Hkv, float scale_log2, int hgroups, int kvsplit = 1, float* __restrict__ ws = nullptr,
-    int32_t* __restrict__ tickets = nullptr, uint64_t* __restrict__ ts = nullptr) {
+    int32_t* __restrict__ tickets = nullptr, uint64_t* __restrict__ ts = nullptr,
+    int bal_work = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // ts (diagnostics, attn_prefill_timing): per workgroup 8 words of s_memrealtime
   // (100 MHz) stamps written by thread 0 -- entry, metadata, first tiles landed, key
@@ -83,9 +84,71 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   const int QB = NW / HPW * kQB;
   // kvsplit = 2: the two workgroups of a (work item, kv head, head group) take the two
   // halves of its key tiles and merge (below); adjacent in the grid, heaviest first
-  const int kvs = blockIdx.x % kvsplit;
-  const int bid = blockIdx.x / kvsplit;
-  const int num_work = gridDim.x / (Hkv * hgroups * kvsplit);
+  //
+  // Balanced form (bal_work = work items <= 128, kvsplit = 4, hgroups = 1, one workgroup
+  // per CU): the grid is an exact task list, not (item, split) slots.  A grid with idle
+  // slots does not help: the dispatcher does not back-fill a CU freed by a workgroup
+  // that leaves at once (r6 phase stamps: the 257th workgroup started after ~24 µs with
+  // 220 of 384 slots active), so here every workgroup derives the same list from the
+  // work items' key-tile counts (two items per lane, wave reductions): tiles per split
+  // = the smallest value >= max(kMinSplitTiles, ceil(tmax / 4)) whose task count fits
+  // the grid, items heaviest first, each item's Hkv x nact tasks contiguous.
+  int kvs, bid, num_work;
+  int split_tiles = kMinSplitTiles;
+  if (bal_work > 0) {
+    num_work = bal_work;
+    auto item_tiles = [&](int w) {
+      const int sq = work_seq[w];
+      const int ql = seq_q_len[sq], kl = seq_kv_len[sq];
+      const int last = min(work_qblk[w] * QB + QB, ql) - 1;
+      return (min(kl, kl - ql + last + 1) + kKT - 1) / kKT;
+    };
+    const int ta = lane < num_work ? item_tiles(lane) : 0;             // item lane
+    const int tb = lane + 64 < num_work ? item_tiles(lane + 64) : 0;   // item lane + 64
+    int tmax = max(ta, tb);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o, 64));
+    tmax = __builtin_amdgcn_readfirstlane(tmax);
+    int tgt = max(kMinSplitTiles, (tmax + kvsplit - 1) / kvsplit);
+    auto nsp = [&](int t) { return t == 0 ? 0 : max(1, min(kvsplit, (t + tgt - 1) / tgt)); };
+    // ends: tgt = tmax gives every item one task, num_work * Hkv <= 128 <= gridDim.x
+    for (;;) {
+      int c = nsp(ta) + nsp(tb);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      c = __builtin_amdgcn_readfirstlane(c) * Hkv;
+      if (c <= (int)gridDim.x || tgt >= tmax) break;
+      ++tgt;
+    }
+    split_tiles = tgt;
+    // heavy first = descending item index: items 64..127 (tb) before 0..63 (ta)
+    const int cb = nsp(tb) * Hkv, ca = nsp(ta) * Hkv;
+    int pb = cb, pa = ca;                                 // inclusive prefix over lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int xb = __shfl_up(pb, o, 64), xa = __shfl_up(pa, o, 64);
+      if (lane >= o) { pb += xb; pa += xa; }
+    }
+    const int totb = __builtin_amdgcn_readfirstlane(__shfl(pb, 63, 64));
+    const int tot = totb + __builtin_amdgcn_readfirstlane(__shfl(pa, 63, 64));
+    const int task = blockIdx.x;
+    if (task >= tot) return;                              // more CUs than tasks
+    const int sb = totb - pb, sa = totb + (tot - totb) - pa;   // tasks before the item
+    const uint64_t mb = __builtin_amdgcn_ballot_w64(cb > 0 && task >= sb && task < sb + cb);
+    const uint64_t ma = __builtin_amdgcn_ballot_w64(ca > 0 && task >= sa && task < sa + ca);
+    const int l = mb ? __builtin_ctzll(mb) : __builtin_ctzll(ma);
+    const int item = mb ? l + 64 : l;
+    const int base = __builtin_amdgcn_readfirstlane(mb ? __shfl(sb, l, 64) : __shfl(sa, l, 64));
+    const int ns = nsp(__builtin_amdgcn_readfirstlane(mb ? __shfl(tb, l, 64)
+                                                         : __shfl(ta, l, 64)));
+    const int r = task - base;
+    kvs = r % ns;
+    bid = (num_work - 1 - item) * Hkv + r / ns;
+  } else {
+    kvs = blockIdx.x % kvsplit;
+    bid = blockIdx.x / kvsplit;
+    num_work = gridDim.x / (Hkv * hgroups * kvsplit);
+  }
   const int kvh = bid % Hkv;
   const int hg = (bid / Hkv) % hgroups;
   const int wi = num_work - 1 - bid / (Hkv * hgroups);
@@ -115,7 +178,9 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
   // key tiles [t0, t1) of this workgroup: an item's tiles go to nact <= kvsplit
   // workgroups of >= kMinSplitTiles tiles each; the others leave at once, and an
   // unsplit item's first workgroup writes the output directly
-  const int nact = max(1, min(kvsplit, ntiles / kMinSplitTiles));
+  const int nact = bal_work > 0
+                       ? max(1, min(kvsplit, (ntiles + split_tiles - 1) / split_tiles))
+                       : max(1, min(kvsplit, ntiles / kMinSplitTiles));
   if (kvs >= nact) return;
   const bool split = nact > 1;
   const int t0 = kvs * ntiles / nact;
@@ -549,6 +614,23 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
   // B1 S2048 (64 items) 32.8 -> 31.0 us kernel time (profiles/r4_prefill_small_grid.md).
   const int wg0 = num_work * Hkv;
   const bool small = nw == 8 && wg0 < hsplit_below && ws != nullptr && tickets != nullptr;
+  // small_mode 3 (balanced split-KV): the 8-wave form over an exact task list of up to 4
+  // splits per item, one workgroup per CU (attn_prefill_kernel bal_work; <= 128 items).
+  // Auto takes it for 65-128 items (it replaced the uniform 2-way split there, r6 rank
+  // shape Hq 8 / Hkv 1: S 2,912 with a 416-key prefix 57.5 -> 46.3 µs, S 4,096 75 -> 65 µs,
+  // B2 S2048 45 -> 41 µs, profiles/r6_prefill_balanced.md); at <= 64 items the uniform
+  // 4-way split is faster (the task list costs 2-4 µs of metadata before the first tile).
+  const bool bal = small && wg0 * 2 <= kPrefillSplitMaxWg &&
+                   (small_mode == 3 || (small_mode == 0 && wg0 * 4 > kPrefillSplitMaxWg));
+  if (bal) {
+    const dim3 grid8(kPrefillSplitMaxWg);
+    attn_prefill_kernel<8><<<grid8, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
+                                                   bt_stride, seq_q_start, seq_q_len, seq_kv_len,
+                                                   work_seq, work_qblk, out, out_stride, Hq, Hkv,
+                                                   scale_log2, 1, kMaxKvSplit, ws, tickets,
+                                                   g_prefill_ts, num_work);
+    return;
+  }
   const bool kv8 = small && (small_mode == 2 ||
                              (small_mode == 0 && wg0 * 4 >= kPrefillSplitMaxWg &&
                               wg0 * 2 <= kPrefillSplitMaxWg));

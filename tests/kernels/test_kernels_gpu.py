@@ -223,6 +223,37 @@ def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
     torch.testing.assert_close(out2[:T - 1], out[:T - 1], rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("q_len,kv_len", [(2496, 2912), (2048, 2048), (700, 3000)])
+def test_attn_prefill_balanced_split(gpu, q_len, kv_len):
+    """The TP=8 rank shape (Hq 8 / Hkv 1) of one long prompt, with and without a cached
+    prefix: the auto small-grid form and the balanced split-KV form (small_mode 3: up to
+    4 splits per item, fewer for the light ones) against the fp32 reference; each form
+    runs twice (tickets reset) and the tickets end at zero."""
+    torch.manual_seed(11)
+    Hq, Hkv, qblk = 8, 1, 32
+    pages = (kv_len + 31) // 32
+    k, v = _paged_cache(pages + 8, Hkv, gpu, seed=12)
+    bt = _block_tables([kv_len], pages + 8, gpu, seed=13)
+    q = torch.randn(q_len, Hq * 128, device=gpu, dtype=BF)
+    nqb = (q_len + qblk - 1) // qblk
+    i32 = dict(dtype=torch.int32, device=gpu)
+    qs, ql, kvl = (torch.tensor([x], **i32) for x in (0, q_len, kv_len))
+    ws, wq = torch.zeros(nqb, **i32), torch.arange(nqb, **i32)
+    scale = 1 / math.sqrt(128)
+    exp = torch.zeros(q_len, Hq * 128, dtype=BF)
+    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), qs.cpu(), ql.cpu(), kvl.cpu(), None,
+                     None, exp, Hq, Hkv, scale)
+    out = torch.zeros(q_len, Hq * 128, device=gpu, dtype=BF)
+    for sm in (0, 3, 3, 2):
+        out.zero_()
+        ops.attn_prefill(q, k, v, bt, qs, ql, kvl, ws, wq, out, Hq, Hkv, scale, qblk,
+                         hsplit_below=4096, kvsplit=True, small_mode=sm)
+        _close(out, exp, 2e-2, 0, f"attn_prefill balanced q={q_len} kv={kv_len} mode={sm}")
+    if ops.native_available():
+        torch.cuda.synchronize()
+        assert int(ops.prefill_split_ws(gpu)[1].abs().sum()) == 0, "split tickets not reset"
+
+
 @pytest.mark.parametrize("Hq,Hkv,qblk,spike", [(32, 8, 32, False), (32, 8, 64, False),
                                                (8, 1, 32, False), (64, 8, 32, False),
                                                (32, 8, 64, True)])
@@ -256,9 +287,11 @@ def test_attn_prefill(gpu, Hq, Hkv, qblk, spike):
     # 4-wave workgroups (the small-grid form)
     # kvsplit: the head-split form's items of >= 4 key tiles split over two workgroups
     # (merged in-kernel; run twice, so the tickets must have been reset); small_mode 2:
-    # the 8-wave form with the key tiles split 2-4 ways (8-wave shapes only)
+    # the 8-wave form with the key tiles split 2-4 ways (8-wave shapes only); small_mode 3:
+    # the 8-wave form with a per-item split count from the work list (balanced)
     for hs, kvs, sm in ((0, False, 0), (4096, False, 1), (4096, True, 1), (4096, True, 1),
-                        (4096, True, 2), (4096, True, 2), (4096, True, 0)):
+                        (4096, True, 2), (4096, True, 2), (4096, True, 0), (4096, True, 3),
+                        (4096, True, 3)):
         out.zero_()
         ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out,
                          Hq, Hkv, scale, qblk, hsplit_below=hs, kvsplit=kvs, small_mode=sm)
