@@ -223,14 +223,17 @@ def test_attn_decode_shared_prefix(gpu, Hq, Hkv, tiles, share):
     torch.testing.assert_close(out2[:T - 1], out[:T - 1], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("q_len,kv_len", [(2496, 2912), (2048, 2048), (700, 3000)])
-def test_attn_prefill_balanced_split(gpu, q_len, kv_len):
-    """The TP=8 rank shape (Hq 8 / Hkv 1) of one long prompt, with and without a cached
-    prefix: the auto small-grid form and the balanced split-KV form (small_mode 3: up to
-    4 splits per item, fewer for the light ones) against the fp32 reference; each form
-    runs twice (tickets reset) and the tickets end at zero."""
+@pytest.mark.parametrize("Hq,Hkv,q_len,kv_len", [(8, 1, 2496, 2912), (8, 1, 2048, 2048),
+                                                 (8, 1, 700, 3000), (64, 8, 400, 800),
+                                                 (64, 8, 512, 512)])
+def test_attn_prefill_balanced_split(gpu, Hq, Hkv, q_len, kv_len):
+    """One long prompt at the TP=8 rank shape (Hq 8 / Hkv 1) and a short one at 70B TP=1
+    (64 / 8: 13-16 items x 8 kv heads), with and without a cached prefix: the auto
+    small-grid form and the balanced split-KV form (small_mode 3: up to 4 splits per
+    item, fewer for the light ones) against the fp32 reference; each form runs twice
+    (tickets reset) and the tickets end at zero."""
     torch.manual_seed(11)
-    Hq, Hkv, qblk = 8, 1, 32
+    qblk = 32
     pages = (kv_len + 31) // 32
     k, v = _paged_cache(pages + 8, Hkv, gpu, seed=12)
     bt = _block_tables([kv_len], pages + 8, gpu, seed=13)
