@@ -619,9 +619,11 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
   // Auto takes it for 65-128 items (it replaced the uniform 2-way split there, r6 rank
   // shape Hq 8 / Hkv 1: S 2,912 with a 416-key prefix 57.5 -> 46.3 µs, S 4,096 75 -> 65 µs,
   // B2 S2048 45 -> 41 µs, profiles/r6_prefill_balanced.md); at <= 64 items the uniform
-  // 4-way split is faster (the task list costs 2-4 µs of metadata before the first tile).
+  // 4-way split is faster (the task list costs 2-4 µs of metadata before the first tile),
+  // and so is the 2-way split for few, short items over several kv heads (70B TP=1, 8 kv
+  // heads x 10-16 items: 21-30 µs vs 24-35 µs balanced), hence the rule on items.
   const bool bal = small && wg0 * 2 <= kPrefillSplitMaxWg &&
-                   (small_mode == 3 || (small_mode == 0 && wg0 * 4 > kPrefillSplitMaxWg));
+                   (small_mode == 3 || (small_mode == 0 && num_work * 4 > kPrefillSplitMaxWg));
   if (bal) {
     const dim3 grid8(kPrefillSplitMaxWg);
     attn_prefill_kernel<8><<<grid8, 512, lds, s>>>(q, q_stride, k_cache, v_cache, block_tables,
