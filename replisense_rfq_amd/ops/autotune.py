@@ -514,7 +514,10 @@ def tune_split(groups: dict[str, list[torch.Tensor]], max_m: dict[str, int], qua
                 if act is not None:
                     t_silu = _time(lambda w_, m=m: silu_mul(out[:m], act[:m]), [w], reps,
                                    graph=False)
-                    t_ref = min(t_lib, t_best) + t_silu
+                    # the plain GEMM the reference pays: the hand-written kernel only
+                    # where it won above (t_best is t_lib * margin where it did not --
+                    # using that would apply the margin twice)
+                    t_ref = (t_best if best_c >= 0 else t_lib) + t_silu
                     bs, ts = -1, t_ref * DENSE_MARGIN
                     for c in DENSE_CFGS:
                         if skip(c, m):
