@@ -257,6 +257,43 @@ def test_attn_prefill_balanced_split(gpu, Hq, Hkv, q_len, kv_len):
         assert int(ops.prefill_split_ws(gpu)[1].abs().sum()) == 0, "split tickets not reset"
 
 
+def test_attn_prefill_balanced_multi_sequence(gpu):
+    """A chunked-prefill step at the rank shape with several prompts (fresh, prefix hit,
+    chunk continuation, 1-token extend): 100 work items, so auto takes the balanced task
+    list over a work list that is not one causal ramp."""
+    torch.manual_seed(21)
+    Hq, Hkv, qblk = 8, 1, 32
+    cases = [(800, 800), (640, 1056), (1, 300), (900, 1700), (831, 2000)]
+    qlens = [c[0] for c in cases]
+    kvlens = [c[1] for c in cases]
+    nblocks = sum((l + 31) // 32 for l in kvlens) + 16
+    k, v = _paged_cache(nblocks, Hkv, gpu, seed=22)
+    bt = _block_tables(kvlens, nblocks, gpu, seed=23)
+    T = sum(qlens)
+    starts = torch.tensor([sum(qlens[:i]) for i in range(len(qlens))], dtype=torch.int32)
+    q = torch.randn(T, Hq * 128, device=gpu, dtype=BF)
+    ws, wq = [], []
+    for s_, ql in enumerate(qlens):
+        for j in range((ql + qblk - 1) // qblk):
+            ws.append(s_)
+            wq.append(j)
+    assert 64 < len(ws) <= 128
+    args = [torch.tensor(a, dtype=torch.int32, device=gpu) for a in (qlens, kvlens, ws, wq)]
+    scale = 1 / math.sqrt(128)
+    exp = torch.zeros(T, Hq * 128, dtype=BF)
+    ref.attn_prefill(q.cpu(), k.cpu(), v.cpu(), bt.cpu(), starts, args[0].cpu(), args[1].cpu(),
+                     None, None, exp, Hq, Hkv, scale)
+    out = torch.zeros(T, Hq * 128, device=gpu, dtype=BF)
+    for sm in (0, 0, 2):
+        out.zero_()
+        ops.attn_prefill(q, k, v, bt, starts.to(gpu), args[0], args[1], args[2], args[3], out,
+                         Hq, Hkv, scale, qblk, hsplit_below=4096, kvsplit=True, small_mode=sm)
+        _close(out, exp, 2e-2, 0, f"attn_prefill multi-sequence mode={sm}")
+    if ops.native_available():
+        torch.cuda.synchronize()
+        assert int(ops.prefill_split_ws(gpu)[1].abs().sum()) == 0, "split tickets not reset"
+
+
 @pytest.mark.parametrize("Hq,Hkv,qblk,spike", [(32, 8, 32, False), (32, 8, 64, False),
                                                (8, 1, 32, False), (64, 8, 32, False),
                                                (32, 8, 64, True)])
