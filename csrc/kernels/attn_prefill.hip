@@ -133,7 +133,7 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const int tot = totb + __builtin_amdgcn_readfirstlane(__shfl(pa, 63, 64));
     const int task = blockIdx.x;
     if (task >= tot) return;                              // more CUs than tasks
-    const int sb = totb - pb, sa = totb + (tot - totb) - pa;   // tasks before the item
+    const int sb = totb - pb, sa = tot - pa;              // tasks before the item
     const uint64_t mb = __builtin_amdgcn_ballot_w64(cb > 0 && task >= sb && task < sb + cb);
     const uint64_t ma = __builtin_amdgcn_ballot_w64(ca > 0 && task >= sa && task < sa + ca);
     const int l = mb ? __builtin_ctzll(mb) : __builtin_ctzll(ma);
@@ -141,9 +141,9 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(
     const int base = __builtin_amdgcn_readfirstlane(mb ? __shfl(sb, l, 64) : __shfl(sa, l, 64));
     const int ns = nsp(__builtin_amdgcn_readfirstlane(mb ? __shfl(tb, l, 64)
                                                          : __shfl(ta, l, 64)));
-    const int r = task - base;
-    kvs = r % ns;
-    bid = (num_work - 1 - item) * Hkv + r / ns;
+    const int rank_in_item = task - base;                 // kv head major, split minor
+    kvs = rank_in_item % ns;
+    bid = (num_work - 1 - item) * Hkv + rank_in_item / ns;
   } else {
     kvs = blockIdx.x % kvsplit;
     bid = blockIdx.x / kvsplit;
@@ -617,7 +617,7 @@ void launch_attn_prefill(const bf16_t* q, int64_t q_stride, const bf16_t* k_cach
   // small_mode 3 (balanced split-KV): the 8-wave form over an exact task list of up to 4
   // splits per item, one workgroup per CU (attn_prefill_kernel bal_work; <= 128 items).
   // Auto takes it for 65-128 items (it replaced the uniform 2-way split there, r6 rank
-  // shape Hq 8 / Hkv 1: S 2,912 with a 416-key prefix 57.5 -> 46.3 µs, S 4,096 75 -> 65 µs,
+  // shape Hq 8 / Hkv 1: S 2,912 with a 416-key prefix 57.5 -> 44.0 µs, S 4,096 75 -> 63 µs,
   // B2 S2048 45 -> 41 µs, profiles/r6_prefill_balanced.md); at <= 64 items the uniform
   // 4-way split is faster (the task list costs 2-4 µs of metadata before the first tile),
   // and so is the 2-way split for few, short items over several kv heads (70B TP=1, 8 kv
